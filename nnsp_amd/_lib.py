@@ -1,0 +1,198 @@
+"""ctypes view of libnnsp_mi355x.so (the C-ABI of include/nnsp_api.h and
+include/nnsp_batch.h).
+
+The library is built in-tree (``nnsp_amd/libnnsp_mi355x.so``, see
+``__graft_entry__.build``).  Loading fails loudly when it is missing: there is
+no CPU fallback anywhere in the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libnnsp_mi355x.so")
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(no CPU fallback exists)")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+class NeuralNetClass(C.Structure):
+    """ABI mirror of NeuralNetClass (reference neural_nets.h:15-32)."""
+    _fields_ = [
+        ("numlayers", C.c_int8),
+        ("size_layer", C.c_int16 * 11),
+        ("net_layer_type", C.c_int * 10),
+        ("qbit_kernel", C.c_int8 * 10),
+        ("qbit_input", C.c_int8 * 10),
+        ("qbit_bias", C.c_int8 * 10),
+        ("activation_type", C.c_int * 10),
+        ("pt_cstate", C.c_void_p * 10),
+        ("pt_hstate", C.c_void_p * 10),
+        ("act_func", C.c_void_p * 10),
+        ("layer_func", C.c_void_p * 10),
+        ("pt_kernel", C.c_void_p * 10),
+        ("pt_bias", C.c_void_p * 10),
+        ("pt_kernel_rec", C.c_void_p * 10),
+    ]
+
+
+class stftModule(C.Structure):
+    _fields_ = [("len_win", C.c_int16), ("hop", C.c_int16), ("len_fft", C.c_int16),
+                ("dataBuffer", C.c_int16 * 512), ("window", C.c_void_p)]
+
+
+class FeatureClass(C.Structure):
+    _fields_ = [("state_stftModule", stftModule), ("feature", C.c_int32 * 50),
+                ("normFeatContext", C.c_int16 * 300), ("num_context", C.c_int16),
+                ("dim_feat", C.c_int16), ("pt_norm_mean", C.c_void_p),
+                ("pt_norm_stdR", C.c_void_p), ("qbit_output", C.c_int8)]
+
+
+class NNSPClass(C.Structure):
+    _fields_ = [("nn_id", C.c_char), ("pt_net", C.c_void_p), ("pt_feat", C.c_void_p),
+                ("slides", C.c_int8), ("trigger", C.c_int16), ("pt_thresh_prob", C.c_void_p),
+                ("counts_category", C.c_int16 * 8), ("pt_th_count_trigger", C.c_void_p),
+                ("num_dnsmpl", C.c_int16), ("outputs", C.c_int16 * 3), ("argmax_last", C.c_int16)]
+
+
+class PostState(C.Structure):
+    _fields_ = [("slides", C.c_int16), ("trigger", C.c_int16), ("argmax_last", C.c_int16),
+                ("pad0", C.c_int16), ("counts_category", C.c_int16 * 8),
+                ("outputs", C.c_int16 * 3), ("pad1", C.c_int16)]
+
+
+P = C.c_void_p
+I = C.c_int
+
+
+def _declare(L: C.CDLL) -> None:
+    sig = {
+        "nnsp_batch_create": (I, [C.POINTER(P), P, I, P, P, C.c_int16, C.c_int16, I, I]),
+        "nnsp_batch_destroy": (None, [P]),
+        "nnsp_batch_reset": (I, [P, P]),
+        "nnsp_batch_exec": (I, [P, P, I, P, P, P]),
+        "nnsp_batch_exec_device": (I, [P, P, I, P, P]),
+        "nnsp_batch_sync": (I, [P]),
+        "nnsp_batch_stream": (P, [P]),
+        "nnsp_batch_streams": (I, [P]),
+        "nnsp_batch_nout": (I, [P]),
+        "nnsp_batch_features_device": (P, [P]),
+        "nnsp_batch_last_timing": (I, [P, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+        "nnsp_batch_post_state": (I, [P, P]),
+        "nnsp_batch_state_bytes": (C.c_size_t, [P]),
+        "nnsp_batch_get_state": (I, [P, P, I, I]),
+        "nnsp_batch_set_state": (I, [P, P, I, I]),
+        "nnsp_synth_pcm": (I, [P, I, I, C.c_uint64, I, C.c_int64, I, P]),
+        "nnsp_device_count": (I, [C.POINTER(I)]),
+        "nnsp_set_device": (I, [I]),
+        "nnsp_device_info": (I, [C.POINTER(I), C.POINTER(I), C.c_char_p, I]),
+        "nnsp_strerror": (C.c_char_p, [I]),
+        "NNSPClass_init": (I, [P, P, P, C.c_char, P, P, P, P]),
+        "NNSPClass_reset": (I, [P]),
+        "NNSPClass_exec": (C.c_int16, [P, P]),
+        "NeuralNetClass_exe": (None, [P, P, P, C.c_int8]),
+        "NeuralNetClass_setDefault": (None, [P]),
+        "FeatureClass_construct": (None, [P, P, P, C.c_int8]),
+        "FeatureClass_setDefault": (None, [P]),
+        "FeatureClass_execute": (None, [P, P]),
+        "arm_fft_exec": (None, [P, P]),
+        "spec2pspec_arm": (None, [P, P, I]),
+        "melSpecProc": (None, [P, P]),
+        "log10_vec": (None, [P, P, C.c_int32, C.c_int16]),
+        "my_log10": (None, [P, C.c_int32]),
+        "norm_oneTwo": (None, [C.c_int32, P, P]),
+        "compute_pwr2": (C.c_int32, [C.c_int32]),
+        "ceiling": (C.c_int32, [C.c_int32]),
+        "my_argmax": (None, [P, I, P]),
+        "binary_post_proc": (None, [P, P, P]),
+        "s2i_post_proc": (None, [P, P, P]),
+        "tanh_fix": (P, [P, P, I]),
+        "sigmoid_fix": (P, [P, P, I]),
+        "relu6_fix": (P, [P, P, I]),
+        "linear_fix": (P, [P, P, I]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def check(code: int, what: str = "") -> None:
+    if code != 0:
+        msg = lib().nnsp_strerror(code)
+        raise RuntimeError(f"{what}: libnnsp_mi355x error {code}: {msg.decode() if msg else ''}")
+
+
+def fn_addr(name: str) -> int:
+    return C.cast(getattr(lib(), name), C.c_void_p).value
+
+
+def ptr(a: np.ndarray | None) -> int | None:
+    return None if a is None else a.ctypes.data
+
+
+class NetHandle:
+    """A NeuralNetClass built from nnsp_amd.nets.NetData, holding every buffer
+    it points to (packed weights exactly as a def_nn*.c file holds them)."""
+
+    def __init__(self, data, acc32: bool = False):
+        from .nets import LSTM, LINEAR
+        spec = data.spec
+        Wp, Wrp, Bp = data.packed()
+        self.data = data
+        self.keep = []
+        n = NeuralNetClass()
+        n.numlayers = spec.nl
+        for i, s in enumerate(spec.sizes):
+            n.size_layer[i] = s
+        names = {0: "relu6_fix", 1: "tanh_fix", 2: "sigmoid_fix", 3: "linear_fix"}
+        self.h, self.c = [None] * spec.nl, [None] * spec.nl
+        for i, t in enumerate(spec.types):
+            n.net_layer_type[i] = t
+            n.qbit_kernel[i] = spec.qk[i]
+            n.qbit_input[i] = spec.qi[i]
+            n.qbit_bias[i] = spec.qb[i]
+            n.activation_type[i] = {0: 0, 1: 1, 2: 2, 3: 3}[spec.acts[i]]
+            n.act_func[i] = fn_addr(names[spec.acts[i]])
+            if t == LSTM:
+                lf = "lstm_8x16_acc32b" if acc32 else "lstm_8x16"
+                N = spec.sizes[i + 1]
+                self.h[i] = np.zeros(N, np.int16)
+                self.c[i] = np.zeros(N, np.int32)
+                n.pt_hstate[i] = ptr(self.h[i])
+                n.pt_cstate[i] = ptr(self.c[i])
+            else:
+                lf = "fc_8x16_acc32b" if acc32 else "fc_8x16"
+            n.layer_func[i] = fn_addr(lf)
+            w = np.ascontiguousarray(Wp[i]).view(np.int8)
+            b = np.ascontiguousarray(Bp[i]).astype(np.int16)
+            self.keep += [w, b]
+            n.pt_kernel[i] = ptr(w)
+            n.pt_bias[i] = ptr(b)
+            if Wrp[i] is not None:
+                wr = np.ascontiguousarray(Wrp[i]).view(np.int8)
+                self.keep.append(wr)
+                n.pt_kernel_rec[i] = ptr(wr)
+        self.net = n
+        self.mean = np.ascontiguousarray(data.mean, np.int32)
+        self.stdR = np.ascontiguousarray(data.stdR, np.int32)
+        del LINEAR
+
+    @property
+    def addr(self) -> int:
+        return C.addressof(self.net)

@@ -1,0 +1,266 @@
+/*
+ * nnsp_batch.c -- the batched multi-stream engine (include/nnsp_batch.h).
+ *
+ * Device state per stream (everything NNSPClass_exec carries between frames):
+ *   tail  [320] int16   stftModule.dataBuffer[160..479] (spectrogram_module.c:103-108)
+ *   prev5 [5][40] int16 normFeatContext slots 1..5     (feature_module.c:54-57)
+ *   h/c   [n_lstm][128]  LSTM state                     (def_nn*.c pt_hstate/pt_cstate)
+ *   post  32 B           slides, trigger, counts, outputs, argmax_last (nn_speech.h:12-25)
+ * A chunk of T frames runs as: fe_kernel (all S*T frames in parallel) ->
+ * nn_kernel (per 16-stream tile, the chunk's NN steps in order) -> roll of the
+ * feature context and the PCM tail.
+ */
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../../include/nnsp_batch.h"
+#include "nnsp_host.h"
+
+struct nnsp_batch {
+    int S, Tmax, nout, out_linear, norm_shift;
+    nnsp_image im;
+    void *stream;
+    void *ev[3];
+    int32_t *d_mean, *d_stdR;
+    int16_t *d_tail, *d_prev5, *d_h;
+    int32_t *d_c;
+    NnPost *d_post;
+    int16_t *d_feats, *d_pcm, *d_trig;
+    int32_t *d_logits;
+    uint8_t *d_mask;
+    int last_T;
+};
+
+#define TRY(x)                 \
+    do {                       \
+        int _e = (x);          \
+        if (_e) return _e;     \
+    } while (0)
+
+int nnsp_device_count(int *n) { return nnspk_device_count(n); }
+int nnsp_set_device(int dev) { return nnspk_set_device(dev); }
+int nnsp_device_info(int *cu, int *clk, char *arch, int len) { return nnspk_device_info(cu, clk, arch, len); }
+
+const char *nnsp_strerror(int code)
+{
+    if (code == 0) return "ok";
+    if (code < 0) return nnsp_last_error()[0] ? nnsp_last_error() : "invalid argument";
+    return nnspk_error_string(code);
+}
+
+int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, const int32_t *mean,
+                      const int32_t *stdR, int16_t thresh_prob, int16_t th_count, int n_streams,
+                      int max_frames)
+{
+    *out = NULL;
+    if (!net || !mean || !stdR || n_streams <= 0 || max_frames <= 0) {
+        nnsp_set_error("nnsp_batch_create: bad argument");
+        return NNSP_EINVAL;
+    }
+    if (net->size_layer[0] != NUM_FEATURE_CONTEXT * DIMEMSION_FEATURE) {
+        nnsp_set_error("net input width %d != 240 (6 x 40 context)", net->size_layer[0]);
+        return NNSP_EINVAL;
+    }
+    nnsp_layer_desc L[NN_MAX_LAYERS];
+    int nl = 0, out_linear = 0;
+    TRY(nnsp_describe_net(net, L, &nl, &out_linear));
+    nnsp_batch *b = (nnsp_batch *)calloc(1, sizeof *b);
+    if (!b) return NNSP_ENOMEM;
+    *out = b;
+    b->S = n_streams;
+    b->Tmax = max_frames;
+    b->out_linear = out_linear;
+    b->norm_shift = 30 - net->qbit_input[0]; /* FeatureClass qbit_output, nn_speech.c:40-44 */
+    int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count);
+    if (e) goto fail;
+    b->nout = b->im.img.nout;
+    if ((e = nnspk_stream_create(&b->stream))) goto fail;
+    for (int i = 0; i < 3; ++i)
+        if ((e = nnspk_event_create(&b->ev[i]))) goto fail;
+    if ((e = nnsp_image_upload(&b->im, b->stream))) goto fail;
+    const size_t S = (size_t)n_streams, T = (size_t)max_frames;
+    const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
+    if ((e = nnspk_malloc((void **)&b->d_mean, 40 * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_stdR, 40 * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_tail, S * 320 * 2))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_prev5, S * 200 * 2))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_h, S * nls * NN_MAX_W * 2))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_c, S * nls * NN_MAX_W * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_post, S * sizeof(NnPost)))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_feats, S * T * 40 * 2))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_mask, S))) goto fail;
+    if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
+    if ((e = nnspk_h2d(b->d_stdR, stdR, 40 * 4, b->stream))) goto fail;
+    if ((e = nnspk_memset(b->d_prev5, 0, S * 200 * 2, b->stream))) goto fail;
+    if ((e = nnspk_memset(b->d_post, 0, S * sizeof(NnPost), b->stream))) goto fail;
+    if ((e = nnsp_batch_reset(b, NULL))) goto fail;
+    return 0;
+fail:
+    nnsp_batch_destroy(b);
+    *out = NULL;
+    return e;
+}
+
+void nnsp_batch_destroy(nnsp_batch *b)
+{
+    if (!b) return;
+    if (b->stream) nnspk_sync(b->stream);
+    nnsp_image_free(&b->im);
+    void *bufs[] = {b->d_mean, b->d_stdR, b->d_tail, b->d_prev5, b->d_h, b->d_c, b->d_post,
+                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask};
+    for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
+    for (int i = 0; i < 3; ++i) nnspk_event_destroy(b->ev[i]);
+    nnspk_stream_destroy(b->stream);
+    free(b);
+}
+
+int nnsp_batch_reset(nnsp_batch *b, const uint8_t *mask)
+{
+    if (!b) return NNSP_EINVAL;
+    const uint8_t *dm = NULL;
+    if (mask) {
+        TRY(nnspk_h2d(b->d_mask, mask, (size_t)b->S, b->stream));
+        dm = b->d_mask;
+    }
+    /* FeatureClass_setDefault + NeuralNetClass_setDefault + NNSPClass fields */
+    TRY(nnspk_launch_fe_default(b->d_prev5, b->d_tail, b->d_mean, b->d_stdR, b->norm_shift, dm, b->S,
+                                b->stream));
+    TRY(nnspk_launch_nn_default(b->d_h, b->d_c, b->d_post, b->im.img.n_lstm ? b->im.img.n_lstm : 1,
+                                dm, b->S, b->stream));
+    return nnspk_sync(b->stream);
+}
+
+static int ensure(void **p, size_t bytes)
+{
+    if (*p) return 0;
+    return nnspk_malloc(p, bytes);
+}
+
+int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits)
+{
+    if (!b || !pcm || T <= 0 || T > b->Tmax) {
+        nnsp_set_error("nnsp_batch_exec: T must be in 1..%d", b ? b->Tmax : 0);
+        return NNSP_EINVAL;
+    }
+    FeArgs fa;
+    memset(&fa, 0, sizeof fa);
+    fa.pcm = pcm;
+    fa.tail = b->d_tail;
+    fa.S = b->S;
+    fa.T = T;
+    fa.mean = b->d_mean;
+    fa.stdR = b->d_stdR;
+    fa.norm_shift = b->norm_shift;
+    fa.feats = b->d_feats;
+    TRY(nnspk_event_record(b->ev[0], b->stream));
+    TRY(nnspk_launch_fe(&fa, b->stream));
+    TRY(nnspk_event_record(b->ev[1], b->stream));
+    NnRun r;
+    memset(&r, 0, sizeof r);
+    r.S = b->S;
+    r.T = T;
+    r.mode = NN_MODE_STREAM;
+    r.nl_run = b->im.img.nl;
+    r.feats = b->d_feats;
+    r.prev5 = b->d_prev5;
+    r.h = b->d_h;
+    r.c = b->d_c;
+    r.post = b->d_post;
+    r.trig = trig;
+    r.logits = logits;
+    TRY(nnspk_launch_nn(&b->im.img, &r, b->stream));
+    TRY(nnspk_event_record(b->ev[2], b->stream));
+    /* carry the context (slots 1..5) and the PCM tail (last 320 samples) */
+    TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, b->stream));
+    TRY(nnspk_launch_tail_roll(b->d_tail, pcm, b->S, T, b->stream));
+    b->last_T = T;
+    return 0;
+}
+
+int nnsp_batch_exec(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
+                    int16_t *features)
+{
+    if (!b || !pcm || T <= 0 || T > b->Tmax) return NNSP_EINVAL;
+    const size_t S = (size_t)b->S;
+    TRY(ensure((void **)&b->d_pcm, S * b->Tmax * 160 * 2));
+    TRY(ensure((void **)&b->d_trig, S * b->Tmax * 2));
+    if (logits) TRY(ensure((void **)&b->d_logits, S * b->Tmax * b->nout * 4));
+    TRY(nnspk_h2d(b->d_pcm, pcm, S * T * 160 * 2, b->stream));
+    TRY(nnsp_batch_exec_device(b, b->d_pcm, T, b->d_trig, logits ? b->d_logits : NULL));
+    if (trig) TRY(nnspk_d2h(trig, b->d_trig, S * T * 2, b->stream));
+    if (logits) TRY(nnspk_d2h(logits, b->d_logits, S * T * b->nout * 4, b->stream));
+    if (features) TRY(nnspk_d2h(features, b->d_feats, S * T * 40 * 2, b->stream));
+    return nnspk_sync(b->stream);
+}
+
+int nnsp_batch_sync(nnsp_batch *b) { return b ? nnspk_sync(b->stream) : NNSP_EINVAL; }
+void *nnsp_batch_stream(nnsp_batch *b) { return b ? b->stream : NULL; }
+int nnsp_batch_streams(const nnsp_batch *b) { return b ? b->S : 0; }
+int nnsp_batch_nout(const nnsp_batch *b) { return b ? b->nout : 0; }
+const int16_t *nnsp_batch_features_device(const nnsp_batch *b) { return b ? b->d_feats : NULL; }
+
+int nnsp_batch_last_timing(nnsp_batch *b, float *fe_ms, float *nn_ms)
+{
+    if (!b) return NNSP_EINVAL;
+    TRY(nnspk_sync(b->stream));
+    TRY(nnspk_event_elapsed(fe_ms, b->ev[0], b->ev[1]));
+    TRY(nnspk_event_elapsed(nn_ms, b->ev[1], b->ev[2]));
+    return 0;
+}
+
+int nnsp_batch_post_state(nnsp_batch *b, nnsp_post_state *out)
+{
+    if (!b || !out) return NNSP_EINVAL;
+    TRY(nnspk_d2h(out, b->d_post, (size_t)b->S * sizeof(NnPost), b->stream));
+    return nnspk_sync(b->stream);
+}
+
+/* per-stream state blob: tail | prev5 | h | c | post */
+size_t nnsp_batch_state_bytes(const nnsp_batch *b)
+{
+    const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
+    return 320 * 2 + 200 * 2 + (size_t)nls * NN_MAX_W * 6 + sizeof(NnPost);
+}
+
+static int state_xfer(nnsp_batch *b, void *host, int first, int count, int to_dev)
+{
+    if (!b || !host || first < 0 || count < 0 || first + count > b->S) return NNSP_EINVAL;
+    const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
+    const size_t per = nnsp_batch_state_bytes(b);
+    uint8_t *h = (uint8_t *)host;
+    for (int i = 0; i < count; ++i) {
+        const size_t s = (size_t)(first + i);
+        uint8_t *p = h + per * i;
+        struct { void *dev; size_t n; } seg[5] = {
+            {b->d_tail + s * 320, 640},
+            {b->d_prev5 + s * 200, 400},
+            {b->d_h + s * nls * NN_MAX_W, (size_t)nls * NN_MAX_W * 2},
+            {b->d_c + s * nls * NN_MAX_W, (size_t)nls * NN_MAX_W * 4},
+            {b->d_post + s, sizeof(NnPost)},
+        };
+        for (int k = 0; k < 5; ++k) {
+            if (to_dev)
+                TRY(nnspk_h2d(seg[k].dev, p, seg[k].n, b->stream));
+            else
+                TRY(nnspk_d2h(p, seg[k].dev, seg[k].n, b->stream));
+            p += seg[k].n;
+        }
+    }
+    return nnspk_sync(b->stream);
+}
+
+int nnsp_batch_get_state(nnsp_batch *b, void *host, int first, int count)
+{
+    return state_xfer(b, host, first, count, 0);
+}
+
+int nnsp_batch_set_state(nnsp_batch *b, const void *host, int first, int count)
+{
+    return state_xfer(b, (void *)host, first, count, 1);
+}
+
+int nnsp_synth_pcm(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp, void *stream)
+{
+    if (!dev_out || S <= 0 || T <= 0 || amp <= 0) return NNSP_EINVAL;
+    return nnspk_launch_synth_pcm(dev_out, S, T, (unsigned long long)seed, s0, (long long)t0, amp, stream);
+}

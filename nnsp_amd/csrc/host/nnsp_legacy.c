@@ -1,0 +1,688 @@
+/*
+ * nnsp_legacy.c -- the drop-in single-stream ns-nnsp C API (nnsp_api.h) on
+ * MI355X.
+ *
+ * Semantics follow the reference call by call (file:line cited per function);
+ * the caller-owned structs (NNSPClass, FeatureClass, NeuralNetClass h/c arrays)
+ * stay the source of truth: every call uploads the state it needs, runs the
+ * same gfx950 kernels as the batched engine on a batch of one, and writes the
+ * new state back into the structs.  Nothing is computed on the CPU; host code
+ * here only moves bytes (buffer shifts, struct fields).  Like the reference
+ * (global scratch, T8) this layer is not re-entrant.
+ *
+ * The function addresses fc_8x16 / lstm_8x16 / *_acc32b / tanh_fix /
+ * sigmoid_fix / relu6_fix / linear_fix double as the layer / activation tags
+ * that def_nn*.c store in NeuralNetClass and that nnsp_image.c reads.
+ */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "nnsp_host.h"
+
+/* ---------------------------------------------------------------------------
+ * per-process GPU context: one HIP stream + a bump-allocated scratch arena
+ * ------------------------------------------------------------------------- */
+static struct {
+    void *stream;
+    uint8_t *arena;
+    size_t cap, used;
+    int ready;
+} G;
+
+static int gctx(void)
+{
+    if (G.ready) return 0;
+    int e = nnspk_stream_create(&G.stream);
+    if (e) return e;
+    G.cap = 4u << 20;
+    if ((e = nnspk_malloc((void **)&G.arena, G.cap))) return e;
+    G.ready = 1;
+    return 0;
+}
+
+static void *dscratch(size_t n)
+{
+    n = (n + 255) & ~(size_t)255;
+    if (G.used + n > G.cap) return NULL;
+    void *p = G.arena + G.used;
+    G.used += n;
+    return p;
+}
+
+#define CK(x)                                                                           \
+    do {                                                                                \
+        int _e = (x);                                                                   \
+        if (_e) {                                                                       \
+            fprintf(stderr, "libnnsp_mi355x: %s failed: %s\n", #x, nnsp_strerror(_e)); \
+            abort();                                                                    \
+        }                                                                               \
+    } while (0)
+
+const char *nnsp_strerror(int code);
+
+static void begin(void)
+{
+    CK(gctx());
+    G.used = 0;
+}
+static void *up(const void *h, size_t n)
+{
+    void *d = dscratch(n);
+    if (!d) CK(NNSP_ENOMEM);
+    if (h) CK(nnspk_h2d(d, h, n, G.stream));
+    else CK(nnspk_memset(d, 0, n, G.stream));
+    return d;
+}
+static void down(void *h, const void *d, size_t n) { CK(nnspk_d2h(h, d, n, G.stream)); }
+static void fin(void) { CK(nnspk_sync(G.stream)); }
+
+/* ---------------------------------------------------------------------------
+ * net image cache (keyed by NeuralNetClass* or by a single-layer call site)
+ * ------------------------------------------------------------------------- */
+typedef struct img_node {
+    struct img_node *next;
+    const void *key[4];
+    int ikey[8];
+    nnsp_image im;
+    int out_linear;
+} img_node;
+static img_node *g_imgs;
+
+static img_node *img_find(const void *k0, const void *k1, const void *k2, const void *k3,
+                          const int *ik)
+{
+    for (img_node *n = g_imgs; n; n = n->next)
+        if (n->key[0] == k0 && n->key[1] == k1 && n->key[2] == k2 && n->key[3] == k3 &&
+            !memcmp(n->ikey, ik, sizeof n->ikey))
+            return n;
+    return NULL;
+}
+
+static img_node *img_add(const void *k0, const void *k1, const void *k2, const void *k3,
+                         const int *ik, const nnsp_layer_desc *L, int nl, int out_linear)
+{
+    img_node *n = (img_node *)calloc(1, sizeof *n);
+    if (!n) CK(NNSP_ENOMEM);
+    n->key[0] = k0; n->key[1] = k1; n->key[2] = k2; n->key[3] = k3;
+    memcpy(n->ikey, ik, sizeof n->ikey);
+    CK(nnsp_image_build(&n->im, L, nl, 0, 0, 0));
+    CK(nnsp_image_upload(&n->im, G.stream));
+    n->out_linear = out_linear;
+    n->next = g_imgs;
+    g_imgs = n;
+    return n;
+}
+
+static img_node *net_image(const NeuralNetClass *net)
+{
+    static const int zk[8];
+    img_node *n = img_find(net, NULL, NULL, NULL, zk);
+    if (n) return n;
+    nnsp_layer_desc L[NN_MAX_LAYERS];
+    int nl = 0, lin = 0;
+    CK(nnsp_describe_net(net, L, &nl, &lin));
+    return img_add(net, NULL, NULL, NULL, zk, L, nl, lin);
+}
+
+/* LSTM h/c of a NeuralNetClass <-> device rows [l][NN_MAX_W] */
+static void net_state_up(const NeuralNetClass *net, int16_t **dh, int32_t **dc)
+{
+    int16_t hs[NN_MAX_LSTM][NN_MAX_W];
+    int32_t cs[NN_MAX_LSTM][NN_MAX_W];
+    memset(hs, 0, sizeof hs);
+    memset(cs, 0, sizeof cs);
+    int l = 0;
+    for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
+        if (net->net_layer_type[i] == lstm) {
+            const int N = net->size_layer[i + 1];
+            memcpy(hs[l], net->pt_hstate[i], (size_t)N * 2);
+            memcpy(cs[l], net->pt_cstate[i], (size_t)N * 4);
+            ++l;
+        }
+    *dh = (int16_t *)up(hs, sizeof hs);
+    *dc = (int32_t *)up(cs, sizeof cs);
+}
+
+static void net_state_down(NeuralNetClass *net, const int16_t *dh, const int32_t *dc)
+{
+    int16_t hs[NN_MAX_LSTM][NN_MAX_W];
+    int32_t cs[NN_MAX_LSTM][NN_MAX_W];
+    down(hs, dh, sizeof hs);
+    down(cs, dc, sizeof cs);
+    fin();
+    int l = 0;
+    for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
+        if (net->net_layer_type[i] == lstm) {
+            const int N = net->size_layer[i + 1];
+            memcpy(net->pt_hstate[i], hs[l], (size_t)N * 2);
+            memcpy(net->pt_cstate[i], cs[l], (size_t)N * 4);
+            ++l;
+        }
+}
+
+/* ---------------------------------------------------------------------------
+ * activations (activation.c)
+ * ------------------------------------------------------------------------- */
+static void *act_call(int type, int32_t *x, void *y, int len)
+{
+    if (len <= 0) return y;
+    begin();
+    const size_t ob = (size_t)len * (type == 3 ? 4 : 2);
+    int32_t *dx = (int32_t *)up(x, (size_t)len * 4);
+    void *dy = up(NULL, ob);
+    CK(nnspk_launch_act(type, dx, dy, len, G.stream));
+    down(y, dy, ob);
+    fin();
+    return (char *)y + ob;
+}
+void *relu6_fix(int16_t *y, int32_t *x, int len) { return act_call(0, x, y, len); }
+void *tanh_fix(int16_t *y, int32_t *x, int len) { return act_call(1, x, y, len); }
+void *sigmoid_fix(int16_t *y, int32_t *x, int len) { return act_call(2, x, y, len); }
+void *linear_fix(int32_t *y, int32_t *x, int len) { return act_call(3, x, y, len); }
+
+/* ---------------------------------------------------------------------------
+ * layers (affine.c:409-490, lstm.c:15-214) -- single-layer images
+ * ------------------------------------------------------------------------- */
+static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec,
+                     int16_t *p_bias, int16_t *input, int16_t *h_state, int32_t *c_state,
+                     int16_t dim_output, int16_t dim_input, int16_t qk, int16_t qb, int16_t qi,
+                     int16_t qir, void *(*act)(void *, int32_t *, int))
+{
+    begin();
+    nnsp_layer_desc d;
+    memset(&d, 0, sizeof d);
+    d.type = type;
+    d.K = dim_input;
+    d.N = dim_output;
+    d.acc32 = acc32;
+    d.qk = qk; d.qb = qb; d.qi = qi; d.qir = qir;
+    d.W = p_kernel; d.Wr = p_kernel_rec; d.B = p_bias;
+    d.act = type == NN_LSTM ? 1 : nnsp_act_of(act);
+    if (d.act < 0) {
+        fprintf(stderr, "libnnsp_mi355x: unsupported activation function pointer\n");
+        return -1;
+    }
+    const int ik[8] = {type, acc32, dim_output, dim_input, qk, qb, qi, (qir << 4) | d.act};
+    img_node *n = img_find(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik);
+    if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, &d, 1, d.act == 3);
+    int16_t in_pad[NN_MAX_K];
+    memset(in_pad, 0, sizeof in_pad);
+    memcpy(in_pad, input, (size_t)dim_input * 2);
+    int16_t *din = (int16_t *)up(in_pad, sizeof in_pad);
+    int16_t hs[NN_MAX_W];
+    int32_t cs[NN_MAX_W];
+    memset(hs, 0, sizeof hs);
+    memset(cs, 0, sizeof cs);
+    if (type == NN_LSTM) {
+        memcpy(hs, h_state, (size_t)dim_output * 2);
+        memcpy(cs, c_state, (size_t)dim_output * 4);
+    }
+    int16_t *dh = (int16_t *)up(hs, sizeof hs);
+    int32_t *dc = (int32_t *)up(cs, sizeof cs);
+    int32_t *dout = (int32_t *)up(NULL, NN_MAX_K * 4);
+    NnRun r;
+    memset(&r, 0, sizeof r);
+    r.S = 1; r.T = 1; r.mode = NN_MODE_DIRECT; r.nl_run = 1;
+    r.direct_in = din; r.h = dh; r.c = dc; r.logits = dout; r.out_stride = NN_MAX_K;
+    CK(nnspk_launch_nn(&n->im.img, &r, G.stream));
+    down(p_output, dout, (size_t)dim_output * (n->out_linear ? 4 : 2));
+    if (type == NN_LSTM) {
+        down(hs, dh, sizeof hs);
+        down(cs, dc, sizeof cs);
+    }
+    fin();
+    if (type == NN_LSTM) {
+        memcpy(h_state, hs, (size_t)dim_output * 2);
+        memcpy(c_state, cs, (size_t)dim_output * 4);
+    }
+    return 0;
+}
+
+int fc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+            int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
+            int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
+            int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+            void *(*act)(void *, int32_t *, int))
+{
+    (void)input_rec; (void)c_state; (void)dim_input_rec; (void)act_type;
+    return run_layer(NN_FC, 0, p_output, p_kernel, p_kernel_rec, p_bias, input, NULL, NULL,
+                     dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
+}
+
+int fc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+                   int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
+                   int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+                   int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
+{
+    (void)input_rec; (void)c_state; (void)dim_input_rec; (void)act_type;
+    return run_layer(NN_FC, 1, p_output, p_kernel, p_kernel_rec, p_bias, input, NULL, NULL,
+                     dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
+}
+
+int lstm_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+              int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
+              int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
+              int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+              void *(*act)(void *, int32_t *, int))
+{
+    (void)dim_input_rec; (void)act_type; (void)act;
+    return run_layer(NN_LSTM, 0, p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state,
+                     dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, NULL);
+}
+
+int lstm_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+                     int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
+                     int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+                     int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                     ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
+{
+    (void)dim_input_rec; (void)act_type; (void)act;
+    return run_layer(NN_LSTM, 1, p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state,
+                     dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, NULL);
+}
+
+/* ---------------------------------------------------------------------------
+ * NeuralNetClass (neural_nets.c:22-168)
+ * ------------------------------------------------------------------------- */
+void NeuralNetClass_init(NeuralNetClass *pt_inst) { (void)pt_inst; }
+
+void NeuralNetClass_setDefault(NeuralNetClass *pt_inst)
+{
+    for (int i = 0; i < pt_inst->numlayers; ++i)
+        if (pt_inst->net_layer_type[i] == lstm) {
+            memset(pt_inst->pt_cstate[i], 0, (size_t)pt_inst->size_layer[i + 1] * 4);
+            memset(pt_inst->pt_hstate[i], 0, (size_t)pt_inst->size_layer[i + 1] * 2);
+        }
+}
+
+void NeuralNetClass_exe(NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer)
+{
+    const int nl = debug_layer < 0 ? pt_inst->numlayers : debug_layer;
+    if (nl == 0) { /* neural_nets.c:85-91: copy the input through */
+        memcpy(output, input, (size_t)pt_inst->size_layer[0] * 2);
+        return;
+    }
+    begin();
+    img_node *n = net_image(pt_inst);
+    int16_t in_pad[NN_MAX_K];
+    memset(in_pad, 0, sizeof in_pad);
+    memcpy(in_pad, input, (size_t)pt_inst->size_layer[0] * 2);
+    int16_t *din = (int16_t *)up(in_pad, sizeof in_pad);
+    int16_t *dh;
+    int32_t *dc;
+    net_state_up(pt_inst, &dh, &dc);
+    int32_t *dout = (int32_t *)up(NULL, NN_MAX_K * 4);
+    NnRun r;
+    memset(&r, 0, sizeof r);
+    r.S = 1; r.T = 1; r.mode = NN_MODE_DIRECT; r.nl_run = nl;
+    r.direct_in = din; r.h = dh; r.c = dc; r.logits = dout; r.out_stride = NN_MAX_K;
+    CK(nnspk_launch_nn(&n->im.img, &r, G.stream));
+    const int lin = pt_inst->activation_type[nl - 1] == linear;
+    down(output, dout, (size_t)pt_inst->size_layer[nl] * (lin ? 4 : 2));
+    net_state_down(pt_inst, dh, dc);
+}
+
+/* ---------------------------------------------------------------------------
+ * front end (spectrogram_module.c, feature_module.c, melSpecProc.c, fixlog10.c,
+ * fft_arm.c)
+ * ------------------------------------------------------------------------- */
+int stftModule_construct(stftModule *ps) /* spectrogram_module.c:14-24 */
+{
+    ps->len_win = len_stft_win_coeff;
+    ps->hop = hop;
+    ps->len_fft = LEN_FFT_NNSP;
+    ps->window = stft_win_coeff;
+    arm_fft_init();
+    return 0;
+}
+
+int stftModule_setDefault(stftModule *ps) /* :25-31 */
+{
+    memset(ps->dataBuffer, 0, (size_t)ps->len_win * 2);
+    return 0;
+}
+
+void arm_fft_init(void) { /* twiddles are compile-time tables; nothing to build */ }
+
+void arm_fft_exec(int32_t *y, int32_t *x) /* fft_arm.c:16-20 -> arm_rfft_q31 */
+{
+    begin();
+    int32_t *dx = (int32_t *)up(x, 512 * 4);
+    int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
+    CK(nnspk_launch_rfft(dx, dy, 1, G.stream));
+    down(y, dy, 1024 * 4);
+    down(x, dx, 512 * 4); /* CMSIS transforms pSrc in place */
+    fin();
+}
+
+/* one FE frame on the GPU: tail = dataBuffer[160..479] before the shift */
+static void fe_frame(const int16_t *tail, const int16_t *pcm, const int32_t *mean, const int32_t *stdR,
+                     int qbit, int16_t *feat40, int32_t *log40, int32_t *spec1024)
+{
+    begin();
+    FeArgs a;
+    memset(&a, 0, sizeof a);
+    a.pcm = (const int16_t *)up(pcm, 160 * 2);
+    a.tail = (const int16_t *)up(tail, 320 * 2);
+    a.S = 1; a.T = 1;
+    int32_t zeros[40] = {0};
+    a.mean = (const int32_t *)up(mean ? mean : zeros, 160);
+    a.stdR = (const int32_t *)up(stdR ? stdR : zeros, 160);
+    a.norm_shift = 30 - qbit;
+    a.feats = (int16_t *)up(NULL, 80);
+    if (log40) a.dbg_log = (int32_t *)up(NULL, 160);
+    if (spec1024) a.dbg_spec = (int32_t *)up(NULL, 4096);
+    CK(nnspk_launch_fe(&a, G.stream));
+    if (feat40) down(feat40, a.feats, 80);
+    if (log40) down(log40, a.dbg_log, 160);
+    if (spec1024) down(spec1024, a.dbg_spec, 4096);
+    fin();
+}
+
+int stftModule_analyze_arm(void *ps_, int16_t *x, int32_t *y) /* :94-124 */
+{
+    stftModule *ps = (stftModule *)ps_;
+    int16_t tail[320];
+    memcpy(tail, ps->dataBuffer + 160, sizeof tail);
+    fe_frame(tail, x, NULL, NULL, 8, NULL, NULL, y);
+    memmove(ps->dataBuffer, ps->dataBuffer + 160, 320 * 2);
+    memcpy(ps->dataBuffer + 320, x, 160 * 2);
+    return 0;
+}
+
+void spec2pspec_arm(int32_t *y, int32_t *x, int len) /* :79-92 */
+{
+    if (len <= 0) return;
+    begin();
+    int32_t *dx = (int32_t *)up(x, (size_t)2 * len * 4);
+    int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
+    CK(nnspk_launch_pspec(dy, dx, len, 1, G.stream));
+    down(y, dy, (size_t)len * 4);
+    fin();
+}
+
+void melSpecProc(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
+{
+    begin();
+    int32_t *ds = (int32_t *)up(specs, 257 * 4);
+    int32_t *dm = (int32_t *)up(NULL, 160);
+    CK(nnspk_launch_mel(ds, dm, 1, G.stream));
+    down(melSpecs, dm, 160);
+    fin();
+}
+
+void norm_oneTwo(int32_t x, int32_t *y, int8_t *shift) /* fixlog10.c:9-28 */
+{
+    begin();
+    int32_t *dx = (int32_t *)up(&x, 4);
+    int32_t *dy = (int32_t *)up(NULL, 8);
+    CK(nnspk_launch_scalar(2, dx, dy, 1, G.stream));
+    int32_t o[2];
+    down(o, dy, 8);
+    fin();
+    *y = o[0];
+    *shift = (int8_t)o[1];
+}
+
+void log10_vec(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in) /* :53-61 */
+{
+    if (len <= 0) return;
+    begin();
+    int32_t *dx = (int32_t *)up(x, (size_t)len * 4);
+    int32_t *dy = (int32_t *)up(NULL, (size_t)len * 4);
+    CK(nnspk_launch_log10(dy, dx, len, (15 - bit_frac_in) * 0x2688, G.stream));
+    down(out, dy, (size_t)len * 4);
+    fin();
+}
+
+void my_log10(int32_t *out, int32_t x) { log10_vec(out, &x, 1, 15); } /* :31-50 */
+
+void FeatureClass_construct(FeatureClass *ps, const int32_t *norm_mean, const int32_t *norm_stdR,
+                            int8_t qbit_output) /* feature_module.c:12-24 */
+{
+    stftModule_construct(&ps->state_stftModule);
+    ps->pt_norm_mean = norm_mean;
+    ps->pt_norm_stdR = norm_stdR;
+    ps->num_context = NUM_FEATURE_CONTEXT;
+    ps->dim_feat = DIMEMSION_FEATURE;
+    ps->qbit_output = qbit_output;
+}
+
+void FeatureClass_setDefault(FeatureClass *ps) /* :26-45 */
+{
+    stftModule_setDefault(&ps->state_stftModule);
+    begin();
+    int16_t *dp = (int16_t *)up(ps->normFeatContext + 40, 400);
+    int16_t *dt = (int16_t *)up(NULL, 640);
+    int32_t *dm = (int32_t *)up(ps->pt_norm_mean, 160);
+    int32_t *ds = (int32_t *)up(ps->pt_norm_stdR, 160);
+    CK(nnspk_launch_fe_default(dp, dt, dm, ds, 30 - ps->qbit_output, NULL, 1, G.stream));
+    int16_t p5[200];
+    down(p5, dp, 400);
+    fin();
+    for (int j = 0; j < NUM_FEATURE_CONTEXT - 1; ++j) memcpy(ps->normFeatContext + 40 * j, p5, 80);
+}
+
+void FeatureClass_execute(FeatureClass *ps, int16_t *input) /* :47-74 */
+{
+    int16_t tail[320], f5[40];
+    memcpy(tail, ps->state_stftModule.dataBuffer + 160, sizeof tail);
+    fe_frame(tail, input, ps->pt_norm_mean, ps->pt_norm_stdR, ps->qbit_output, f5, ps->feature, NULL);
+    memmove(ps->normFeatContext, ps->normFeatContext + 40, 200 * 2);
+    memcpy(ps->normFeatContext + 200, f5, 80);
+    memmove(ps->state_stftModule.dataBuffer, ps->state_stftModule.dataBuffer + 160, 320 * 2);
+    memcpy(ps->state_stftModule.dataBuffer + 320, input, 160 * 2);
+}
+
+/* ---------------------------------------------------------------------------
+ * NNSPClass (nn_speech.c)
+ * ------------------------------------------------------------------------- */
+int NNSPClass_init(NNSPClass *pt_inst, void *pt_net, void *pt_feat, char nn_id, const int32_t *pt_mean,
+                   const int32_t *pt_stdR, int16_t *pt_thresh_prob, int16_t *pt_th_count_trigger)
+{ /* :23-55 */
+    pt_inst->nn_id = nn_id;
+    pt_inst->pt_feat = pt_feat;
+    pt_inst->pt_net = pt_net;
+    FeatureClass_construct((FeatureClass *)pt_feat, pt_mean, pt_stdR,
+                           ((NeuralNetClass *)pt_net)->qbit_input[0]);
+    pt_inst->num_dnsmpl = 2;
+    pt_inst->pt_thresh_prob = pt_thresh_prob;
+    pt_inst->pt_th_count_trigger = pt_th_count_trigger;
+    NeuralNetClass_init((NeuralNetClass *)pt_net);
+    return 0;
+}
+
+int NNSPClass_reset(NNSPClass *pt_inst) /* :57-72 */
+{
+    FeatureClass_setDefault((FeatureClass *)pt_inst->pt_feat);
+    NeuralNetClass_setDefault((NeuralNetClass *)pt_inst->pt_net);
+    pt_inst->slides = 1;
+    pt_inst->trigger = 0;
+    for (int i = 0; i < DIM_INTENTS; ++i) pt_inst->counts_category[i] = 0;
+    for (int i = 0; i < 3; ++i) pt_inst->outputs[i] = 0;
+    pt_inst->argmax_last = 0;
+    return 0;
+}
+
+static void post_pack(const NNSPClass *p, NnPost *q)
+{
+    memset(q, 0, sizeof *q);
+    q->slides = p->slides;
+    q->trigger = p->trigger;
+    q->argmax_last = p->argmax_last;
+    memcpy(q->counts, p->counts_category, sizeof q->counts);
+    memcpy(q->outputs, p->outputs, sizeof q->outputs);
+}
+
+static void post_unpack(NNSPClass *p, const NnPost *q)
+{
+    p->slides = (int8_t)q->slides;
+    p->trigger = q->trigger;
+    p->argmax_last = q->argmax_last;
+    memcpy(p->counts_category, q->counts, sizeof q->counts);
+    memcpy(p->outputs, q->outputs, sizeof q->outputs);
+}
+
+int16_t NNSPClass_exec(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
+{
+    FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
+    NeuralNetClass *net = (NeuralNetClass *)pt_inst->pt_net;
+    begin();
+    img_node *n = net_image(net);
+    NnImage img = n->im.img;
+    img.nn_id = pt_inst->nn_id;
+    img.thresh_prob = *pt_inst->pt_thresh_prob;
+    img.th_count = *pt_inst->pt_th_count_trigger;
+    FeArgs a;
+    memset(&a, 0, sizeof a);
+    const int16_t *pcm_d = (const int16_t *)up(rawPCM, 320);
+    a.pcm = pcm_d;
+    a.tail = (const int16_t *)up(fe->state_stftModule.dataBuffer + 160, 640);
+    a.S = 1; a.T = 1;
+    a.mean = (const int32_t *)up(fe->pt_norm_mean, 160);
+    a.stdR = (const int32_t *)up(fe->pt_norm_stdR, 160);
+    a.norm_shift = 30 - fe->qbit_output;
+    a.feats = (int16_t *)up(NULL, 80);
+    a.dbg_log = (int32_t *)up(NULL, 160);
+    CK(nnspk_launch_fe(&a, G.stream));
+    NnPost ps;
+    post_pack(pt_inst, &ps);
+    NnRun r;
+    memset(&r, 0, sizeof r);
+    r.S = 1; r.T = 1; r.mode = NN_MODE_STREAM; r.nl_run = img.nl;
+    r.feats = a.feats;
+    r.prev5 = (const int16_t *)up(fe->normFeatContext + 40, 400);
+    net_state_up(net, &r.h, &r.c);
+    r.post = up(&ps, sizeof ps);
+    r.trig = (int16_t *)up(NULL, 2);
+    CK(nnspk_launch_nn(&img, &r, G.stream));
+    int16_t f5[40];
+    down(f5, a.feats, 80);
+    down(fe->feature, a.dbg_log, 160);
+    down(&ps, r.post, sizeof ps);
+    net_state_down(net, r.h, r.c); /* syncs */
+    memmove(fe->normFeatContext, fe->normFeatContext + 40, 200 * 2);
+    memcpy(fe->normFeatContext + 200, f5, 80);
+    memmove(fe->state_stftModule.dataBuffer, fe->state_stftModule.dataBuffer + 160, 320 * 2);
+    memcpy(fe->state_stftModule.dataBuffer + 320, rawPCM, 160 * 2);
+    post_unpack(pt_inst, &ps);
+    return pt_inst->trigger;
+}
+
+void my_argmax(int32_t *vec, int len, int16_t *Imax) /* :130-144 */
+{
+    begin();
+    int32_t *dv = (int32_t *)up(vec, (size_t)len * 4);
+    int32_t *dy = (int32_t *)up(NULL, 4);
+    CK(nnspk_launch_scalar(3, dv, dy, len, G.stream));
+    int32_t o;
+    down(&o, dy, 4);
+    fin();
+    *Imax = (int16_t)o;
+}
+
+static int32_t scalar1(int op, int32_t x)
+{
+    begin();
+    int32_t *dx = (int32_t *)up(&x, 4);
+    int32_t *dy = (int32_t *)up(NULL, 4);
+    CK(nnspk_launch_scalar(op, dx, dy, 1, G.stream));
+    int32_t o;
+    down(&o, dy, 4);
+    fin();
+    return o;
+}
+int32_t ceiling(int32_t input) { return scalar1(0, input); }      /* :229-235 */
+int32_t compute_pwr2(int32_t input) { return scalar1(1, input); } /* :237-258 */
+
+static void post_call(NNSPClass *pt_inst, int32_t *est, int16_t *pt_trigger, int nn_id)
+{
+    begin();
+    NnPost ps;
+    post_pack(pt_inst, &ps);
+    void *dps = up(&ps, sizeof ps);
+    const int n = nn_id == 0 ? 41 : 2;
+    int32_t *de = (int32_t *)up(est, (size_t)n * 4);
+    CK(nnspk_launch_post(nn_id, *pt_inst->pt_thresh_prob, *pt_inst->pt_th_count_trigger, dps, de,
+                         G.stream));
+    down(&ps, dps, sizeof ps);
+    down(est, de, (size_t)n * 4);
+    fin();
+    const int16_t keep = pt_inst->trigger;
+    post_unpack(pt_inst, &ps);
+    pt_inst->trigger = keep;
+    *pt_trigger = ps.trigger;
+}
+
+void binary_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :191-227 */
+{
+    post_call(pt_inst, pt_nn_est, pt_trigger, 1);
+}
+
+void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :146-189 */
+{
+    post_call(pt_inst, pt_nn_est, pt_trigger, 0);
+}
+
+/* ---------------------------------------------------------------------------
+ * row-block primitives (affine.c:12-407, affine_acc32b.c) -- not yet on GPU
+ * ------------------------------------------------------------------------- */
+static int unsupported(const char *fn)
+{
+    fprintf(stderr, "libnnsp_mi355x: %s is not provided by this build (use fc_8x16 / lstm_8x16)\n", fn);
+    return -1;
+}
+int affine_Krows_8x16(int16_t a, int16_t **b, int8_t **c, int16_t **d, int16_t *e, int16_t f,
+                      int16_t g, int16_t h, int16_t i, int64_t *j, int8_t k,
+                      void *(*l)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l;
+    return unsupported("affine_Krows_8x16");
+}
+int affine_Krows_8x16_acc32b(int16_t a, int16_t **b, int8_t **c, int16_t **d, int16_t *e, int16_t f,
+                             int16_t g, int16_t h, int16_t i, int32_t *j, int8_t k,
+                             void *(*l)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l;
+    return unsupported("affine_Krows_8x16_acc32b");
+}
+int rc_Krows_8x16(int16_t a, int16_t **b, int8_t **c, int8_t **d, int16_t **e, int16_t *f, int16_t *g,
+                  int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m,
+                  void *(*n)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n;
+    return unsupported("rc_Krows_8x16");
+}
+int rc_Krows_8x16_acc32b(int16_t a, int16_t **b, int8_t **c, int8_t **d, int16_t **e, int16_t *f,
+                         int16_t *g, int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m,
+                         void *(*n)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n;
+    return unsupported("rc_Krows_8x16_acc32b");
+}
+int rc_8x16(int16_t *a, int8_t *b, int8_t *c, int16_t *d, int16_t *e, int16_t *f, int16_t g, int16_t h,
+            int16_t i, int16_t j, int16_t k, int16_t l, int16_t m, ACTIVATION_TYPE n,
+            void *(*o)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n; (void)o;
+    return unsupported("rc_8x16");
+}
+int rc_8x16_acc32b(int16_t *a, int8_t *b, int8_t *c, int16_t *d, int16_t *e, int16_t *f, int16_t g,
+                   int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m, ACTIVATION_TYPE n,
+                   void *(*o)(void *, int32_t *, int))
+{
+    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n; (void)o;
+    return unsupported("rc_8x16_acc32b");
+}
+void shift_64b(int64_t *x, int8_t shift, int len)
+{
+    (void)x; (void)shift; (void)len;
+    unsupported("shift_64b");
+}
+void shift_32b(int32_t *x, int8_t shift, int len)
+{
+    (void)x; (void)shift; (void)len;
+    unsupported("shift_32b");
+}

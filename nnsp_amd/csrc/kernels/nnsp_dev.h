@@ -1,0 +1,201 @@
+// nnsp_dev.h -- gfx950 device building blocks of the ns-nnsp hot path.
+//
+// Every function here reproduces the integer semantics of the reference C
+// (ARM_OPTIMIZED=1 build, reference/ns-nnsp/src) or of CMSIS-DSP 1.10.0's
+// arm_rfft_q31 bit for bit; file:line citations name the code each follows.
+// Signed overflow wraps (as on the Cortex-M4): all such arithmetic goes
+// through uint32 helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../gen/nnsp_tables.h"
+
+namespace nnsp {
+
+// ---- wrapping int32 helpers -------------------------------------------------
+__device__ __forceinline__ int32_t wadd(int32_t a, int32_t b) { return (int32_t)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int32_t wsub(int32_t a, int32_t b) { return (int32_t)((uint32_t)a - (uint32_t)b); }
+__device__ __forceinline__ int32_t wshl(int32_t a, int s) { return (int32_t)((uint32_t)a << s); }
+__device__ __forceinline__ int32_t sat32(int64_t v) {
+    return v > INT32_MAX ? INT32_MAX : (v < INT32_MIN ? INT32_MIN : (int32_t)v);
+}
+__device__ __forceinline__ int16_t sat16(int64_t v) {
+    return v > 32767 ? (int16_t)32767 : (v < -32768 ? (int16_t)-32768 : (int16_t)v);
+}
+// (int32)(((int64)a*b) >> 32): v_mul_hi_i32
+__device__ __forceinline__ int32_t mulhi(int32_t a, int32_t b) { return __mulhi(a, b); }
+
+// SMMLAR / SMMULR contribution: floor((x*c + 2^31) / 2^32)
+__device__ __forceinline__ int32_t rnd_add(int32_t x, int32_t c) {
+    return (int32_t)(((int64_t)x * c + 0x80000000LL) >> 32);
+}
+// SMMLSR contribution: floor((2^31 - x*c) / 2^32) = -floor((x*c + 2^31 - 1) / 2^32)
+__device__ __forceinline__ int32_t rnd_sub(int32_t x, int32_t c) {
+    return (int32_t)(-(((int64_t)x * c + 0x7FFFFFFFLL) >> 32));
+}
+
+__device__ __forceinline__ int rev8(int i) { return (int)(__brev((uint32_t)i) >> 24); }
+
+// Keep intra-wave LDS producer/consumer order (all lanes of one wave).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ---- radix-4 butterflies of arm_radix4_butterfly_q31 (CMSIS-DSP 1.10.0) -----
+// first stage: inputs pre-scaled >>4, rotated outputs (..)<<1
+// middle stages: sums >>2, rotated outputs (..)>>1 ; twiddles (co,si) k,2k,3k
+struct Tw3 { int32_t c1, s1, c2, s2, c3, s3; };
+
+__device__ __forceinline__ Tw3 load_tw3(int k) {
+    Tw3 t;
+    t.c1 = nnsp_tbl_tw256[2 * k];     t.s1 = nnsp_tbl_tw256[2 * k + 1];
+    t.c2 = nnsp_tbl_tw256[4 * k];     t.s2 = nnsp_tbl_tw256[4 * k + 1];
+    t.c3 = nnsp_tbl_tw256[6 * k];     t.s3 = nnsp_tbl_tw256[6 * k + 1];
+    return t;
+}
+
+template <bool FIRST>
+__device__ __forceinline__ void bfly4(int32_t& xa, int32_t& ya, int32_t& xb, int32_t& yb,
+                                      int32_t& xc, int32_t& yc, int32_t& xd, int32_t& yd,
+                                      const Tw3& w) {
+    if (FIRST) {
+        xa >>= 4; ya >>= 4; xb >>= 4; yb >>= 4; xc >>= 4; yc >>= 4; xd >>= 4; yd >>= 4;
+    }
+    int32_t r1 = wadd(xa, xc), r2 = wsub(xa, xc), s1 = wadd(ya, yc), s2 = wsub(ya, yc);
+    int32_t t1 = wadd(xb, xd), t2 = wadd(yb, yd);
+    const int32_t oa = FIRST ? wadd(r1, t1) : (wadd(r1, t1) >> 2);
+    const int32_t pa = FIRST ? wadd(s1, t2) : (wadd(s1, t2) >> 2);
+    r1 = wsub(r1, t1);
+    s1 = wsub(s1, t2);
+    t1 = wsub(yb, yd);
+    t2 = wsub(xb, xd);
+    int32_t ob = wadd(mulhi(r1, w.c2), mulhi(s1, w.s2));   // -> slot i1 ("xc'")
+    int32_t pb = wsub(mulhi(s1, w.c2), mulhi(r1, w.s2));
+    const int32_t q1 = wadd(r2, t1), q2 = wsub(r2, t1), u1 = wsub(s2, t2), u2 = wadd(s2, t2);
+    int32_t oc = wadd(mulhi(q1, w.c1), mulhi(u1, w.s1));   // -> slot i2 ("xb'")
+    int32_t pc = wsub(mulhi(u1, w.c1), mulhi(q1, w.s1));
+    int32_t od = wadd(mulhi(q2, w.c3), mulhi(u2, w.s3));   // -> slot i3
+    int32_t pd = wsub(mulhi(u2, w.c3), mulhi(q2, w.s3));
+    if (FIRST) {
+        ob = wshl(ob, 1); pb = wshl(pb, 1); oc = wshl(oc, 1); pc = wshl(pc, 1);
+        od = wshl(od, 1); pd = wshl(pd, 1);
+    } else {
+        ob >>= 1; pb >>= 1; oc >>= 1; pc >>= 1; od >>= 1; pd >>= 1;
+    }
+    xa = oa; ya = pa; xb = ob; yb = pb; xc = oc; yc = pc; xd = od; yd = pd;
+}
+
+// last radix-4 stage: unscaled, outputs in slot order a, c', b', d'
+__device__ __forceinline__ void bfly4_last(int32_t* q) {
+    const int32_t xa = q[0], ya = q[1], xb = q[2], yb = q[3];
+    const int32_t xc = q[4], yc = q[5], xd = q[6], yd = q[7];
+    q[0] = wadd(wadd(xa, xb), wadd(xc, xd));
+    q[1] = wadd(wadd(ya, yb), wadd(yc, yd));
+    q[2] = wsub(wadd(xa, xc), wadd(xb, xd));
+    q[3] = wsub(wadd(ya, yc), wadd(yb, yd));
+    q[4] = wsub(wadd(xa, yb), wadd(xc, yd));
+    q[5] = wsub(wadd(ya, xd), wadd(xb, yc));
+    q[6] = wsub(wadd(xa, yd), wadd(yb, xc));
+    q[7] = wsub(wadd(ya, xb), wadd(yc, xd));
+}
+
+// arm_split_rfft_q31 for one bin k in 1..255 (modifier 16):
+// Z = bit-reversed cfft output; (xr,xi) = Z[k], (yr,yi) = Z[256-k]
+__device__ __forceinline__ void split_bin(int32_t xr, int32_t xi, int32_t yr, int32_t yi,
+                                          int32_t A1, int32_t A2, int32_t B1, int32_t& re,
+                                          int32_t& im) {
+    re = wadd(wadd(rnd_add(xr, A1), rnd_sub(xi, A2)), wadd(rnd_sub(yi, A2), rnd_add(yr, B1)));
+    im = wadd(wadd(rnd_add(xr, A2), rnd_add(xi, A1)), wadd(rnd_sub(yi, B1), rnd_sub(yr, A2)));
+}
+
+// spec2pspec_arm (spectrogram_module.c:79-92): truncating cast of (re^2+im^2)>>27
+__device__ __forceinline__ int32_t pspec_of(int32_t re, int32_t im) {
+    return (int32_t)(((int64_t)re * re + (int64_t)im * im) >> 27);
+}
+
+// my_log10 + norm_oneTwo (fixlog10.c:9-50), bit_frac_in = 15
+__device__ __forceinline__ int32_t log10_q15(int32_t x) {
+    if (x == 0) x = 1;
+    const uint32_t m = (uint32_t)x & 0x7FFFFFFFu;   // bits 30..0 searched
+    int sh = 0;
+    if (m) {
+        const int b = 31 - __clz((int)m);
+        sh = 15 - b;
+    }
+    const int32_t y = sh >= 0 ? wshl(x, sh) : (x >> -sh);
+    const int e = -sh;
+    int32_t kx = (y - 32768) >> 8;
+    const int32_t dx = (y - 32768) - (kx << 8);
+    kx = kx < 0 ? 0 : (kx > 127 ? 127 : kx);   // only x<0 (T3 wrap) leaves 0..127
+    int32_t v = nnsp_tbl_log[2 * kx] + ((nnsp_tbl_log[2 * kx + 1] * dx) >> 15);
+    v = (int32_t)(((int64_t)v * 0x3796) >> 15);
+    return wadd(v, 0x2688 * e);
+}
+
+// ---- activations (activation.c) --------------------------------------------
+__device__ __forceinline__ int16_t tanh_q15(int32_t x, const int16_t* tbl) {   // :31-69
+    const bool neg = x < 0;
+    const int32_t a = neg ? wsub(0, x) : x;
+    int16_t y;
+    if (a >= (5 << 15)) {
+        y = 0x7fff;
+    } else {
+        int32_t kx = wsub(a, 512) >> 10;
+        kx = kx < 0 ? 0 : (kx > 191 ? 191 : kx);
+        const int32_t dx = a - 512 - (kx << 10);
+        const int32_t v = tbl[2 * kx] + ((dx * tbl[2 * kx + 1]) >> 15);
+        y = (int16_t)(v > 0 ? v : 0);
+    }
+    return neg ? (int16_t)-y : y;
+}
+__device__ __forceinline__ int16_t sigmoid_q15(int32_t x, const int16_t* tbl) {   // :72-87
+    return (int16_t)((tanh_q15(x >> 1, tbl) >> 1) + 16384);
+}
+__device__ __forceinline__ int16_t relu6_q12(int32_t x) {   // :6-17
+    int32_t v = x >> 3;
+    v = v > 24576 ? 24576 : v;
+    return (int16_t)(v < 0 ? 0 : v);
+}
+
+enum { ACT_RELU6 = 0, ACT_TANH = 1, ACT_SIGMOID = 2, ACT_LINEAR = 3 };
+
+// shift_64b / shift_32b (affine.c:565-591, affine_acc32b.c:566-592)
+__device__ __forceinline__ int64_t shift64(int64_t v, int sh) {
+    if (sh < 0) return v >> -sh;
+    if (sh > 0) {
+        const int64_t M = (int64_t)((1ULL << (63 - sh)) - 1), mn = -M - 1;
+        v = v > M ? M : (v < mn ? mn : v);
+        return (int64_t)((uint64_t)v << sh);
+    }
+    return v;
+}
+__device__ __forceinline__ int32_t shift32(int32_t v, int sh) {
+    if (sh < 0) return v >> -sh;
+    if (sh > 0) {
+        const int32_t M = (int32_t)((1u << (31 - sh)) - 1), mn = -M - 1;
+        v = v > M ? M : (v < mn ? mn : v);
+        return wshl(v, sh);
+    }
+    return v;
+}
+
+// post-processing helpers (nn_speech.c:229-258)
+__device__ __forceinline__ int32_t ceiling_q15(int32_t x) {
+    const int32_t o = wshl(x >> 15, 15);
+    return o == x ? o : wadd(o, 32768);
+}
+__device__ __forceinline__ int32_t pwr2_q15(int32_t x) {
+    const int32_t c = ceiling_q15(x);
+    const int32_t f = wsub(x, c);
+    const int32_t sh = c >> 15;
+    if (sh <= -15) return 0;
+    const int32_t t = wadd(wshl(f, 1), 32768);
+    int32_t o = 0x1fd7 + ((t * 0x057a) >> 15);
+    o = 0x5a82 + ((t * o) >> 15);
+    return sh < 0 ? (o >> -sh) : wshl(o, sh);
+}
+
+}  // namespace nnsp

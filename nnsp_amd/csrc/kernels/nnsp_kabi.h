@@ -1,0 +1,117 @@
+/* nnsp_kabi.h -- plain-C argument blocks shared by the C host library and the
+ * HIP launch layer (nnsp_kernels.hip).  No HIP or torch types. */
+#ifndef NNSP_KABI_H
+#define NNSP_KABI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NN_MAX_LAYERS 10
+#define NN_MAX_LSTM 2   /* LSTM layers per net */
+#define NN_MAX_W 128    /* LSTM width; also the h/c row stride in device state */
+#define NN_MAX_K 256    /* FC / LSTM input width (4 MFMA k-tiles) */
+#define NN_MAX_OUT 64   /* width of the last layer */
+#define NN_FC 0
+#define NN_LSTM 1
+#define NN_MODE_STREAM 0 /* NNSPClass_exec over a chunk: FE features in, post-proc */
+#define NN_MODE_DIRECT 1 /* NeuralNetClass_exe: 240-wide input in, raw output */
+
+typedef struct {
+    const int16_t *pcm;  /* [S][T][160] */
+    const int16_t *tail; /* [S][320]: samples of the two frames before the chunk */
+    int32_t S, T;
+    const int32_t *mean, *stdR;
+    int32_t norm_shift;  /* 30 - qbit_output */
+    int16_t *feats;      /* [S][T][40] normalised log-Mel (context slot 5) */
+    int32_t *dbg_spec;   /* optional [S*T][1024] rfft output */
+    int32_t *dbg_log;    /* optional [S*T][40] log10 Mel (FeatureClass.feature) */
+} FeArgs;
+
+typedef struct {
+    int32_t type, K, N, act;
+    int32_t rows;        /* FC: N; LSTM: 16 * nrt (re-tiled, padded) */
+    int32_t nrt, nkt, nkt_r;
+    int32_t has_bias, bias_sh, out_sh; /* affine_Krows epilogue */
+    int32_t xs_sh;       /* LSTM: shift_64b(acc, qi_rec - qi) on the input part */
+    int32_t ep_off;      /* row offset into wsum / wsum_r / bias */
+    int32_t pad;
+    int64_t a_off, ar_off; /* byte offsets of the MFMA A fragments */
+} NnLayer;
+
+typedef struct {
+    const uint8_t *A;      /* A fragments, 1 KiB per (row tile, k tile) */
+    const int32_t *wsum;   /* per row: 128 * sum_k W (hi/lo split correction) */
+    const int32_t *wsum_r; /* per row: 128 * sum_k W_rec */
+    const int16_t *bias;   /* per row (re-tiled order for LSTM) */
+    int32_t nl, acc32, nout, n_lstm;
+    int32_t nn_id, thresh_prob, th_count, pad;
+    int32_t lstm_n[NN_MAX_LSTM];
+    NnLayer L[NN_MAX_LAYERS];
+} NnImage;
+
+typedef struct {
+    int32_t S, T, mode, nl_run;
+    const int16_t *feats;     /* [S][T][40] */
+    const int16_t *prev5;     /* [S][5][40] */
+    const int16_t *direct_in; /* [S][NN_MAX_K] (DIRECT mode) */
+    int16_t *h;               /* [S][n_lstm][NN_MAX_W] */
+    int32_t *c;               /* [S][n_lstm][NN_MAX_W] */
+    void *post;               /* [S] post-processing state (32 B each) */
+    int16_t *trig;            /* [S][T] NNSPClass_exec return value per frame */
+    int32_t *logits;          /* STREAM: [S][T][nout] (NN frames only); DIRECT: [S][out_stride] */
+    int32_t out_stride, pad;
+} NnRun;
+
+/* 32-byte device post-processing state, one per stream */
+typedef struct {
+    int16_t slides, trigger, argmax_last, pad0;
+    int16_t counts[8];
+    int16_t outputs[3], pad1;
+} NnPost;
+
+/* launch layer (nnsp_kernels.hip) */
+int nnspk_launch_fe(const FeArgs *a, void *stream);
+int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
+int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, void *stream);
+int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, void *stream);
+int nnspk_launch_synth_pcm(int16_t *out, int S, int T, unsigned long long seed, int s0,
+                           long long t0, int amp, void *stream);
+int nnspk_launch_rfft(int32_t *x, int32_t *y, int n, void *stream);
+int nnspk_launch_pspec(int32_t *y, const int32_t *x, int len, int n, void *stream);
+int nnspk_launch_mel(const int32_t *spec, int32_t *mel, int n, void *stream);
+int nnspk_launch_log10(int32_t *out, const int32_t *x, int n, int add, void *stream);
+int nnspk_launch_act(int type, const int32_t *x, void *y, int n, void *stream);
+int nnspk_launch_scalar(int op, const int32_t *in, int32_t *out, int n, void *stream);
+int nnspk_launch_post(int nn_id, int thresh_prob, int th_count, void *post, int32_t *est,
+                      void *stream);
+int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
+                            const int32_t *stdR, int norm_shift, const uint8_t *mask, int n,
+                            void *stream);
+int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
+                            int n, void *stream);
+int nnspk_malloc(void **p, size_t n);
+int nnspk_free(void *p);
+int nnspk_memset(void *p, int v, size_t n, void *stream);
+int nnspk_h2d(void *d, const void *h, size_t n, void *stream);
+int nnspk_d2h(void *h, const void *d, size_t n, void *stream);
+int nnspk_d2d(void *d, const void *s, size_t n, void *stream);
+int nnspk_sync(void *stream);
+int nnspk_device_count(int *n);
+int nnspk_set_device(int d);
+int nnspk_get_device(int *d);
+const char *nnspk_error_string(int e);
+int nnspk_stream_create(void **s);
+int nnspk_stream_destroy(void *s);
+int nnspk_event_create(void **e);
+int nnspk_event_destroy(void *e);
+int nnspk_event_record(void *e, void *stream);
+int nnspk_event_elapsed(float *ms, void *a, void *b);
+int nnspk_device_info(int *cus, int *clock_khz, char *name, int name_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,837 @@
+// nnsp_kernels.hip -- hand-written gfx950 kernels of the ns-nnsp hot path and
+// the thin C-ABI launch layer the host library calls (nnsp_dev.h has the
+// bit-exact building blocks).
+//
+//   fe_kernel : FeatureClass_execute for every (stream, frame) of a chunk,
+//               one wave64 per frame (window, 256-pt radix-4 q31 cFFT with one
+//               butterfly per lane, split, power, 40-bank Mel, log10, norm).
+//   nn_kernel : NeuralNetClass_exe + NNSPClass post-processing, persistent over
+//               the chunk's NN steps; one wave per 16-stream tile; every FC /
+//               LSTM matrix product on v_mfma_i32_16x16x64_i8 with int16
+//               activations split into hi/lo int8 planes (exact in int32).
+//   k_*       : batched single-stage kernels backing the legacy scalar API.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nnsp_dev.h"
+#include "nnsp_kabi.h"
+
+using namespace nnsp;
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// ============================================================================
+// Front end
+// ============================================================================
+// LDS image of one frame: 256 complex q31, with a 32-dword pad after every
+// 64 complex so the stage-2 access pattern (i0 = 64b + j) is conflict-free.
+#define FE_SEG 160   // dwords per 64-complex segment (128 data + 32 pad)
+#define FE_FRAME_DW (4 * FE_SEG)
+__device__ __forceinline__ int cidx(int c) { return 2 * c + 32 * (c >> 6); }
+
+struct FeLane {
+    int16_t win[8];
+    Tw3 t1, t2, t3;
+    int32_t A1[4], A2[4], B1[4];
+    int rk[4], rn[4];
+    int mstart, mend, moff;
+};
+
+__device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
+    for (int j = 0; j < 8; ++j) L.win[j] = lane < 60 ? nnsp_tbl_window[8 * lane + j] : 0;
+    L.t1 = load_tw3(lane);
+    L.t2 = load_tw3(4 * (lane & 15));
+    L.t3 = load_tw3(16 * (lane & 3));
+    for (int m = 0; m < 4; ++m) {
+        const int k = lane + 64 * m;
+        L.A1[m] = nnsp_tbl_split[3 * k];
+        L.A2[m] = nnsp_tbl_split[3 * k + 1];
+        L.B1[m] = nnsp_tbl_split[3 * k + 2];
+        L.rk[m] = rev8(k);
+        L.rn[m] = rev8((256 - k) & 255);
+    }
+    // Mel bank 'lane' inside the packed [start, end, coef...] table
+    int off = 0;
+    L.mstart = 1; L.mend = 0; L.moff = 0;
+    for (int b = 0; b < 40; ++b) {
+        const int st = nnsp_tbl_mel[off], en = nnsp_tbl_mel[off + 1];
+        if (b == lane) { L.mstart = st; L.mend = en; L.moff = off + 2; }
+        off += 2 + (en - st + 1);
+    }
+}
+
+// In-place radix-4 cFFT (arm_radix4_butterfly_q31) of one frame held in LDS.
+__device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int lane) {
+    // stage 1: butterfly i0 = lane, stride 64
+    {
+        int32_t v[8];
+        for (int m = 0; m < 4; ++m) {
+            const int2 p = *reinterpret_cast<const int2*>(X + cidx(lane + 64 * m));
+            v[2 * m] = p.x; v[2 * m + 1] = p.y;
+        }
+        bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t1);
+        for (int m = 0; m < 4; ++m)
+            *reinterpret_cast<int2*>(X + cidx(lane + 64 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
+    }
+    wave_lds_sync();
+    // stage 2: i0 = 64*(lane>>4) + (lane&15), stride 16
+    {
+        const int i0 = 64 * (lane >> 4) + (lane & 15);
+        int32_t v[8];
+        for (int m = 0; m < 4; ++m) {
+            const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 16 * m));
+            v[2 * m] = p.x; v[2 * m + 1] = p.y;
+        }
+        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t2);
+        for (int m = 0; m < 4; ++m)
+            *reinterpret_cast<int2*>(X + cidx(i0 + 16 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
+    }
+    wave_lds_sync();
+    // stage 3: i0 = 16*(lane>>2) + (lane&3), stride 4
+    {
+        const int i0 = 16 * (lane >> 2) + (lane & 3);
+        int32_t v[8];
+        for (int m = 0; m < 4; ++m) {
+            const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 4 * m));
+            v[2 * m] = p.x; v[2 * m + 1] = p.y;
+        }
+        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t3);
+        for (int m = 0; m < 4; ++m)
+            *reinterpret_cast<int2*>(X + cidx(i0 + 4 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
+    }
+    wave_lds_sync();
+    // last stage: complex 4*lane .. 4*lane+3 (contiguous inside a segment)
+    {
+        int32_t* q = X + cidx(4 * lane);
+        int32_t v[8];
+        const int4 a = *reinterpret_cast<const int4*>(q);
+        const int4 b = *reinterpret_cast<const int4*>(q + 4);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        bfly4_last(v);
+        *reinterpret_cast<int4*>(q) = make_int4(v[0], v[1], v[2], v[3]);
+        *reinterpret_cast<int4*>(q + 4) = make_int4(v[4], v[5], v[6], v[7]);
+    }
+    wave_lds_sync();
+}
+
+// Split of bin k = lane + 64m from the (not yet bit-reversed) cFFT output Y.
+// Lane 0 / m 0 produces DC (re0) and Nyquist (reN) instead.
+__device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeLane& L, int lane, int m,
+                                               int32_t& re, int32_t& im, int32_t& reN) {
+    if (lane == 0 && m == 0) {
+        const int2 z0 = *reinterpret_cast<const int2*>(X + cidx(0));
+        re = wadd(z0.x, z0.y) >> 1;
+        im = 0;
+        reN = wsub(z0.x, z0.y) >> 1;
+        return;
+    }
+    const int2 zk = *reinterpret_cast<const int2*>(X + cidx(L.rk[m]));
+    const int2 zn = *reinterpret_cast<const int2*>(X + cidx(L.rn[m]));
+    split_bin(zk.x, zk.y, zn.x, zn.y, L.A1[m], L.A2[m], L.B1[m], re, im);
+    reN = 0;
+}
+
+// One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.
+// 'buf' supplies the 480 samples (frames t-2, t-1, t) in 8-sample chunks.
+__global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
+    __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_FRAME_DW];
+    __shared__ int32_t Ps[4][264];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int32_t* X = Xs[wv];
+    int32_t* P = Ps[wv];
+    FeLane L;
+    fe_lane_init(L, lane);
+    const int32_t mean = lane < 40 ? a.mean[lane] : 0;
+    const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
+    const long long nfr = (long long)a.S * a.T;
+    for (long long f = (long long)blockIdx.x * 4 + wv; f < nfr; f += (long long)gridDim.x * 4) {
+        const int s = (int)(f / a.T), t = (int)(f - (long long)s * a.T);
+        // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30
+        if (lane < 60) {
+            const int fi = t - 2 + lane / 20, off = (lane % 20) * 8;
+            const int16_t* src = fi >= 0 ? a.pcm + ((size_t)s * a.T + fi) * 160 + off
+                                         : a.tail + (size_t)s * 320 + (fi + 2) * 160 + off;
+            const int4 raw = *reinterpret_cast<const int4*>(src);
+            const int16_t* sm = reinterpret_cast<const int16_t*>(&raw);
+            int32_t xv[8];
+            for (int j = 0; j < 8; ++j) xv[j] = (int32_t)L.win[j] * (int32_t)sm[j];
+            int32_t* q = X + cidx(4 * lane);
+            *reinterpret_cast<int4*>(q) = make_int4(xv[0], xv[1], xv[2], xv[3]);
+            *reinterpret_cast<int4*>(q + 4) = make_int4(xv[4], xv[5], xv[6], xv[7]);
+        } else {
+            int32_t* q = X + cidx(4 * lane);
+            *reinterpret_cast<int4*>(q) = make_int4(0, 0, 0, 0);
+            *reinterpret_cast<int4*>(q + 4) = make_int4(0, 0, 0, 0);
+        }
+        wave_lds_sync();
+        wave_cfft256(X, L, lane);
+        // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
+        for (int m = 0; m < 4; ++m) {
+            int32_t re, im, reN;
+            wave_split_bin(X, L, lane, m, re, im, reN);
+            P[lane + 64 * m] = pspec_of(re, im);
+            if (lane == 0 && m == 0) P[256] = pspec_of(reN, 0);
+            if (a.dbg_spec) {
+                int32_t* ds = a.dbg_spec + (size_t)f * 1024;
+                const int k = lane + 64 * m;
+                ds[2 * k] = re; ds[2 * k + 1] = im;
+                if (k) { ds[1024 - 2 * k] = re; ds[1024 - 2 * k + 1] = wsub(0, im); }
+                else { ds[512] = reN; ds[513] = 0; }
+            }
+        }
+        wave_lds_sync();
+        // ---- Mel (melSpecProc.c:6-27), log10 (fixlog10.c:53-61), normalise
+        if (lane < 40) {
+            int64_t mac = 0;
+            int o = L.moff;
+            for (int j = L.mstart; j <= L.mend; ++j, ++o) mac += (int64_t)nnsp_tbl_mel[o] * P[j];
+            const int32_t lg = log10_q15(sat32(mac >> 15));
+            if (a.dbg_log) a.dbg_log[(size_t)f * 40 + lane] = lg;
+            const int64_t d = (int64_t)lg - mean;
+            a.feats[(size_t)f * 40 + lane] = sat16((d * stdR) >> a.norm_shift);  // feature_module.c:67-73
+        }
+        wave_lds_sync();
+    }
+}
+
+// ============================================================================
+// NN: generic fc / lstm stack on int8 MFMA
+// ============================================================================
+#define NN_ASTRIDE 264   // int16 per stream row of an activation buffer (256 + pad)
+#define NN_HSTRIDE 136   // int16 per stream row of an LSTM h buffer (128 + pad)
+#define NN_CW 128        // int32 per stream row of an LSTM c buffer
+
+struct alignas(16) NnLds {
+    int16_t act[2][16][NN_ASTRIDE];
+    int16_t h[NN_MAX_LSTM][16][NN_HSTRIDE];
+    int32_t c[NN_MAX_LSTM][16][NN_CW];
+    int16_t tanh_tbl[384];
+    int32_t slides[16];
+    int32_t active[16];
+};
+
+// 16 int16 activations -> hi / lo' int8 planes: x = 256*hi + lo' + 128
+__device__ __forceinline__ void split_hilo(const int16_t* p, v4i& hi, v4i& lo) {
+    const int4 a = *reinterpret_cast<const int4*>(p);
+    const int4 b = *reinterpret_cast<const int4*>(p + 8);
+    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
+    hi.x = (int)__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, HS);
+    hi.y = (int)__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, HS);
+    hi.z = (int)__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, HS);
+    hi.w = (int)__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, HS);
+    lo.x = (int)(__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, LS) ^ 0x80808080u);
+    lo.y = (int)(__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, LS) ^ 0x80808080u);
+    lo.z = (int)(__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, LS) ^ 0x80808080u);
+    lo.w = (int)(__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, LS) ^ 0x80808080u);
+}
+
+__device__ __forceinline__ v4i mfma8(v4i a, v4i b, v4i c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ v4i load_frag(const uint8_t* base, int lane) {
+    return *reinterpret_cast<const v4i*>(base + 16 * lane);
+}
+
+// Fixed-point epilogue of affine_Krows (is_out=1): exact sum + bias, shift,
+// clamp (acc64) or wrap (acc32).  'pre' is the int64/int32 pre-bias value.
+__device__ __forceinline__ int32_t affine_out(int64_t pre, int16_t b, const NnLayer& Ly, int acc32) {
+    if (acc32) {
+        int32_t s = (int32_t)pre;
+        if (Ly.has_bias) s = wadd(s, Ly.bias_sh >= 0 ? wshl(b, Ly.bias_sh) : ((int32_t)b >> -Ly.bias_sh));
+        return shift32(s, Ly.out_sh);
+    }
+    int64_t s = pre;
+    if (Ly.has_bias) s += Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
+    return sat32(shift64(s, Ly.out_sh));
+}
+
+__device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) {
+    return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15(v, tt) : sigmoid_q15(v, tt));
+}
+
+// Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
+template <int MAXKT>
+__device__ __forceinline__ void load_b(const int16_t* buf, int stride, int nkt, int lane,
+                                       v4i (&bh)[MAXKT], v4i (&bl)[MAXKT]) {
+    const int sc = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt)
+        if (kt < nkt) split_hilo(buf + sc * stride + 64 * kt + 16 * q, bh[kt], bl[kt]);
+}
+
+__device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
+                              int16_t* out, const int16_t* tt, int lane) {
+    v4i bh[4], bl[4];
+    load_b<4>(in, NN_ASTRIDE, Ly.nkt, lane, bh, bl);
+    const int sc = lane & 15, q = lane >> 4;
+    const uint8_t* A = img.A + Ly.a_off;
+    for (int rt = 0; rt < Ly.nrt; ++rt) {
+        v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+            if (kt < Ly.nkt) {
+                const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
+                ah = mfma8(w, bh[kt], ah);
+                al = mfma8(w, bl[kt], al);
+            }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 16 * rt + 4 * q + i;
+            if (row >= Ly.rows) continue;
+            const int32_t sum = (ah[i] << 8) + al[i] + img.wsum[Ly.ep_off + row];
+            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
+            if (Ly.act == ACT_LINEAR)
+                reinterpret_cast<int32_t*>(out + sc * NN_ASTRIDE)[row] = v;
+            else
+                out[sc * NN_ASTRIDE + row] = act16(Ly.act, v, tt);
+        }
+    }
+}
+
+// lstm_8x16 (lstm.c:15-214): per 4-unit group, gates i,j,f,o; every group
+// reads the previous h (T6).  Rows are re-tiled so that lane group q of row
+// tile rt holds gates i,j,f,o of unit 4*rt+q in its 4 accumulator registers.
+__device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
+                                int16_t* out, int16_t* hbuf, int32_t* cbuf, const int16_t* tt,
+                                int lane, bool commit) {
+    v4i bxh[4], bxl[4], bhh[2], bhl[2];
+    load_b<4>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
+    load_b<2>(hbuf, NN_HSTRIDE, Ly.nkt_r, lane, bhh, bhl);
+    const int sc = lane & 15, q = lane >> 4;
+    const uint8_t* A = img.A + Ly.a_off;
+    const uint8_t* Ar = img.A + Ly.ar_off;
+    const int acc32 = img.acc32;
+    for (int rt = 0; rt < Ly.nrt; ++rt) {
+        v4i xh = {0, 0, 0, 0}, xl = {0, 0, 0, 0}, hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+            if (kt < Ly.nkt) {
+                const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
+                xh = mfma8(w, bxh[kt], xh);
+                xl = mfma8(w, bxl[kt], xl);
+            }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+            if (kt < Ly.nkt_r) {
+                const v4i w = load_frag(Ar + (size_t)(rt * Ly.nkt_r + kt) * 1024, lane);
+                hh = mfma8(w, bhh[kt], hh);
+                hl = mfma8(w, bhl[kt], hl);
+            }
+        const int u = 4 * rt + q;
+        if (u >= Ly.N) continue;
+        int16_t g[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 16 * rt + 4 * q + i;
+            const int32_t sx = (xh[i] << 8) + xl[i] + img.wsum[Ly.ep_off + row];
+            const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[Ly.ep_off + row];
+            // rc_Krows_8x16 (affine.c:348-407): x part, shift_64b(qi_rec - qi),
+            // then the recurrent part + bias with the is_out epilogue
+            int64_t pre;
+            if (acc32)
+                pre = (int64_t)wadd(shift32(sx, Ly.xs_sh), sh);
+            else
+                pre = shift64((int64_t)sx, Ly.xs_sh) + (int64_t)sh;
+            const int32_t v = affine_out(pre, img.bias[Ly.ep_off + row], Ly, acc32);
+            g[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+        }
+        const int32_t c_old = cbuf[sc * NN_CW + u];
+        const int32_t c_new = sat32(((int64_t)g[0] * g[1] + (int64_t)g[2] * c_old) >> 15);
+        const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
+        if (commit) cbuf[sc * NN_CW + u] = c_new;
+        out[sc * NN_ASTRIDE + u] = hv;
+    }
+}
+
+// Post-processing for one stream (nn_speech.c:146-227); lane-private state.
+struct PostState {
+    int16_t slides, trigger, argmax_last, pad0;
+    int16_t counts[8];
+    int16_t outputs[3], pad1;
+};
+
+__device__ __forceinline__ int argmax_lw(const int32_t* v, int n) {
+    int am = 0;
+    int32_t m = v[0];
+    for (int i = 1; i < n; ++i)
+        if (v[i] >= m) { m = v[i]; am = i; }
+    return am;
+}
+
+__device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, const int32_t* lg) {
+    if (img.nn_id == 0) {  // s2i_post_proc
+        ps.trigger = 0;
+        ps.outputs[0] = ps.outputs[1] = ps.outputs[2] = 0;
+        const int am = argmax_lw(lg, 7);
+        if (ps.argmax_last == 0 || ps.argmax_last == am) {
+            if (am != 0) {
+                ps.counts[am] = (int16_t)(ps.counts[am] + 1);
+                if (ps.counts[am] > img.th_count) {
+                    ps.trigger = 1;
+                    ps.outputs[0] = (int16_t)am;
+                    ps.outputs[1] = (int16_t)argmax_lw(lg + 7, 17);
+                    ps.outputs[2] = (int16_t)argmax_lw(lg + 24, 17);
+                }
+            }
+        } else {
+            for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
+        }
+        ps.argmax_last = (int16_t)am;
+    } else {  // binary_post_proc (T7: logits overwritten by exp2 values)
+        const int32_t mx = lg[0] > lg[1] ? lg[0] : lg[1];
+        int32_t e[2];
+        for (int i = 0; i < 2; ++i) e[i] = pwr2_q15(sat32(((int64_t)wsub(lg[i], mx) * 0xB8AA) >> 15));
+        const int32_t den = wadd(e[0], e[1]);
+        const int32_t lim = (int32_t)(((int64_t)(32768 - img.thresh_prob) * den) >> 15);
+        ps.counts[0] = e[0] <= lim ? (int16_t)(ps.counts[0] + 1) : (int16_t)0;
+        ps.trigger = ps.counts[0] >= img.th_count ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
+    __shared__ NnLds sm;
+    const int lane = threadIdx.x;
+    const int sc = lane & 15;
+    const int s0 = blockIdx.x * 16;
+    const int s = s0 + sc;
+    const bool valid = s < r.S;
+    for (int i = lane; i < 384; i += 64) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
+    // ---- LSTM state in (neural_nets.c:27-42 layout: h int16[N], c int32[N])
+    for (int l = 0; l < img.n_lstm; ++l) {
+        const int N = img.lstm_n[l];
+        for (int idx = lane; idx < 16 * N; idx += 64) {
+            const int st = idx / N, u = idx - st * N, gs = s0 + st;
+            const bool ok = gs < r.S;
+            sm.h[l][st][u] = ok ? r.h[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] : (int16_t)0;
+            sm.c[l][st][u] = ok ? r.c[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] : 0;
+        }
+    }
+    PostState ps = {};
+    if (lane < 16 && valid && r.post) ps = reinterpret_cast<const PostState*>(r.post)[s];
+    if (lane < 16) sm.slides[lane] = (valid && r.post) ? ps.slides : 1;
+    wave_lds_sync();
+    const int phase = r.mode == NN_MODE_DIRECT ? 0 : 1 - sm.slides[sc];
+    const int T = r.mode == NN_MODE_DIRECT ? 1 : r.T;
+    const int nsteps = (T + 1) / 2;
+    const int nl = r.nl_run;
+    if (lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
+
+    for (int j = 0; j < nsteps; ++j) {
+        const int t = 2 * j + phase;
+        const bool active = valid && t < T;
+        if (lane < 16) sm.active[lane] = active;
+        // ---- context window V[t..t+5], V = prev5 ++ feats (feature_module.c:54-57)
+        {
+            const int q = lane >> 4;
+            const int nch = r.mode == NN_MODE_DIRECT ? (img.L[0].K + 7) / 8 : 30;
+            for (int cch = q; cch < nch; cch += 4) {
+                const int m = cch / 5, part = cch - 5 * m;
+                int4 v = make_int4(0, 0, 0, 0);
+                if (active) {
+                    const int16_t* src;
+                    if (r.mode == NN_MODE_DIRECT) {
+                        src = r.direct_in + (size_t)s * NN_MAX_K + 8 * cch;
+                    } else {
+                        const int idx = t + m;
+                        src = idx < 5 ? r.prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part
+                                      : r.feats + ((size_t)s * r.T + (idx - 5)) * 40 + 8 * part;
+                    }
+                    v = *reinterpret_cast<const int4*>(src);
+                }
+                *reinterpret_cast<int4*>(&sm.act[0][sc][8 * cch]) = v;
+            }
+        }
+        wave_lds_sync();
+        int lst = 0;
+        for (int i = 0; i < nl; ++i) {
+            const NnLayer& Ly = img.L[i];
+            const int16_t* in = &sm.act[i & 1][0][0];
+            int16_t* out = &sm.act[(i + 1) & 1][0][0];
+            if (Ly.type == NN_LSTM) {
+                lstm_layer_mfma(img, Ly, in, out, &sm.h[lst][0][0], &sm.c[lst][0][0], sm.tanh_tbl,
+                                lane, active);
+                wave_lds_sync();
+                // h_state := output after all groups (lstm.c:205-206)
+                for (int idx = lane; idx < 16 * Ly.N; idx += 64) {
+                    const int st = idx / Ly.N, u = idx - st * Ly.N;
+                    if (sm.active[st]) sm.h[lst][st][u] = sm.act[(i + 1) & 1][st][u];
+                }
+                ++lst;
+            } else {
+                fc_layer_mfma(img, Ly, in, out, sm.tanh_tbl, lane);
+            }
+            wave_lds_sync();
+        }
+        const int16_t* fin = &sm.act[nl & 1][sc][0];
+        const int nout = img.L[nl - 1].N;
+        const bool lin = img.L[nl - 1].act == ACT_LINEAR;
+        if (active && r.logits) {
+            // each lane group q copies a quarter of its stream's outputs
+            const int q = lane >> 4;
+            if (r.mode == NN_MODE_DIRECT) {
+                if (lin) {
+                    int32_t* dst = reinterpret_cast<int32_t*>(r.logits) + (size_t)s * r.out_stride;
+                    for (int o = q; o < nout; o += 4) dst[o] = reinterpret_cast<const int32_t*>(fin)[o];
+                } else {
+                    int16_t* dst = reinterpret_cast<int16_t*>(r.logits) + (size_t)s * r.out_stride * 2;
+                    for (int o = q; o < nout; o += 4) dst[o] = fin[o];
+                }
+            } else {
+                int32_t* dst = r.logits + ((size_t)s * T + t) * nout;
+                for (int o = q; o < nout; o += 4)
+                    dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
+            }
+        }
+        if (r.mode != NN_MODE_DIRECT && lane < 16 && active) {
+            int32_t lg[64];
+            for (int o = 0; o < nout && o < 64; ++o)
+                lg[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
+            post_proc(ps, img, lg);
+            if (r.trig) {
+                r.trig[(size_t)s * T + t] = ps.trigger;
+                if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+            }
+        }
+        wave_lds_sync();
+    }
+    // ---- state out
+    for (int l = 0; l < img.n_lstm; ++l) {
+        const int N = img.lstm_n[l];
+        for (int idx = lane; idx < 16 * N; idx += 64) {
+            const int st = idx / N, u = idx - st * N, gs = s0 + st;
+            if (gs < r.S) {
+                r.h[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] = sm.h[l][st][u];
+                r.c[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] = sm.c[l][st][u];
+            }
+        }
+    }
+    if (r.mode != NN_MODE_DIRECT && lane < 16 && valid && r.post) {
+        ps.slides = (int16_t)(ps.slides ^ (T & 1));
+        reinterpret_cast<PostState*>(r.post)[s] = ps;
+    }
+}
+
+// prev5 := V[T..T+4] after the chunk; one block per stream, read all then write.
+__global__ __launch_bounds__(64) void ctx_roll_kernel(int16_t* prev5, const int16_t* feats, int S, int T) {
+    const int s = blockIdx.x, c = threadIdx.x;   // c: 8-int16 chunk of the 5x40 context
+    if (s >= S) return;
+    int4 v = make_int4(0, 0, 0, 0);
+    if (c < 25) {
+        const int m = c / 5, part = c % 5, idx = T + m;
+        v = idx < 5 ? *reinterpret_cast<const int4*>(prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part)
+                    : *reinterpret_cast<const int4*>(feats + ((size_t)s * T + idx - 5) * 40 + 8 * part);
+    }
+    __syncthreads();
+    if (c < 25) *reinterpret_cast<int4*>(prev5 + (size_t)s * 200 + 8 * c) = v;
+}
+
+// tail := last 320 samples of (tail ++ chunk), read all before writing.
+__global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int16_t* pcm, int S, int T) {
+    const int s = blockIdx.x;
+    if (s >= S) return;
+    int16_t v[5];
+    for (int k = 0; k < 5; ++k) {
+        const int i = threadIdx.x + 64 * k;
+        const long long pos = 160LL * T + i;   // index into tail(320) ++ pcm(160 T)
+        v[k] = pos < 320 ? tail[(size_t)s * 320 + pos] : pcm[(size_t)s * T * 160 + (pos - 320)];
+    }
+    __syncthreads();
+    for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
+}
+
+// ============================================================================
+// Stage kernels (legacy scalar API + per-stage parity tests)
+// ============================================================================
+__global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
+    __shared__ __attribute__((aligned(16))) int32_t X[FE_FRAME_DW];
+    const int lane = threadIdx.x;
+    FeLane L;
+    fe_lane_init(L, lane);
+    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+        int32_t* xb = x + (size_t)b * 512;
+        for (int c = lane; c < 256; c += 64) {
+            X[cidx(c)] = xb[2 * c];
+            X[cidx(c) + 1] = xb[2 * c + 1];
+        }
+        wave_lds_sync();
+        wave_cfft256(X, L, lane);
+        int32_t* yb = y + (size_t)b * 1024;
+        for (int m = 0; m < 4; ++m) {
+            int32_t re, im, reN;
+            wave_split_bin(X, L, lane, m, re, im, reN);
+            const int k = lane + 64 * m;
+            yb[2 * k] = re; yb[2 * k + 1] = im;
+            if (k) { yb[1024 - 2 * k] = re; yb[1024 - 2 * k + 1] = wsub(0, im); }
+            else { yb[512] = reN; yb[513] = 0; }
+        }
+        // pSrc holds the bit-reversed cFFT output afterwards (in-place CMSIS)
+        for (int c = lane; c < 256; c += 64) {
+            xb[2 * c] = X[cidx(rev8(c))];
+            xb[2 * c + 1] = X[cidx(rev8(c)) + 1];
+        }
+        wave_lds_sync();
+    }
+}
+
+__global__ void k_pspec(int32_t* y, const int32_t* x, int len, int n) {
+    const int b = blockIdx.y;
+    if (b >= n) return;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
+        const int32_t* xb = x + (size_t)b * 1024;
+        y[(size_t)b * 1024 + i] = pspec_of(xb[2 * i], xb[2 * i + 1]);
+    }
+}
+
+__global__ void k_mel(const int32_t* spec, int32_t* mel, int n) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int b = gid / 40, m = gid % 40;
+    if (b >= n) return;
+    int off = 0;
+    for (int i = 0; i < m; ++i) off += 2 + nnsp_tbl_mel[off + 1] - nnsp_tbl_mel[off] + 1;
+    const int st = nnsp_tbl_mel[off], en = nnsp_tbl_mel[off + 1];
+    int64_t mac = 0;
+    for (int j = st, o = off + 2; j <= en; ++j, ++o) mac += (int64_t)nnsp_tbl_mel[o] * spec[(size_t)b * 1024 + j];
+    mel[(size_t)b * 40 + m] = sat32(mac >> 15);
+}
+
+__global__ void k_log10(int32_t* out, const int32_t* x, int n, int add) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = wadd(log10_q15(x[i]), add);
+}
+
+__global__ void k_act(int type, const int32_t* x, void* y, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (type == ACT_LINEAR)
+        reinterpret_cast<int32_t*>(y)[i] = x[i];
+    else
+        reinterpret_cast<int16_t*>(y)[i] = type == ACT_RELU6 ? relu6_q12(x[i])
+                                          : (type == ACT_TANH ? tanh_q15(x[i], nnsp_tbl_tanh)
+                                                              : sigmoid_q15(x[i], nnsp_tbl_tanh));
+}
+
+// Scalar helpers of the legacy API: 0 ceiling, 1 compute_pwr2, 2 norm_oneTwo
+// (out[2i] = y, out[2i+1] = shift), 3 my_argmax over n (out[0]).
+__global__ void k_scalar(int op, const int32_t* in, int32_t* out, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (op == 3) {
+        if (i == 0) out[0] = argmax_lw(in, n);
+        return;
+    }
+    if (i >= n) return;
+    const int32_t x = in[i];
+    if (op == 0) out[i] = ceiling_q15(x);
+    else if (op == 1) out[i] = pwr2_q15(x);
+    else {
+        const uint32_t m = (uint32_t)x & 0x7FFFFFFFu;
+        int sh = 0;
+        if (m) sh = 15 - (31 - __clz((int)m));
+        out[2 * i] = sh >= 0 ? wshl(x, sh) : (x >> -sh);
+        out[2 * i + 1] = -sh;
+    }
+}
+
+// binary_post_proc / s2i_post_proc on one stream's state; est is overwritten
+// with the exp2 values for the binary case as the reference does (T7).
+__global__ void k_post(int nn_id, int thresh_prob, int th_count, void* post, int32_t* est) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    PostState* ps = reinterpret_cast<PostState*>(post);
+    NnImage im;
+    im.nn_id = nn_id; im.thresh_prob = thresh_prob; im.th_count = th_count;
+    int32_t lg[41];
+    const int n = nn_id == 0 ? 41 : 2;
+    for (int i = 0; i < n; ++i) lg[i] = est[i];
+    post_proc(*ps, im, lg);
+    if (nn_id != 0) {
+        const int32_t mx = lg[0] > lg[1] ? lg[0] : lg[1];
+        for (int i = 0; i < 2; ++i) est[i] = pwr2_q15(sat32(((int64_t)wsub(lg[i], mx) * 0xB8AA) >> 15));
+    }
+}
+
+// FeatureClass_setDefault (feature_module.c:26-45) for n streams: ctx slots 0-4.
+__global__ void k_fe_default(int16_t* prev5, int16_t* tail, const int32_t* mean, const int32_t* stdR,
+                             int norm_shift, const uint8_t* mask, int n) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int s = gid / 40, m = gid % 40;
+    if (s >= n || (mask && !mask[s])) return;
+    int64_t v = (int64_t)wsub(-147963, mean[m]);
+    const int16_t q = sat16((v * stdR[m]) >> norm_shift);
+    // after reset ctx = [q q q q q X]; the next frame sees V[0..4] = [q q q q X]
+    const int16_t X = prev5[((size_t)s * 5 + 4) * 40 + m];
+    for (int j = 0; j < 4; ++j) prev5[((size_t)s * 5 + j) * 40 + m] = q;
+    prev5[((size_t)s * 5 + 4) * 40 + m] = X;
+    for (int i = m; i < 320; i += 40) tail[(size_t)s * 320 + i] = 0;
+}
+
+// NNSPClass_reset post/NN part (nn_speech.c:57-72, neural_nets.c:27-42)
+__global__ void k_nn_default(int16_t* h, int32_t* c, void* post, int n_lstm, const uint8_t* mask, int n) {
+    const int s = blockIdx.x;
+    if (s >= n || (mask && !mask[s])) return;
+    for (int i = threadIdx.x; i < n_lstm * NN_MAX_W; i += blockDim.x) {
+        h[(size_t)s * n_lstm * NN_MAX_W + i] = 0;
+        c[(size_t)s * n_lstm * NN_MAX_W + i] = 0;
+    }
+    if (threadIdx.x == 0 && post) {
+        PostState* p = reinterpret_cast<PostState*>(post) + s;
+        p->slides = 1;
+        p->trigger = 0;
+        for (int i = 0; i < 7; ++i) p->counts[i] = 0;
+        p->outputs[0] = p->outputs[1] = p->outputs[2] = 0;
+        p->argmax_last = 0;
+    }
+}
+
+// Synthetic PCM (bench / tests): SplitMix64(seed, stream, sample) -> int16 in
+// [-amp, amp-1]; identical to oracle.synthetic_pcm.
+__global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp) {
+    const long long n = (long long)S * T * 160;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        const unsigned long long s = (unsigned long long)(i / (160LL * T)) + (unsigned long long)s0;
+        const unsigned long long k = (unsigned long long)(i % (160LL * T)) + (unsigned long long)t0 * 160ULL;
+        unsigned long long z = seed + s * 0x9E3779B97F4A7C15ULL + k * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+        z = z ^ (z >> 31);
+        out[i] = (int16_t)((long long)(z % (unsigned long long)(2 * amp)) - amp);
+    }
+}
+
+// ============================================================================
+// C-ABI launch layer (plain pointers; stream passed as void*)
+// ============================================================================
+static int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+extern "C" {
+
+int nnspk_launch_fe(const FeArgs* a, void* stream) {
+    if (a->S <= 0 || a->T <= 0) return 0;
+    const long long nfr = (long long)a->S * a->T;
+    long long blocks = (nfr + 3) / 4;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_nn(const NnImage* img, const NnRun* r, void* stream) {
+    if (r->S <= 0) return 0;
+    hipLaunchKernelGGL(nn_kernel, dim3((r->S + 15) / 16), dim3(64), 0, (hipStream_t)stream, *img, *r);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_ctx_roll(int16_t* prev5, const int16_t* feats, int S, int T, void* stream) {
+    hipLaunchKernelGGL(ctx_roll_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, prev5, feats, S, T);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_tail_roll(int16_t* tail, const int16_t* pcm, int S, int T, void* stream) {
+    hipLaunchKernelGGL(tail_roll_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, tail, pcm, S, T);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp,
+                           void* stream) {
+    hipLaunchKernelGGL(k_synth_pcm, dim3(4096), dim3(256), 0, (hipStream_t)stream, out, S, T, seed, s0, t0, amp);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_rfft(int32_t* x, int32_t* y, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_rfft, dim3(n < 4096 ? n : 4096), dim3(64), 0, (hipStream_t)stream, x, y, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_pspec(int32_t* y, const int32_t* x, int len, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_pspec, dim3((len + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, y, x, len, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_mel(const int32_t* spec, int32_t* mel, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_mel, dim3((n * 40 + 255) / 256), dim3(256), 0, (hipStream_t)stream, spec, mel, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_log10(int32_t* out, const int32_t* x, int n, int add, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_log10, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, out, x, n, add);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_act(int type, const int32_t* x, void* y, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_act, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, type, x, y, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_scalar(int op, const int32_t* in, int32_t* out, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_scalar, dim3(op == 3 ? 1 : (n + 255) / 256), dim3(256), 0, (hipStream_t)stream, op, in, out, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_post(int nn_id, int thresh_prob, int th_count, void* post, int32_t* est, void* stream) {
+    hipLaunchKernelGGL(k_post, dim3(1), dim3(64), 0, (hipStream_t)stream, nn_id, thresh_prob, th_count, post, est);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_fe_default(int16_t* prev5, int16_t* tail, const int32_t* mean, const int32_t* stdR,
+                            int norm_shift, const uint8_t* mask, int n, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_fe_default, dim3((n * 40 + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                       prev5, tail, mean, stdR, norm_shift, mask, n);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_nn_default(int16_t* h, int32_t* c, void* post, int n_lstm, const uint8_t* mask, int n,
+                            void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_nn_default, dim3(n), dim3(64), 0, (hipStream_t)stream, h, c, post, n_lstm, mask, n);
+    return ok(hipGetLastError());
+}
+
+// ---- thin runtime wrappers so the C host library needs no HIP headers -------
+int nnspk_malloc(void** p, size_t n) { return ok(hipMalloc(p, n ? n : 16)); }
+int nnspk_free(void* p) { return p ? ok(hipFree(p)) : 0; }
+int nnspk_memset(void* p, int v, size_t n, void* stream) { return ok(hipMemsetAsync(p, v, n, (hipStream_t)stream)); }
+int nnspk_h2d(void* d, const void* h, size_t n, void* stream) {
+    return ok(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, (hipStream_t)stream));
+}
+int nnspk_d2h(void* h, const void* d, size_t n, void* stream) {
+    return ok(hipMemcpyAsync(h, d, n, hipMemcpyDeviceToHost, (hipStream_t)stream));
+}
+int nnspk_d2d(void* d, const void* s, size_t n, void* stream) {
+    return ok(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+}
+int nnspk_sync(void* stream) { return ok(hipStreamSynchronize((hipStream_t)stream)); }
+int nnspk_device_count(int* n) { return ok(hipGetDeviceCount(n)); }
+int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
+int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
+const char* nnspk_error_string(int e) { return hipGetErrorString((hipError_t)e); }
+int nnspk_stream_create(void** s) { return ok(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); }
+int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
+int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
+int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }
+int nnspk_event_record(void* e, void* stream) { return ok(hipEventRecord((hipEvent_t)e, (hipStream_t)stream)); }
+int nnspk_event_elapsed(float* ms, void* a, void* b) {
+    return ok(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
+}
+int nnspk_device_info(int* cus, int* clock_khz, char* name, int name_len) {
+    int d = 0;
+    hipDeviceProp_t p;
+    int e = ok(hipGetDevice(&d));
+    if (e) return e;
+    e = ok(hipGetDeviceProperties(&p, d));
+    if (e) return e;
+    *cus = p.multiProcessorCount;
+    *clock_khz = p.clockRate;
+    if (name && name_len > 0) {
+        int i = 0;
+        for (; i < name_len - 1 && p.gcnArchName[i]; ++i) name[i] = p.gcnArchName[i];
+        name[i] = 0;
+    }
+    return 0;
+}
+
+}  // extern "C"

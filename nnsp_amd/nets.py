@@ -1,0 +1,205 @@
+"""Net descriptions, synthetic weights and the ns-nnsp weight byte layout.
+
+The three reference nets share one topology (python/nn_arch/def_*_nn_arch.txt,
+exported by python/c_code_table_converter.py): conv1d(k=6 frames, stride 2) as
+an FC over the 6x40 context -> LSTM -> FC -> FC -> FC.  Their shapes and
+fixed-point formats are the ``NeuralNetClass`` initialisers of
+evb/src/def_nn1_vad.c:29-110, def_nn2_kws_galaxy.c:29-111, def_nn0_s2i.c:29-110.
+
+The reference's weight tables are random (reference README.md:67, :111), so
+the benchmark and the GPU-box tests use seeded synthetic weights of exactly
+those shapes and formats, drawn with per-layer spreads that match the shipped
+tables (int8 std 3-30, int16 bias std 2e3-1.2e4).
+
+Byte layout (``pack_fc`` / ``pack_lstm``): the CMSIS-NN interleaved order the
+shipped ARM path walks (ns-nnsp/src/affine.c:80-149; producer
+python/nnsp_pack/c_weight_man.py:23-124, checked byte-for-byte by
+tests/test_layout.py when the reference is present).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+
+FC, LSTM = 0, 1
+RELU6, TANH, SIGMOID, LINEAR = 0, 1, 2, 3
+NN_ID = {"s2i": 0, "vad": 1, "kws": 2}
+
+
+@dataclass
+class NetSpec:
+    name: str
+    sizes: list[int]
+    types: list[int]
+    qk: list[int]
+    qi: list[int]
+    qb: list[int]
+    acts: list[int]
+    # synthetic-weight spreads per layer: (std of W, std of Wrec, bias mean, bias std)
+    spread: list[tuple] = field(default_factory=list)
+
+    @property
+    def nl(self) -> int:
+        return len(self.types)
+
+    @property
+    def nout(self) -> int:
+        return self.sizes[-1]
+
+    @property
+    def nn_id(self) -> int:
+        return NN_ID[self.name]
+
+
+SPECS = {
+    # evb/src/def_nn1_vad.c:31-41
+    "vad": NetSpec("vad", [240, 28, 28, 28, 28, 2], [FC, LSTM, FC, FC, FC],
+                   [7, 5, 5, 5, 7], [8, 15, 15, 12, 12], [14, 13, 15, 15, 15],
+                   [TANH, TANH, RELU6, RELU6, LINEAR],
+                   [(14, 0, 1700, 10000), (7, 15, 500, 8300), (12, 0, -2800, 8300),
+                    (19, 0, 5000, 4300), (30, 0, 0, 7000)]),
+    # evb/src/def_nn2_kws_galaxy.c:31-41
+    "kws": NetSpec("kws", [240, 64, 64, 64, 64, 2], [FC, LSTM, FC, FC, FC],
+                   [6, 5, 5, 5, 7], [8, 15, 15, 12, 12], [13, 14, 15, 15, 15],
+                   [TANH, TANH, RELU6, RELU6, LINEAR],
+                   [(14, 0, 400, 7300), (5, 12.5, 4600, 10000), (11, 0, 2900, 5500),
+                    (10, 0, 2200, 8500), (19, 0, 0, 2000)]),
+    # evb/src/def_nn0_s2i.c:31-41
+    "s2i": NetSpec("s2i", [240, 72, 72, 72, 72, 41], [FC, LSTM, FC, FC, FC],
+                   [7, 5, 4, 4, 5], [8, 15, 15, 12, 12], [14, 14, 14, 14, 14],
+                   [TANH, TANH, RELU6, RELU6, LINEAR],
+                   [(12.6, 0, -800, 7300), (2.8, 9.6, 4800, 8000), (5.2, 0, -3000, 6000),
+                    (11.3, 0, 2800, 6400), (12.9, 0, -11000, 12000)]),
+}
+
+# Cascade / post-processing parameters, evb/src/ParamsNNCntrl.h:8-21
+THRESH_PROB = 32767 >> 1
+THRESH_CNTS = 4
+LOOKBACK = 80
+TIMEOUT = 1000
+
+
+# --------------------------------------------------------------------------
+# byte layout
+# --------------------------------------------------------------------------
+def _pack_block(m: np.ndarray) -> list[np.ndarray]:
+    """One affine_Krows block of R<=4 rows over K columns (affine.c:74-184)."""
+    R, K = m.shape
+    out = []
+    for p in range(K // 2):
+        c0, c1 = m[:, 2 * p], m[:, 2 * p + 1]
+        if R == 4:
+            out.append(np.array([c0[0], c0[1], c1[0], c1[1], c0[2], c0[3], c1[2], c1[3]]))
+        elif R == 3:
+            out.append(np.array([c0[0], c0[1], c1[0], c1[1], c0[2], c1[2]]))
+        elif R == 2:
+            out.append(np.array([c0[0], c0[1], c1[0], c1[1]]))
+        else:
+            out.append(np.array([c0[0], c1[0]]))
+    if K % 2:
+        out.append(m[:, K - 1].copy())
+    return out
+
+
+def pack_fc(w: np.ndarray) -> np.ndarray:
+    """Natural W[N][K] int8 -> interleaved byte stream."""
+    N = w.shape[0]
+    parts = []
+    for r0 in range(0, N, 4):
+        parts += _pack_block(w[r0:r0 + 4])
+    return np.concatenate(parts).astype(np.int8)
+
+
+def unpack_fc(blob: np.ndarray, N: int, K: int) -> np.ndarray:
+    """Inverse of pack_fc (via the packed order of element indices)."""
+    ids = _pack_index(N, K)
+    out = np.zeros(N * K, dtype=np.int8)
+    out[ids] = np.asarray(blob, dtype=np.int8)[: N * K]
+    return out.reshape(N, K)
+
+
+def _pack_index(N: int, K: int) -> np.ndarray:
+    ar = np.arange(N * K).reshape(N, K)
+    parts = []
+    for r0 in range(0, N, 4):
+        parts += _pack_block(ar[r0:r0 + 4])
+    return np.concatenate(parts)
+
+
+def pack_lstm(w: np.ndarray) -> np.ndarray:
+    """Natural gate-major W[4N][K] (rows: i block, j block, f block, o block;
+    python/c_code_table_converter.py:64-73 order) -> per-4-unit-group
+    [i rows][j rows][f rows][o rows] interleaved stream (c_weight_man.py:61-92)."""
+    N = w.shape[0] // 4
+    g = [w[k * N:(k + 1) * N] for k in range(4)]
+    parts = []
+    for u0 in range(0, N, 4):
+        for k in range(4):
+            parts += _pack_block(g[k][u0:u0 + 4])
+    return np.concatenate(parts).astype(np.int8)
+
+
+def pack_lstm_bias(b: np.ndarray) -> np.ndarray:
+    N = b.shape[0] // 4
+    g = [b[k * N:(k + 1) * N] for k in range(4)]
+    parts = []
+    for u0 in range(0, N, 4):
+        for k in range(4):
+            parts.append(g[k][u0:u0 + 4])
+    return np.concatenate(parts).astype(np.int16)
+
+
+# --------------------------------------------------------------------------
+# synthetic nets
+# --------------------------------------------------------------------------
+@dataclass
+class NetData:
+    spec: NetSpec
+    W: list            # natural int8 matrices (W[N][K]; LSTM: [4N][K] gate-major i,j,f,o)
+    Wr: list           # LSTM recurrent [4N][N] or None
+    B: list            # natural int16 biases (LSTM: [4N] gate-major)
+    mean: np.ndarray   # int32[40]
+    stdR: np.ndarray   # int32[40]
+
+    def packed(self):
+        """Byte streams exactly as a def_nn*.c file holds them."""
+        Wp, Wrp, Bp = [], [], []
+        for i, t in enumerate(self.spec.types):
+            if t == LSTM:
+                Wp.append(pack_lstm(self.W[i]))
+                Wrp.append(pack_lstm(self.Wr[i]))
+                Bp.append(pack_lstm_bias(self.B[i]))
+            else:
+                Wp.append(pack_fc(self.W[i]))
+                Wrp.append(None)
+                Bp.append(self.B[i].astype(np.int16))
+        return Wp, Wrp, Bp
+
+
+def synth_net(name: str, seed: int = 1234) -> NetData:
+    spec = SPECS[name]
+    rng = np.random.default_rng([seed, spec.nn_id])
+
+    def i8(shape, std):
+        return np.clip(np.round(rng.normal(0.0, std, shape)), -128, 127).astype(np.int8)
+
+    def i16(n, mean, std):
+        return np.clip(np.round(rng.normal(mean, std, n)), -32768, 32767).astype(np.int16)
+
+    W, Wr, B = [], [], []
+    for i, t in enumerate(spec.types):
+        K, N = spec.sizes[i], spec.sizes[i + 1]
+        sw, swr, bm, bs = spec.spread[i]
+        if t == LSTM:
+            W.append(i8((4 * N, K), sw))
+            Wr.append(i8((4 * N, N), swr))
+            B.append(i16(4 * N, bm, bs))
+        else:
+            W.append(i8((N, K), sw))
+            Wr.append(None)
+            B.append(i16(N, bm, bs))
+    # feature statistics in the ranges of the shipped tables (def_nn*.c:8-9)
+    mean = np.sort(rng.uniform(-110000, -25000, 40)).astype(np.int32)[::-1].copy()
+    stdR = rng.uniform(16500, 24500, 40).astype(np.int32)
+    return NetData(spec, W, Wr, B, mean, stdR)

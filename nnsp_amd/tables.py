@@ -1,0 +1,180 @@
+"""Constant-table generator for the ns-nnsp hot path.
+
+Every constant table the fixed-point path needs is regenerated here from a
+closed-form rule; nothing is copied from the reference.  Each rule was pinned
+against the reference's own table bytes in the build container (see
+tests/test_tables.py, which re-checks all of them whenever /root/reference is
+present):
+
+=========================  ==========================================  ==========================================
+table                      reference location                          rule (exact, all entries)
+=========================  ==========================================  ==========================================
+stft window (480 x i16)    ns-nnsp/src/window_stft_coef.c:6            floor(sqrt(hop/win*(1-cos(2*pi*n/win)))*2^15)
+                           (generator python/nnsp_pack/gen_stft_win.py:14-19)
+mel banks (534 x i16)      ns-nnsp/src/melSpec_coeff.c:5               packed [start,end,coef...] per bank,
+                           (generator python/nnsp_pack/mel.py:10-50)   coef = floor(tri * 2^15)
+log10 interp (256 x i16)   ns-nnsp/src/fixlog10.c:6                    [floor(ln(1+k/128)*2^15), min(floor(2^15/(1+k/128)),32767)]
+tanh interp (384 x i16)    ns-nnsp/src/activation.c:5                  c=(512+1024k)/2^15: [floor(tanh c*2^15), floor((1-tanh^2 c)*2^15)]
+cfft twiddles (384 x q31)  CMSIS-DSP 1.10.0 twiddleCoef_256_q31         floor(x*2^31 + 0.05), x = cos/sin(2*pi*i/256)
+                           (binary only: evb/libs/libCMSISDSP.a)
+rfft split A/B (q31)       CMSIS-DSP 1.10.0 realCoefAQ31/realCoefBQ31   round(0.5*(1-+sin t)*2^31), round(-+0.5*cos t*2^31)
+bit reversal               CMSIS-DSP armBitRevIndexTable_fixed_256      8-bit bit reversal of the 256 complex slots
+=========================  ==========================================  ==========================================
+
+The twiddle rule ("floor(x*2^31 + 0.05)") is empirical: it is the rule that
+reproduces all 384 words of the shipped ``twiddleCoef_256_q31`` data section
+(plain round() misses 171 words, plain floor() 18).
+
+``write_header`` emits ``nnsp_amd/csrc/gen/nnsp_tables.h`` used by both the
+HIP kernels / host library and the test oracle.
+"""
+from __future__ import annotations
+
+import math
+import os
+
+import numpy as np
+
+WIN_LEN = 480      # LEN_STFT_WIN_COEFF, ambiq_nnsp_const.h:4
+HOP = 160          # LEN_STFT_HOP, ambiq_nnsp_const.h:5
+FFT_LEN = 512      # LEN_FFT_NNSP, ambiq_nnsp_const.h:3
+N_MEL = 40         # NUM_MELBANKS, ambiq_nnsp_const.h:6
+FS = 16000         # SAMPLING_RATE, ambiq_nnsp_const.h:9
+
+
+def stft_window() -> np.ndarray:
+    n = np.arange(WIN_LEN)
+    w = np.sqrt(HOP / WIN_LEN * (1.0 - np.cos(2.0 * np.pi / WIN_LEN * n)))
+    return np.minimum(np.floor(w * 2 ** 15), 32767).astype(np.int16)
+
+
+def mel_bank_packed() -> np.ndarray:
+    hi = 2595.0 * np.log10(1.0 + (FS / 2) / 700.0)
+    mel_pts = np.linspace(0.0, hi, N_MEL + 2)
+    hz = 700.0 * (10.0 ** (mel_pts / 2595.0) - 1.0)
+    edge = np.floor((FFT_LEN + 1) * hz / FS)
+    out: list[int] = []
+    for b in range(1, N_MEL + 1):
+        lo, mid, up = edge[b - 1], edge[b], edge[b + 1]
+        tri = np.zeros(FFT_LEN // 2 + 1)
+        for k in range(int(lo), int(mid)):
+            tri[k] = (k - lo) / (mid - lo)
+        for k in range(int(mid), int(up)):
+            tri[k] = (up - k) / (up - mid)
+        out += [int(lo) + 1, int(up) - 1]
+        for k in range(int(lo) + 1, int(up)):
+            out.append(int(min(max(math.floor(tri[k] * 2 ** 15), -32768), 32767)))
+    return np.asarray(out, dtype=np.int16)
+
+
+def log_interp() -> np.ndarray:
+    k = np.arange(128)
+    val = np.floor(np.log(1.0 + k / 128.0) * 2 ** 15)
+    slope = np.minimum(np.floor(2 ** 15 / (1.0 + k / 128.0)), 32767)
+    return np.stack([val, slope], 1).reshape(-1).astype(np.int16)
+
+
+def tanh_interp() -> np.ndarray:
+    k = np.arange(192)
+    c = (512.0 + 1024.0 * k) / 2 ** 15
+    t = np.tanh(c)
+    val = np.floor(t * 2 ** 15)
+    der = np.floor((1.0 - t * t) * 2 ** 15)
+    return np.minimum(np.stack([val, der], 1).reshape(-1), 32767).astype(np.int16)
+
+
+def cfft256_twiddles() -> np.ndarray:
+    i = np.arange(192)
+    v = np.stack([np.cos(2 * np.pi * i / 256), np.sin(2 * np.pi * i / 256)], 1).reshape(-1) * 2.0 ** 31
+    return np.clip(np.floor(v + 0.05), -2 ** 31, 2 ** 31 - 1).astype(np.int32)
+
+
+def rfft_split_full(n: int = 4096) -> tuple[np.ndarray, np.ndarray]:
+    """Full CMSIS realCoefAQ31 / realCoefBQ31 (n complex entries each)."""
+    i = np.arange(n)
+    th = 2 * np.pi * i / (2 * n)
+
+    def q31(x):
+        return np.clip(np.round(x * 2.0 ** 31), -2 ** 31, 2 ** 31 - 1).astype(np.int64)
+
+    a = np.stack([q31(0.5 * (1 - np.sin(th))), q31(-0.5 * np.cos(th))], 1).reshape(-1)
+    b = np.stack([q31(0.5 * (1 + np.sin(th))), q31(0.5 * np.cos(th))], 1).reshape(-1)
+    return a.astype(np.int32), b.astype(np.int32)
+
+
+def rfft512_split_coefs() -> np.ndarray:
+    """The (A_re, A_im, B_re) triple the 512-point split uses for bins k=0..255.
+
+    arm_rfft_init_q31(512) sets twidCoefRModifier = 8192/512 = 16, so bin k
+    reads realCoefAQ31[2*16*k], [2*16*k+1] and realCoefBQ31[2*16*k].
+    """
+    a, b = rfft_split_full()
+    k = np.arange(256)
+    return np.stack([a[32 * k], a[32 * k + 1], b[32 * k]], 1).astype(np.int32)
+
+
+def bitrev8() -> np.ndarray:
+    return np.array([int(f"{i:08b}"[::-1], 2) for i in range(256)], dtype=np.int32)
+
+
+def _c_array(ctype: str, name: str, vals, per_line: int = 12) -> str:
+    vals = [int(v) for v in np.asarray(vals).reshape(-1)]
+    lines = []
+    for i in range(0, len(vals), per_line):
+        lines.append("    " + ", ".join(str(v) for v in vals[i:i + per_line]) + ",")
+    return f"static const {ctype} {name}[{len(vals)}] = {{\n" + "\n".join(lines) + "\n};\n"
+
+
+def header_text() -> str:
+    mel = mel_bank_packed()
+    parts = [
+        "/* GENERATED by nnsp_amd/tables.py -- do not edit.\n"
+        " * Closed-form regenerations of the ns-nnsp / CMSIS-DSP constant tables;\n"
+        " * exactness vs the reference is checked by tests/test_tables.py. */\n",
+        "#ifndef NNSP_GEN_TABLES_H\n#define NNSP_GEN_TABLES_H\n#include <stdint.h>\n",
+        f"#define NNSP_TBL_MEL_LEN {len(mel)}\n",
+        _c_array("int16_t", "nnsp_tbl_window", stft_window()),
+        _c_array("int16_t", "nnsp_tbl_mel", mel),
+        _c_array("int16_t", "nnsp_tbl_log", log_interp()),
+        _c_array("int16_t", "nnsp_tbl_tanh", tanh_interp()),
+        _c_array("int32_t", "nnsp_tbl_tw256", cfft256_twiddles(), 6),
+        _c_array("int32_t", "nnsp_tbl_split", rfft512_split_coefs(), 6),
+        "#endif\n",
+    ]
+    return "\n".join(parts)
+
+
+def export_text() -> str:
+    """C file exporting the tables under the reference library's symbol names
+    (window_stft_coef.c:3-6, melSpec_coeff.c:3-5, fixlog10.c:6, activation.c:5)."""
+    def arr(ctype, name, vals):
+        return _c_array(ctype, name, vals).replace("static const ", "").replace(f"{ctype} {name}", f"{ctype} {name}")
+    mel = mel_bank_packed()
+    return "\n".join([
+        "/* GENERATED by nnsp_amd/tables.py -- do not edit. */",
+        "#include <stdint.h>",
+        f"const int16_t len_stft_win_coeff = {WIN_LEN};",
+        f"const int16_t hop = {HOP};",
+        f"const int16_t num_mfltrBank = {N_MEL};",
+        arr("const int16_t", "stft_win_coeff", stft_window()),
+        arr("const int16_t", "mfltrBank_coeff", mel),
+        arr("const int16_t", "log_tayler_coeff", log_interp()),
+        arr("int16_t", "coeffs_tanh", tanh_interp()),
+    ])
+
+
+def write_header(path: str | None = None) -> str:
+    if path is None:
+        path = os.path.join(os.path.dirname(__file__), "csrc", "gen", "nnsp_tables.h")
+    for p, text in ((path, header_text()),
+                    (os.path.join(os.path.dirname(path), "nnsp_tables_export.c"), export_text())):
+        old = open(p).read() if os.path.exists(p) else None
+        if old != text:
+            os.makedirs(os.path.dirname(p), exist_ok=True)
+            with open(p, "w") as f:
+                f.write(text)
+    return path
+
+
+if __name__ == "__main__":
+    print(write_header())

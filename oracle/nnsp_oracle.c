@@ -1,0 +1,663 @@
+/*
+ * nnsp_oracle.c -- TEST INFRASTRUCTURE ONLY (see nnsp_oracle.h).
+ *
+ * Scalar restatement of the ns-nnsp ARM_OPTIMIZED=1 per-frame path and of
+ * CMSIS-DSP 1.10.0's arm_rfft_q31.  Written from the reference's behaviour;
+ * every block cites the reference file:line it follows.  Signed arithmetic
+ * that wraps on the Cortex-M4 wraps here too (explicit unsigned casts; the
+ * file is also compiled with -fwrapv).
+ */
+#include "nnsp_oracle.h"
+
+#include <string.h>
+
+#include "../nnsp_amd/csrc/gen/nnsp_tables.h"
+
+typedef int64_t i64;
+typedef int32_t i32;
+typedef int16_t i16;
+typedef uint32_t u32;
+
+static inline i32 w32(i64 v) { return (i32)(u32)(uint64_t)v; }
+static inline i32 add(i32 a, i32 b) { return (i32)((u32)a + (u32)b); }
+static inline i32 sub(i32 a, i32 b) { return (i32)((u32)a - (u32)b); }
+static inline i32 shl(i32 a, int s) { return (i32)((u32)a << s); }
+static inline i32 sat32(i64 v) { return v > INT32_MAX ? INT32_MAX : (v < INT32_MIN ? INT32_MIN : (i32)v); }
+static inline i16 sat16(i64 v) { return v > 32767 ? 32767 : (v < -32768 ? -32768 : (i16)v); }
+
+/* ------------------------------------------------------------------------
+ * CMSIS-DSP 1.10.0 arm_rfft_q31, forward, 512 points, bit reversal on
+ * (called from ns-nnsp/src/fft_arm.c:10-19).  Restated from the published
+ * algorithm: arm_cfft_q31 (256-pt) -> arm_radix4_butterfly_q31 ->
+ * arm_bitreversal_32 -> arm_split_rfft_q31.  Rounding macros are those of the
+ * vendored evb/includes/extern/CMSIS/CMSIS_5-5.9.0/CMSIS/DSP/Include/dsp/
+ * none.h:185-194 (SMMLAR / SMMLSR / SMMULR).
+ * ---------------------------------------------------------------------- */
+static inline i32 mhi(i32 a, i32 b) { return (i32)(((i64)a * (i64)b) >> 32); }
+
+/* arm_radix4_butterfly_q31: radix-4 DIF over 256 interleaved complex q31. */
+static void cfft256_radix4(i32 *p)
+{
+    const i32 *tw = nnsp_tbl_tw256;
+    /* first stage: 4 guard bits (inputs >> 4), products re-scaled << 1 */
+    for (int i0 = 0; i0 < 64; ++i0) {
+        const int i1 = i0 + 64, i2 = i0 + 128, i3 = i0 + 192;
+        const i32 xa = p[2 * i0] >> 4, ya = p[2 * i0 + 1] >> 4;
+        const i32 xb = p[2 * i1] >> 4, yb = p[2 * i1 + 1] >> 4;
+        const i32 xc = p[2 * i2] >> 4, yc = p[2 * i2 + 1] >> 4;
+        const i32 xd = p[2 * i3] >> 4, yd = p[2 * i3 + 1] >> 4;
+        i32 r1 = add(xa, xc), r2 = sub(xa, xc), s1 = add(ya, yc), s2 = sub(ya, yc);
+        i32 t1 = add(xb, xd), t2 = add(yb, yd);
+        p[2 * i0] = add(r1, t1);
+        p[2 * i0 + 1] = add(s1, t2);
+        r1 = sub(r1, t1);
+        s1 = sub(s1, t2);
+        t1 = sub(yb, yd);
+        t2 = sub(xb, xd);
+        const int k = i0; /* ia1, modifier 1 */
+        const i32 co1 = tw[2 * k], si1 = tw[2 * k + 1];
+        const i32 co2 = tw[4 * k], si2 = tw[4 * k + 1];
+        const i32 co3 = tw[6 * k], si3 = tw[6 * k + 1];
+        p[2 * i1] = shl(add(mhi(r1, co2), mhi(s1, si2)), 1);
+        p[2 * i1 + 1] = shl(sub(mhi(s1, co2), mhi(r1, si2)), 1);
+        r1 = add(r2, t1);
+        r2 = sub(r2, t1);
+        s1 = sub(s2, t2);
+        s2 = add(s2, t2);
+        p[2 * i2] = shl(add(mhi(r1, co1), mhi(s1, si1)), 1);
+        p[2 * i2 + 1] = shl(sub(mhi(s1, co1), mhi(r1, si1)), 1);
+        p[2 * i3] = shl(add(mhi(r2, co3), mhi(s2, si3)), 1);
+        p[2 * i3 + 1] = shl(sub(mhi(s2, co3), mhi(r2, si3)), 1);
+    }
+    /* two middle stages: sums >> 2, products >> 1 */
+    int n2 = 64, mod = 4;
+    for (int stage = 0; stage < 2; ++stage) {
+        const int n1 = n2;
+        n2 >>= 2;
+        for (int j = 0; j < n2; ++j) {
+            const int k = j * mod;
+            const i32 co1 = tw[2 * k], si1 = tw[2 * k + 1];
+            const i32 co2 = tw[4 * k], si2 = tw[4 * k + 1];
+            const i32 co3 = tw[6 * k], si3 = tw[6 * k + 1];
+            for (int i0 = j; i0 < 256; i0 += n1) {
+                const int i1 = i0 + n2, i2 = i1 + n2, i3 = i2 + n2;
+                const i32 xa = p[2 * i0], ya = p[2 * i0 + 1];
+                const i32 xb = p[2 * i1], yb = p[2 * i1 + 1];
+                const i32 xc = p[2 * i2], yc = p[2 * i2 + 1];
+                const i32 xd = p[2 * i3], yd = p[2 * i3 + 1];
+                i32 r1 = add(xa, xc), r2 = sub(xa, xc), s1 = add(ya, yc), s2 = sub(ya, yc);
+                i32 t1 = add(xb, xd), t2 = add(yb, yd);
+                p[2 * i0] = add(r1, t1) >> 2;
+                p[2 * i0 + 1] = add(s1, t2) >> 2;
+                r1 = sub(r1, t1);
+                s1 = sub(s1, t2);
+                t1 = sub(yb, yd);
+                t2 = sub(xb, xd);
+                p[2 * i1] = add(mhi(r1, co2), mhi(s1, si2)) >> 1;
+                p[2 * i1 + 1] = sub(mhi(s1, co2), mhi(r1, si2)) >> 1;
+                r1 = add(r2, t1);
+                r2 = sub(r2, t1);
+                s1 = sub(s2, t2);
+                s2 = add(s2, t2);
+                p[2 * i2] = add(mhi(r1, co1), mhi(s1, si1)) >> 1;
+                p[2 * i2 + 1] = sub(mhi(s1, co1), mhi(r1, si1)) >> 1;
+                p[2 * i3] = add(mhi(r2, co3), mhi(s2, si3)) >> 1;
+                p[2 * i3 + 1] = sub(mhi(s2, co3), mhi(r2, si3)) >> 1;
+            }
+        }
+        mod <<= 2;
+    }
+    /* last stage: unscaled, outputs written in a, c, b, d order */
+    for (int g = 0; g < 64; ++g) {
+        i32 *q = p + 8 * g;
+        const i32 xa = q[0], ya = q[1], xb = q[2], yb = q[3];
+        const i32 xc = q[4], yc = q[5], xd = q[6], yd = q[7];
+        q[0] = add(add(xa, xb), add(xc, xd));
+        q[1] = add(add(ya, yb), add(yc, yd));
+        q[2] = sub(add(xa, xc), add(xb, xd));
+        q[3] = sub(add(ya, yc), add(yb, yd));
+        q[4] = sub(add(xa, yb), add(xc, yd));
+        q[5] = sub(add(ya, xd), add(xb, yc));
+        q[6] = sub(add(xa, yd), add(yb, xc));
+        q[7] = sub(add(ya, xb), add(yc, xd));
+    }
+}
+
+static int rev8(int i)
+{
+    int r = 0;
+    for (int b = 0; b < 8; ++b) r |= ((i >> b) & 1) << (7 - b);
+    return r;
+}
+
+/* multAcc_32x32_keep32_R / multSub_32x32_keep32_R contributions */
+static inline i32 rnd_add(i32 x, i32 c) { return (i32)(((i64)x * c + 0x80000000LL) >> 32); }
+static inline i32 rnd_sub(i32 x, i32 c) { return (i32)(-(((i64)x * c + 0x7FFFFFFFLL) >> 32)); }
+
+void or_rfft512(int32_t *x, int32_t *y)
+{
+    cfft256_radix4(x);
+    for (int i = 0; i < 256; ++i) { /* arm_bitreversal_32 */
+        const int r = rev8(i);
+        if (i < r) {
+            i32 t = x[2 * i]; x[2 * i] = x[2 * r]; x[2 * r] = t;
+            t = x[2 * i + 1]; x[2 * i + 1] = x[2 * r + 1]; x[2 * r + 1] = t;
+        }
+    }
+    /* arm_split_rfft_q31, modifier 16 */
+    for (int k = 1; k < 256; ++k) {
+        const i32 A1 = nnsp_tbl_split[3 * k], A2 = nnsp_tbl_split[3 * k + 1];
+        const i32 B1 = nnsp_tbl_split[3 * k + 2];
+        const i32 xr = x[2 * k], xi = x[2 * k + 1];
+        const i32 yr = x[512 - 2 * k], yi = x[512 - 2 * k + 1];
+        i32 re = rnd_add(xr, A1);
+        re = add(re, rnd_sub(xi, A2));
+        re = add(re, rnd_sub(yi, A2));
+        re = add(re, rnd_add(yr, B1));
+        i32 im = rnd_add(xr, A2);
+        im = add(im, rnd_add(xi, A1));
+        im = add(im, rnd_sub(yi, B1));
+        im = add(im, rnd_sub(yr, A2));
+        y[2 * k] = re;
+        y[2 * k + 1] = im;
+        y[1024 - 2 * k] = re;
+        y[1024 - 2 * k + 1] = sub(0, im);
+    }
+    y[512] = sub(x[0], x[1]) >> 1;
+    y[513] = 0;
+    y[0] = add(x[0], x[1]) >> 1;
+    y[1] = 0;
+}
+
+/* ------------------------------------------------------------------------
+ * Front end (ns-nnsp/src/feature_module.c, spectrogram_module.c,
+ * melSpecProc.c, fixlog10.c)
+ * ---------------------------------------------------------------------- */
+void or_spec2pspec(int32_t *y, const int32_t *x, int n) /* spectrogram_module.c:79-92 */
+{
+    for (int i = 0; i < n; ++i) {
+        const i64 e = (i64)x[2 * i] * x[2 * i] + (i64)x[2 * i + 1] * x[2 * i + 1];
+        y[i] = (i32)(e >> 27); /* truncating cast (T3) */
+    }
+}
+
+void or_mel(const int32_t *pspec, int32_t *mel) /* melSpecProc.c:6-27 */
+{
+    const i16 *t = nnsp_tbl_mel;
+    for (int b = 0; b < 40; ++b) {
+        const int lo = *t++, hi = *t++;
+        i64 acc = 0;
+        for (int j = lo; j <= hi; ++j) acc += (i64)(*t++) * pspec[j];
+        mel[b] = sat32(acc >> 15);
+    }
+}
+
+int32_t or_log10(int32_t x) /* fixlog10.c:31-50 with norm_oneTwo :9-28 */
+{
+    if (x == 0) x = 1;
+    int sh = 0;
+    for (int b = 30; b >= 0; --b)
+        if ((x >> b) & 1) { sh = 15 - b; break; }
+    const i32 y = sh >= 0 ? shl(x, sh) : (x >> -sh);
+    const int e = -sh;
+    i32 kx = (y - 32768) >> 8;
+    const i32 dx = (y - 32768) - (kx << 8);
+    /* x < 0 (only reachable through the T3 wrap) indexes outside the table in
+     * the reference; both oracle and kernel clamp the segment index. */
+    if (kx < 0) kx = 0;
+    if (kx > 127) kx = 127;
+    i32 v = nnsp_tbl_log[2 * kx] + ((nnsp_tbl_log[2 * kx + 1] * dx) >> 15);
+    v = (i32)(((i64)v * 0x3796) >> 15);
+    return add(v, 0x2688 * e);
+}
+
+void or_fe_reset(or_stream *st, const or_cfg *cfg) /* feature_module.c:26-45 */
+{
+    memset(st->buf, 0, sizeof st->buf);
+    for (int i = 0; i < 40; ++i) {
+        i64 v = (i64)sub(-147963, cfg->mean[i]);
+        v = (v * cfg->stdR[i]) >> (30 - cfg->qbit_out);
+        const i16 q = sat16(v);
+        for (int j = 0; j < 5; ++j) st->ctx[i + 40 * j] = q; /* slot 5 kept (T4) */
+    }
+}
+
+void or_fe_exec(or_stream *st, const or_cfg *cfg, const int16_t *pcm) /* feature_module.c:47-74 */
+{
+    i32 x[514], spec[1024], mel[40];
+    memmove(st->ctx, st->ctx + 40, 200 * sizeof(i16));
+    memmove(st->buf, st->buf + 160, 320 * sizeof(i16)); /* spectrogram_module.c:103-108 */
+    memcpy(st->buf + 320, pcm, 160 * sizeof(i16));
+    for (int i = 0; i < 480; ++i) x[i] = (i32)nnsp_tbl_window[i] * st->buf[i]; /* Q30 */
+    for (int i = 480; i < 514; ++i) x[i] = 0;
+    or_rfft512(x, spec);
+    or_spec2pspec(spec, spec, 257);
+    or_mel(spec, mel);
+    for (int i = 0; i < 40; ++i) {
+        const i64 d = (i64)or_log10(mel[i]) - cfg->mean[i];
+        st->ctx[200 + i] = sat16((d * cfg->stdR[i]) >> (30 - cfg->qbit_out));
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * Activations (ns-nnsp/src/activation.c)
+ * ---------------------------------------------------------------------- */
+static i16 tanh1(i32 x) /* activation.c:31-69 */
+{
+    const int neg = x < 0;
+    const i32 a = neg ? sub(0, x) : x;
+    i16 y;
+    if (a >= (5 << 15)) {
+        y = 0x7fff;
+    } else {
+        i32 kx = sub(a, 512) >> 10;
+        if (kx < 0) kx = 0;
+        if (kx > 191) kx = 191; /* only INT32_MIN reaches here; reference reads OOB */
+        const i32 dx = a - 512 - (kx << 10);
+        const i32 v = nnsp_tbl_tanh[2 * kx] + ((dx * nnsp_tbl_tanh[2 * kx + 1]) >> 15);
+        y = (i16)(v > 0 ? v : 0);
+    }
+    return neg ? (i16)-y : y;
+}
+
+static i16 sigm1(i32 x) { return (i16)((tanh1(x >> 1) >> 1) + 16384); } /* activation.c:72-87 */
+
+static i16 relu6_1(i32 x) /* activation.c:6-17 */
+{
+    i32 v = x >> 3;
+    if (v > 24576) v = 24576;
+    return (i16)(v < 0 ? 0 : v);
+}
+
+void or_act(int32_t type, const int32_t *x, void *y, int32_t n)
+{
+    for (int i = 0; i < n; ++i) {
+        switch (type) {
+        case OR_RELU6: ((i16 *)y)[i] = relu6_1(x[i]); break;
+        case OR_TANH: ((i16 *)y)[i] = tanh1(x[i]); break;
+        case OR_SIGMOID: ((i16 *)y)[i] = sigm1(x[i]); break;
+        default: ((i32 *)y)[i] = x[i]; break;
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------
+ * 8x16 affine kernels (ns-nnsp/src/affine.c ARM path :12-259, affine_acc32b.c
+ * :12-260).  Weight bytes are walked in the CMSIS-NN interleaved order:
+ * per column pair, 4-row block [r0c0 r1c0 r0c1 r1c1 r2c0 r3c0 r2c1 r3c1],
+ * 3-row [r0c0 r1c0 r0c1 r1c1 r2c0 r2c1], 2-row [r0c0 r1c0 r0c1 r1c1],
+ * 1-row [r0c0 r0c1]; odd-column tail one byte per row.  __SMLALD/__SMLAD are
+ * dual 16x16 MACs into a 64-bit / wrapping 32-bit accumulator.
+ * ---------------------------------------------------------------------- */
+static void shift_acc(i64 *a, int sh, int n, int acc32) /* shift_64b :565-591 / shift_32b */
+{
+    if (sh == 0) return;
+    for (int r = 0; r < n; ++r) {
+        if (sh < 0) {
+            a[r] = acc32 ? (i64)((i32)a[r] >> -sh) : (a[r] >> -sh);
+        } else if (acc32) {
+            const i32 M = (i32)(((u32)1 << (31 - sh)) - 1), m = -M - 1;
+            i32 v = (i32)a[r];
+            v = v > M ? M : (v < m ? m : v);
+            a[r] = (i64)shl(v, sh);
+        } else {
+            const i64 M = (i64)(((uint64_t)1 << (63 - sh)) - 1), m = -M - 1;
+            i64 v = a[r] > M ? M : (a[r] < m ? m : a[r]);
+            a[r] = (i64)((uint64_t)v << sh);
+        }
+    }
+}
+
+/* One affine_Krows call: R in 1..4 rows.  *pw / *pb advance like the
+ * reference's pp_kernel / pp_bias; *po advances by the activation's width. */
+static void affine_rows(int R, const int8_t **pw, const int16_t **pb, const int16_t *x, int K,
+                        int qk, int qb, int qi, i64 *acc, int acc32, int is_out, int act,
+                        char **po)
+{
+    const int8_t *w = *pw;
+    const int qs = pb ? (qi + qk > 15 ? qi + qk : 15) : qi + qk;
+    i64 s0 = acc[0], s1 = R > 1 ? acc[1] : 0, s2 = R > 2 ? acc[2] : 0, s3 = R > 3 ? acc[3] : 0;
+    for (int p = 0; p < (K >> 1); ++p) {
+        const i64 x0 = x[2 * p], x1 = x[2 * p + 1];
+        switch (R) {
+        case 4:
+            s0 += w[0] * x0 + w[2] * x1; s1 += w[1] * x0 + w[3] * x1;
+            s2 += w[4] * x0 + w[6] * x1; s3 += w[5] * x0 + w[7] * x1;
+            w += 8; break;
+        case 3:
+            s0 += w[0] * x0 + w[2] * x1; s1 += w[1] * x0 + w[3] * x1;
+            s2 += w[4] * x0 + w[5] * x1;
+            w += 6; break;
+        case 2:
+            s0 += w[0] * x0 + w[2] * x1; s1 += w[1] * x0 + w[3] * x1;
+            w += 4; break;
+        default:
+            s0 += w[0] * x0 + w[1] * x1;
+            w += 2; break;
+        }
+    }
+    i64 s[4] = {s0, s1, s2, s3};
+    if (K & 1) {
+        const i64 xl = x[K - 1];
+        for (int r = 0; r < R; ++r) s[r] += w[r] * xl;
+        w += R;
+    }
+    if (acc32)
+        for (int r = 0; r < R; ++r) s[r] = w32(s[r]);
+    /* affine.c:186-187: the "align acc" shift acts on pt_accum, which is
+     * overwritten below -- dead in the shipped build (trap T1). */
+    if (pb) {
+        const int16_t *b = *pb;
+        const int sh = qs - qb;
+        for (int r = 0; r < R; ++r) {
+            if (acc32) {
+                const i32 bv = sh >= 0 ? shl(b[r], sh) : (b[r] >> -sh);
+                s[r] = add((i32)s[r], bv);
+            } else {
+                s[r] += sh >= 0 ? (i64)((uint64_t)(i64)b[r] << sh) : ((i64)b[r] >> -sh);
+            }
+        }
+        *pb = b + R;
+    }
+    for (int r = 0; r < R; ++r) acc[r] = s[r];
+    if (is_out) {
+        i32 v[4];
+        shift_acc(acc, 15 - qs, R, acc32);
+        for (int r = 0; r < R; ++r) v[r] = acc32 ? (i32)acc[r] : sat32(acc[r]);
+        or_act(act, v, *po, R);
+        *po += R * (act == OR_LINEAR ? 4 : 2);
+    }
+    *pw = w;
+}
+
+static void rc_rows(int R, char **po, const int8_t **pw, const int8_t **pwr, const int16_t **pb,
+                    const int16_t *x, const int16_t *h, int K, int Kr, int qk, int qb, int qi,
+                    int qir, int act, int acc32) /* affine.c:348-407 */
+{
+    i64 acc[4] = {0, 0, 0, 0};
+    affine_rows(R, pw, NULL, x, K, qk, qb, qi, acc, acc32, 0, act, po);
+    shift_acc(acc, qir - qi, R, acc32);
+    affine_rows(R, pwr, pb, h, Kr, qk, qb, qir, acc, acc32, 1, act, po);
+}
+
+static void fc_layer(char *out, const int8_t *w, const int16_t *b, const int16_t *x, int N, int K,
+                     int qk, int qb, int qi, int act, int acc32) /* affine.c:409-490 */
+{
+    char *po = out;
+    for (int r0 = 0; r0 < N; r0 += 4) {
+        const int R = N - r0 >= 4 ? 4 : N - r0;
+        i64 acc[4] = {0, 0, 0, 0};
+        affine_rows(R, &w, &b, x, K, qk, qb, qi, acc, acc32, 1, act, &po);
+    }
+}
+
+static void lstm_layer(i16 *out, const int8_t *w, const int8_t *wr, const int16_t *b,
+                       const int16_t *x, i16 *h, i32 *c, int N, int K, int qk, int qb, int qi,
+                       int qir, int acc32) /* lstm.c:15-214 */
+{
+    for (int u0 = 0; u0 < N; u0 += 4) {
+        const int R = N - u0 >= 4 ? 4 : N - u0;
+        i16 gi[4], gj[4], gf[4], go[4];
+        char *p;
+        p = (char *)gi; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
+        p = (char *)gj; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_TANH, acc32);
+        p = (char *)gf; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
+        p = (char *)go; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
+        for (int r = 0; r < R; ++r) {
+            const i64 cv = ((i64)gi[r] * gj[r] + (i64)gf[r] * c[u0 + r]) >> 15;
+            c[u0 + r] = sat32(cv);
+            const i32 hv = ((i32)tanh1(c[u0 + r]) * go[r]) >> 15;
+            out[u0 + r] = sat16(hv);
+        }
+    }
+    memcpy(h, out, (size_t)N * sizeof(i16)); /* h updated after all groups (T6) */
+}
+
+void or_nn_reset(const or_net *net, or_stream *st) /* neural_nets.c:27-42 */
+{
+    int l = 0;
+    for (int i = 0; i < net->nl; ++i)
+        if (net->type[i] == OR_LSTM) {
+            memset(st->h[l], 0, sizeof st->h[l]);
+            memset(st->c[l], 0, sizeof st->c[l]);
+            ++l;
+        }
+}
+
+void or_net_forward(const or_net *net, or_stream *st, const int16_t *in, int32_t *out,
+                    int32_t n_layers) /* neural_nets.c:44-168 */
+{
+    i32 b0[150], b1[150]; /* 300 x int16 each, int32-aligned */
+    i16 *cur = (i16 *)b0, *nxt = (i16 *)b1;
+    const int nl = n_layers < 0 ? net->nl : n_layers;
+    if (nl == 0) {
+        memcpy(out, in, (size_t)net->size[0] * sizeof(i16));
+        return;
+    }
+    memcpy(cur, in, (size_t)net->size[0] * sizeof(i16));
+    int l = 0;
+    for (int i = 0; i < nl; ++i) {
+        const int K = net->size[i], N = net->size[i + 1];
+        const int qir = i + 1 < OR_MAX_LAYERS ? net->qi[i + 1] : 0;
+        if (net->type[i] == OR_LSTM) {
+            lstm_layer(nxt, net->W[i], net->Wr[i], net->B[i], cur, st->h[l], st->c[l], N, K,
+                       net->qk[i], net->qb[i], net->qi[i], qir, net->acc32);
+            ++l;
+        } else {
+            fc_layer((char *)nxt, net->W[i], net->B[i], cur, N, K, net->qk[i], net->qb[i],
+                     net->qi[i], net->act[i], net->acc32);
+        }
+        i16 *t = cur; cur = nxt; nxt = t;
+    }
+    const int N = net->size[nl];
+    if (net->act[nl - 1] == OR_LINEAR)
+        memcpy(out, cur, (size_t)N * sizeof(i32));
+    else
+        memcpy(out, cur, (size_t)N * sizeof(i16));
+}
+
+/* ------------------------------------------------------------------------
+ * Post-processing (ns-nnsp/src/nn_speech.c:130-258)
+ * ---------------------------------------------------------------------- */
+int32_t or_ceiling(int32_t x)
+{
+    const i32 o = shl(x >> 15, 15);
+    return o == x ? o : add(o, 32768);
+}
+
+int32_t or_pwr2(int32_t x)
+{
+    const i32 c = or_ceiling(x);
+    const i32 f = sub(x, c);
+    const i32 sh = c >> 15;
+    if (sh <= -15) return 0;
+    const i32 t = add(shl(f, 1), 32768);
+    i32 o = 0x1fd7 + ((t * 0x057a) >> 15);
+    o = 0x5a82 + ((t * o) >> 15);
+    return sh < 0 ? (o >> -sh) : shl(o, sh);
+}
+
+void or_binary_post(or_stream *st, const or_cfg *cfg, int32_t *est)
+{
+    const i32 mx = est[0] > est[1] ? est[0] : est[1];
+    for (int i = 0; i < 2; ++i) {
+        const i64 r = ((i64)sub(est[i], mx) * 0xB8AA) >> 15;
+        est[i] = or_pwr2(sat32(r));
+    }
+    const i32 den = add(est[0], est[1]);
+    const i32 thr = 32768 - cfg->thresh_prob;
+    const i32 lim = (i32)(((i64)thr * den) >> 15);
+    if (est[0] <= lim)
+        st->counts[0] = (i16)(st->counts[0] + 1);
+    else
+        st->counts[0] = 0;
+    st->trigger = st->counts[0] >= cfg->th_count ? 1 : 0;
+}
+
+static int argmax_last_wins(const i32 *v, int n)
+{
+    int am = 0;
+    i32 m = v[0];
+    for (int i = 1; i < n; ++i)
+        if (v[i] >= m) { m = v[i]; am = i; }
+    return am;
+}
+
+void or_s2i_post(or_stream *st, const or_cfg *cfg, int32_t *est)
+{
+    st->trigger = 0;
+    st->outputs[0] = st->outputs[1] = st->outputs[2] = 0;
+    const int am = argmax_last_wins(est, 7);
+    if (st->argmax_last == 0 || st->argmax_last == am) {
+        if (am != 0) {
+            st->counts[am] = (i16)(st->counts[am] + 1);
+            if (st->counts[am] > cfg->th_count) {
+                st->trigger = 1;
+                st->outputs[0] = (i16)am;
+                st->outputs[1] = (i16)argmax_last_wins(est + 7, 17);
+                st->outputs[2] = (i16)argmax_last_wins(est + 24, 17);
+            }
+        }
+    } else {
+        for (int i = 0; i < 7; ++i) st->counts[i] = 0;
+    }
+    st->argmax_last = (i16)am;
+}
+
+/* ------------------------------------------------------------------------
+ * NNSPClass (nn_speech.c:57-127)
+ * ---------------------------------------------------------------------- */
+void or_nnsp_reset(const or_net *net, or_stream *st, const or_cfg *cfg)
+{
+    or_fe_reset(st, cfg);
+    or_nn_reset(net, st);
+    st->slides = 1;
+    st->trigger = 0;
+    for (int i = 0; i < 7; ++i) st->counts[i] = 0;
+    st->outputs[0] = st->outputs[1] = st->outputs[2] = 0;
+    st->argmax_last = 0;
+}
+
+int16_t or_nnsp_exec(const or_net *net, or_stream *st, const or_cfg *cfg, const int16_t *pcm,
+                     int32_t *logits, int32_t *ran_nn)
+{
+    or_fe_exec(st, cfg, pcm);
+    if (ran_nn) *ran_nn = st->slides == 1;
+    if (st->slides == 1) {
+        i32 out[50];
+        or_net_forward(net, st, st->ctx, out, -1);
+        if (logits) memcpy(logits, out, (size_t)net->size[net->nl] * sizeof(i32));
+        if (cfg->nn_id == 0)
+            or_s2i_post(st, cfg, out);
+        else
+            or_binary_post(st, cfg, out);
+    }
+    st->slides = (i16)((st->slides + 1) % 2);
+    return st->trigger;
+}
+
+void or_run_streams(const or_net *net, const or_cfg *cfg, or_stream *st, int32_t S, int32_t T,
+                    const int16_t *pcm, int16_t *trig, int32_t *logits, int16_t *feat)
+{
+    const int nout = net->size[net->nl];
+    for (int s = 0; s < S; ++s)
+        for (int t = 0; t < T; ++t) {
+            const size_t f = (size_t)s * T + t;
+            trig[f] = or_nnsp_exec(net, st + s, cfg, pcm + f * 160,
+                                   logits ? logits + f * nout : NULL, NULL);
+            if (feat) memcpy(feat + f * 40, st[s].ctx + 200, 40 * sizeof(i16));
+        }
+}
+
+/* ------------------------------------------------------------------------
+ * Cascade (evb/src/nnCntrlClass.c:130-272, PcmBufClass.c:19-85)
+ * ---------------------------------------------------------------------- */
+void or_cascade_reset(or_cascade *c, const or_cascade_cfg *cfg)
+{
+    memset(c->ring, 0, sizeof c->ring);
+    c->idx_set = 0;
+    c->idx_latest = 99;
+    c->pos_seq = 0; /* nnCntrlClass_init:125 */
+    c->cnt_timeout_kws = c->cnt_timeout_s2i = 0;
+    for (int i = 0; i < 3; ++i) or_nnsp_reset(cfg->net[i], &c->nnsp[i], &cfg->cfg[i]);
+}
+
+static const int16_t *ring_get(const or_cascade *c, int lookback)
+{
+    int start = (c->idx_latest - lookback) % 100;
+    if (start < 0) start += 100;
+    return c->ring + start * 160;
+}
+
+int32_t or_cascade_exec(or_cascade *c, const or_cascade_cfg *cfg, const int16_t *pcm,
+                        int16_t *detected, int16_t *out3)
+{
+    const int cur = cfg->seq[c->pos_seq];
+    memcpy(c->ring + c->idx_set * 160, pcm, 160 * sizeof(i16));
+    c->idx_latest = c->idx_set;
+    c->idx_set = (int16_t)((c->idx_set + 1) % 100);
+    or_stream *st = &c->nnsp[cur];
+    const or_net *net = cfg->net[cur];
+    const or_cfg *nc = &cfg->cfg[cur];
+    int16_t det = 0;
+    int next_pos, next_id;
+    if (cur == 0) { /* s2i */
+        det = or_nnsp_exec(net, st, nc, ring_get(c, cfg->lookback_s2i), NULL, NULL);
+        memcpy(out3, st->outputs, 3 * sizeof(i16)); /* printed before the reset, :191-194 */
+        c->cnt_timeout_s2i = (uint16_t)((c->cnt_timeout_s2i + 1) % cfg->timeout_s2i);
+        if (det || c->cnt_timeout_s2i == cfg->timeout_s2i - 1) {
+            next_pos = (c->pos_seq + 1) % cfg->len_seq;
+            next_id = cfg->seq[next_pos];
+            if (det || cur != next_id) {
+                c->cnt_timeout_s2i = 0;
+                or_nnsp_reset(net, st, nc);
+            }
+            c->pos_seq = (int16_t)next_pos;
+        }
+    } else if (cur == 2) { /* kws */
+        det = or_nnsp_exec(net, st, nc, ring_get(c, cfg->lookback_kws), NULL, NULL);
+        memcpy(out3, st->outputs, 3 * sizeof(i16));
+        c->cnt_timeout_kws = (uint16_t)((c->cnt_timeout_kws + 1) % cfg->timeout_kws);
+        if (det || c->cnt_timeout_kws == cfg->timeout_kws - 1) {
+            if (det) {
+                next_pos = (c->pos_seq + 1) % cfg->len_seq;
+            } else {
+                next_pos = (c->pos_seq - 1) % cfg->len_seq;
+                if (next_pos < 0) next_pos += cfg->len_seq;
+            }
+            next_id = cfg->seq[next_pos];
+            if (det || cur != next_id) {
+                c->cnt_timeout_kws = 0;
+                or_nnsp_reset(net, st, nc);
+            }
+            c->pos_seq = (int16_t)next_pos;
+        }
+    } else { /* vad */
+        det = or_nnsp_exec(net, st, nc, ring_get(c, 0), NULL, NULL);
+        memcpy(out3, st->outputs, 3 * sizeof(i16));
+        if (det) {
+            next_pos = (c->pos_seq + 1) % cfg->len_seq;
+            or_nnsp_reset(net, st, nc);
+            c->pos_seq = (int16_t)next_pos;
+        }
+    }
+    *detected = det;
+    return cur;
+}
+
+void or_run_cascade(const or_cascade_cfg *cfg, or_cascade *c, int32_t S, int32_t T,
+                    const int16_t *pcm, int8_t *net_ran, int16_t *detected, int16_t *outputs3)
+{
+    for (int s = 0; s < S; ++s)
+        for (int t = 0; t < T; ++t) {
+            const size_t f = (size_t)s * T + t;
+            int16_t det = 0, o3[3];
+            const int ran = or_cascade_exec(c + s, cfg, pcm + f * 160, &det, o3);
+            if (net_ran) net_ran[f] = (int8_t)ran;
+            if (detected) detected[f] = det;
+            if (outputs3) memcpy(outputs3 + 3 * f, o3, sizeof o3);
+        }
+}
+
+int32_t or_sizeof_stream(void) { return (int32_t)sizeof(or_stream); }
+int32_t or_sizeof_cascade(void) { return (int32_t)sizeof(or_cascade); }

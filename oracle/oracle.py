@@ -1,0 +1,155 @@
+"""TEST INFRASTRUCTURE ONLY -- ctypes wrapper of the CPU oracle (liboracle.so,
+a scalar restatement of the reference path; see nnsp_oracle.h for what is
+pinned and how).  Imported only by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg; never by the product package.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+REF = os.path.join(HERE, "_ref", "libnnsp_ref_partial.so")
+
+MAXL = 10
+
+
+class or_net(C.Structure):
+    _fields_ = [("nl", C.c_int32), ("size", C.c_int32 * (MAXL + 1)), ("type", C.c_int32 * MAXL),
+                ("qk", C.c_int32 * MAXL), ("qi", C.c_int32 * MAXL), ("qb", C.c_int32 * MAXL),
+                ("act", C.c_int32 * MAXL), ("acc32", C.c_int32), ("W", C.c_void_p * MAXL),
+                ("Wr", C.c_void_p * MAXL), ("B", C.c_void_p * MAXL)]
+
+
+class or_cfg(C.Structure):
+    _fields_ = [("nn_id", C.c_int32), ("thresh_prob", C.c_int32), ("th_count", C.c_int32),
+                ("qbit_out", C.c_int32), ("mean", C.c_void_p), ("stdR", C.c_void_p)]
+
+
+class or_cascade_cfg(C.Structure):
+    _fields_ = [("net", C.c_void_p * 3), ("cfg", or_cfg * 3), ("seq", C.c_int32 * 3),
+                ("len_seq", C.c_int32), ("lookback_kws", C.c_int32), ("lookback_s2i", C.c_int32),
+                ("timeout_kws", C.c_int32), ("timeout_s2i", C.c_int32)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-s", "liboracle.so"], cwd=HERE)
+        _lib = C.CDLL(LIB)
+        _lib.or_log10.restype = C.c_int32
+        _lib.or_log10.argtypes = [C.c_int32]
+        _lib.or_pwr2.restype = C.c_int32
+        _lib.or_pwr2.argtypes = [C.c_int32]
+        _lib.or_ceiling.restype = C.c_int32
+        _lib.or_ceiling.argtypes = [C.c_int32]
+        _lib.or_nnsp_exec.restype = C.c_int16
+        _lib.or_cascade_exec.restype = C.c_int32
+        _lib.or_sizeof_stream.restype = C.c_int32
+        _lib.or_sizeof_cascade.restype = C.c_int32
+    return _lib
+
+
+def p(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class OracleNet:
+    """or_net + or_cfg built from nnsp_amd.nets.NetData (packed byte layout)."""
+
+    def __init__(self, data, acc32: bool = False, thresh_prob: int = 32767 >> 1, th_count: int = 4):
+        spec = data.spec
+        Wp, Wrp, Bp = data.packed()
+        self.keep = []
+        n = or_net()
+        n.nl = spec.nl
+        for i, s in enumerate(spec.sizes):
+            n.size[i] = s
+        for i in range(spec.nl):
+            n.type[i] = spec.types[i]
+            n.qk[i], n.qi[i], n.qb[i] = spec.qk[i], spec.qi[i], spec.qb[i]
+            n.act[i] = spec.acts[i]
+            w = np.ascontiguousarray(Wp[i]).view(np.int8)
+            b = np.ascontiguousarray(Bp[i], np.int16)
+            self.keep += [w, b]
+            n.W[i] = w.ctypes.data
+            n.B[i] = b.ctypes.data
+            if Wrp[i] is not None:
+                wr = np.ascontiguousarray(Wrp[i]).view(np.int8)
+                self.keep.append(wr)
+                n.Wr[i] = wr.ctypes.data
+        n.acc32 = int(acc32)
+        self.net = n
+        self.mean = np.ascontiguousarray(data.mean, np.int32)
+        self.stdR = np.ascontiguousarray(data.stdR, np.int32)
+        c = or_cfg()
+        c.nn_id = spec.nn_id
+        c.thresh_prob = thresh_prob
+        c.th_count = th_count
+        c.qbit_out = spec.qi[0]
+        c.mean = self.mean.ctypes.data
+        c.stdR = self.stdR.ctypes.data
+        self.cfg = c
+        self.nout = spec.nout
+
+    def new_states(self, S: int) -> np.ndarray:
+        L = lib()
+        st = np.zeros((S, L.or_sizeof_stream()), np.uint8)
+        for s in range(S):
+            L.or_nnsp_reset(C.byref(self.net), C.c_void_p(st[s].ctypes.data), C.byref(self.cfg))
+        return st
+
+    def run(self, pcm: np.ndarray, states: np.ndarray | None = None, want_logits=True,
+            want_feats=True):
+        """pcm [S][T][160] -> trig [S][T], logits [S][T][nout] (0 on non-NN frames), feats."""
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        S, T, _ = pcm.shape
+        if states is None:
+            states = self.new_states(S)
+        trig = np.zeros((S, T), np.int16)
+        logits = np.zeros((S, T, self.nout), np.int32) if want_logits else None
+        feats = np.zeros((S, T, 40), np.int16) if want_feats else None
+        lib().or_run_streams(C.byref(self.net), C.byref(self.cfg), p(states), S, T, p(pcm),
+                             p(trig), p(logits), p(feats))
+        return trig, logits, feats, states
+
+    def reset_streams(self, states: np.ndarray, mask) -> None:
+        for s in np.nonzero(mask)[0]:
+            lib().or_nnsp_reset(C.byref(self.net), C.c_void_p(states[s].ctypes.data), C.byref(self.cfg))
+
+    def forward(self, x240: np.ndarray, state: np.ndarray, n_layers: int = -1) -> np.ndarray:
+        out = np.zeros(64, np.int32)
+        x = np.ascontiguousarray(x240, np.int16)
+        lib().or_net_forward(C.byref(self.net), C.c_void_p(state.ctypes.data), p(x), p(out), n_layers)
+        return out
+
+
+def rfft512(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    x = np.ascontiguousarray(x, np.int32).copy()
+    xi = np.zeros(514, np.int32)
+    xi[:512] = x
+    y = np.zeros(1024, np.int32)
+    lib().or_rfft512(p(xi), p(y))
+    return y, xi[:512]
+
+
+def synthetic_pcm(S: int, T: int, seed: int = 0x4E4E5350, t0: int = 0, s0: int = 0,
+                  amp: int = 4096) -> np.ndarray:
+    """SplitMix64(seed, stream, sample) -> int16 in [-amp, amp-1]."""
+    s = (np.arange(S, dtype=np.uint64) + np.uint64(s0))[:, None]
+    n = (np.arange(T * 160, dtype=np.uint64) + np.uint64(t0 * 160))[None, :]
+    with np.errstate(over="ignore"):
+        z = np.uint64(seed) + s * np.uint64(0x9E3779B97F4A7C15) + n * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    v = (z % np.uint64(2 * amp)).astype(np.int64) - amp
+    return v.astype(np.int16).reshape(S, T, 160)
