@@ -153,3 +153,35 @@ def synthetic_pcm(S: int, T: int, seed: int = 0x4E4E5350, t0: int = 0, s0: int =
         z = z ^ (z >> np.uint64(31))
     v = (z % np.uint64(2 * amp)).astype(np.int64) - amp
     return v.astype(np.int16).reshape(S, T, 160)
+
+
+class or_stream(C.Structure):
+    _fields_ = [("buf", C.c_int16 * 480), ("ctx", C.c_int16 * 240), ("h", (C.c_int16 * 128) * 2),
+                ("c", (C.c_int32 * 128) * 2), ("slides", C.c_int16), ("trigger", C.c_int16),
+                ("argmax_last", C.c_int16), ("pad0", C.c_int16), ("counts", C.c_int16 * 8),
+                ("outputs", C.c_int16 * 3), ("pad1", C.c_int16)]
+
+
+def act(kind: int, x: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(x, np.int32)
+    y = np.zeros(len(x), np.int32 if kind == 3 else np.int16)
+    lib().or_act(kind, p(x), p(y), len(x))
+    return y
+
+
+def log10(x: np.ndarray) -> np.ndarray:
+    return np.array([lib().or_log10(int(v)) for v in np.asarray(x, np.int64)], np.int32)
+
+
+def spec2pspec(spec1024: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(spec1024, np.int32)
+    y = np.zeros(257, np.int32)
+    lib().or_spec2pspec(p(y), p(x), 257)
+    return y
+
+
+def mel(pspec: np.ndarray) -> np.ndarray:
+    x = np.ascontiguousarray(pspec, np.int32)
+    y = np.zeros(40, np.int32)
+    lib().or_mel(p(x), p(y))
+    return y

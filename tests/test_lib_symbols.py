@@ -1,0 +1,97 @@
+"""libnnsp_mi355x.so loads on a machine without a GPU and exports every
+function and table declared in include/*.h (no compute calls here)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from nnsp_amd import _lib
+
+
+def _declared_functions():
+    names = set()
+    for h in ("nnsp_api.h", "nnsp_batch.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"typedef[^;]*;", "", text, flags=re.S)
+        text = re.sub(r"#define[^\n]*", "", text)
+        for m in re.finditer(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\([^;{]*\)\s*;", text):
+            n = m.group(1)
+            if n not in ("if", "while", "sizeof", "MAX", "MIN"):
+                names.add(n)
+    return names
+
+
+def test_every_declared_symbol_is_exported():
+    L = _lib.lib()
+    names = _declared_functions()
+    assert len(names) > 50
+    missing = [n for n in sorted(names) if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_tables_exported():
+    L = _lib.lib()
+    for sym, n in (("stft_win_coeff", 480), ("mfltrBank_coeff", 534), ("log_tayler_coeff", 256),
+                   ("coeffs_tanh", 384)):
+        arr = (C.c_int16 * n).in_dll(L, sym)
+        assert any(arr)
+    assert C.c_int16.in_dll(L, "len_stft_win_coeff").value == 480
+    assert C.c_int16.in_dll(L, "hop").value == 160
+    assert C.c_int16.in_dll(L, "num_mfltrBank").value == 40
+
+
+PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "neural_nets.h"
+#include "nn_speech.h"
+#include "feature_module.h"
+#define O(T, f) printf("%s.%s %zu\n", #T, #f, offsetof(T, f))
+int main(void) {
+    printf("NeuralNetClass %zu\nNNSPClass %zu\nFeatureClass %zu\nstftModule %zu\n",
+           sizeof(NeuralNetClass), sizeof(NNSPClass), sizeof(FeatureClass), sizeof(stftModule));
+    O(NeuralNetClass, size_layer); O(NeuralNetClass, net_layer_type); O(NeuralNetClass, qbit_kernel);
+    O(NeuralNetClass, activation_type); O(NeuralNetClass, pt_cstate); O(NeuralNetClass, act_func);
+    O(NeuralNetClass, layer_func); O(NeuralNetClass, pt_kernel_rec);
+    O(NNSPClass, pt_net); O(NNSPClass, slides); O(NNSPClass, trigger); O(NNSPClass, counts_category);
+    O(NNSPClass, pt_th_count_trigger); O(NNSPClass, outputs); O(NNSPClass, argmax_last);
+    O(FeatureClass, feature); O(FeatureClass, normFeatContext); O(FeatureClass, pt_norm_mean);
+    O(FeatureClass, qbit_output); O(stftModule, dataBuffer); O(stftModule, window);
+    return 0;
+}
+"""
+
+
+def _layout(include_dir):
+    import subprocess
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "p.c")
+        open(src, "w").write(PROBE)
+        exe = os.path.join(d, "p")
+        subprocess.check_call(["gcc", "-I", include_dir, src, "-o", exe])
+        return dict(l.rsplit(" ", 1) for l in subprocess.check_output([exe]).decode().split("\n") if l)
+
+
+def _ctypes_layout():
+    out = {"NeuralNetClass": C.sizeof(_lib.NeuralNetClass), "NNSPClass": C.sizeof(_lib.NNSPClass),
+           "FeatureClass": C.sizeof(_lib.FeatureClass), "stftModule": C.sizeof(_lib.stftModule)}
+    for T in (_lib.NeuralNetClass, _lib.NNSPClass, _lib.FeatureClass, _lib.stftModule):
+        for f, *_ in T._fields_:
+            out[f"{T.__name__}.{f}"] = getattr(T, f).offset
+    return {k: str(v) for k, v in out.items()}
+
+
+def test_struct_abi_matches_headers():
+    mine = _layout(os.path.join(ROOT, "include"))
+    ct = _ctypes_layout()
+    for k, v in mine.items():
+        assert ct[k] == v, (k, v, ct[k])
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/ns-nnsp"), reason="reference absent")
+def test_struct_abi_matches_reference_headers():
+    assert _layout(os.path.join(ROOT, "include")) == _layout("/root/reference/ns-nnsp/includes-api")
