@@ -29,7 +29,43 @@ struct nnsp_batch {
     int32_t *d_logits;
     uint8_t *d_mask;
     int last_T;
+    /* split NN path (one LSTM layer) */
+    int fast, li, nstep_max, rec_waves, proj_blocks;
+    int32_t *d_gx;
 };
+
+#define LDS_MAX (160 * 1024)
+
+/* Use the split proj/recur kernels when the net has exactly one LSTM layer,
+ * every other layer is FC and the staged weights fit in LDS. */
+static void plan_fast(nnsp_batch *b)
+{
+    const NnImage *g = &b->im.img;
+    b->fast = 0;
+    if (getenv("NNSP_FUSED_NN")) return;
+    if (g->n_lstm != 1) return;
+    int li = -1;
+    for (int i = 0; i < g->nl; ++i)
+        if (g->L[i].type == NN_LSTM) li = i;
+    for (int i = li + 1; i < g->nl; ++i)
+        if (g->L[i].N > 128 || g->L[i].K > 128) return;
+    const int a_proj = (int)g->L[li].ar_off;
+    const int a_rec = (int)(b->im.a_bytes - (size_t)g->L[li].ar_off);
+    if (nnspk_fast_lds_bytes(0, a_proj, 4) > LDS_MAX) return;
+    int maxw = 0;
+    for (int w = 1; w <= 4; ++w)
+        if (nnspk_fast_lds_bytes(1, a_rec, w) <= LDS_MAX) maxw = w;
+    if (!maxw) return;
+    const int tiles = (b->S + 15) / 16;
+    int w = (tiles + 255) / 256;
+    b->rec_waves = w < 1 ? 1 : (w > maxw ? maxw : w);
+    b->li = li;
+    b->nstep_max = (b->Tmax + 1) / 2;
+    const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);
+    long long blocks = (ptiles + 3) / 4;
+    b->proj_blocks = (int)(blocks < 256 ? blocks : 256);
+    b->fast = 1;
+}
 
 #define TRY(x)                 \
     do {                       \
@@ -55,6 +91,10 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     *out = NULL;
     if (!net || !mean || !stdR || n_streams <= 0 || max_frames <= 0) {
         nnsp_set_error("nnsp_batch_create: bad argument");
+        return NNSP_EINVAL;
+    }
+    if ((long long)n_streams * max_frames >= (1LL << 31) / 2) {
+        nnsp_set_error("n_streams * max_frames must stay below 2^30");
         return NNSP_EINVAL;
     }
     if (net->size_layer[0] != NUM_FEATURE_CONTEXT * DIMEMSION_FEATURE) {
@@ -89,6 +129,12 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     if ((e = nnspk_malloc((void **)&b->d_post, S * sizeof(NnPost)))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_feats, S * T * 40 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_mask, S))) goto fail;
+    plan_fast(b);
+    if (b->fast) {
+        if ((e = nnspk_set_lds_limit())) goto fail;
+        const size_t rows = (size_t)b->im.img.L[b->li].rows;
+        if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
+    }
     if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
     if ((e = nnspk_h2d(b->d_stdR, stdR, 40 * 4, b->stream))) goto fail;
     if ((e = nnspk_memset(b->d_prev5, 0, S * 200 * 2, b->stream))) goto fail;
@@ -107,7 +153,7 @@ void nnsp_batch_destroy(nnsp_batch *b)
     if (b->stream) nnspk_sync(b->stream);
     nnsp_image_free(&b->im);
     void *bufs[] = {b->d_mean, b->d_stdR, b->d_tail, b->d_prev5, b->d_h, b->d_c, b->d_post,
-                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask};
+                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 3; ++i) nnspk_event_destroy(b->ev[i]);
     nnspk_stream_destroy(b->stream);
@@ -155,20 +201,44 @@ int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *tr
     TRY(nnspk_event_record(b->ev[0], b->stream));
     TRY(nnspk_launch_fe(&fa, b->stream));
     TRY(nnspk_event_record(b->ev[1], b->stream));
-    NnRun r;
-    memset(&r, 0, sizeof r);
-    r.S = b->S;
-    r.T = T;
-    r.mode = NN_MODE_STREAM;
-    r.nl_run = b->im.img.nl;
-    r.feats = b->d_feats;
-    r.prev5 = b->d_prev5;
-    r.h = b->d_h;
-    r.c = b->d_c;
-    r.post = b->d_post;
-    r.trig = trig;
-    r.logits = logits;
-    TRY(nnspk_launch_nn(&b->im.img, &r, b->stream));
+    if (b->fast) {
+        FastRun f;
+        memset(&f, 0, sizeof f);
+        f.S = b->S;
+        f.T = T;
+        f.li = b->li;
+        f.nstep_max = b->nstep_max;
+        f.feats = b->d_feats;
+        f.prev5 = b->d_prev5;
+        f.post = b->d_post;
+        f.gx = b->d_gx;
+        f.h = b->d_h;
+        f.c = b->d_c;
+        f.trig = trig;
+        f.logits = logits;
+        const NnLayer *LL = &b->im.img.L[b->li];
+        f.a_off = 0;
+        f.a_lds_bytes = (int)LL->ar_off;
+        TRY(nnspk_launch_proj(&b->im.img, &f, b->proj_blocks, b->stream));
+        f.a_off = LL->ar_off;
+        f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
+        TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, b->stream));
+    } else {
+        NnRun r;
+        memset(&r, 0, sizeof r);
+        r.S = b->S;
+        r.T = T;
+        r.mode = NN_MODE_STREAM;
+        r.nl_run = b->im.img.nl;
+        r.feats = b->d_feats;
+        r.prev5 = b->d_prev5;
+        r.h = b->d_h;
+        r.c = b->d_c;
+        r.post = b->d_post;
+        r.trig = trig;
+        r.logits = logits;
+        TRY(nnspk_launch_nn(&b->im.img, &r, b->stream));
+    }
     TRY(nnspk_event_record(b->ev[2], b->stream));
     /* carry the context (slots 1..5) and the PCM tail (last 320 samples) */
     TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, b->stream));

@@ -1,0 +1,338 @@
+// nnsp_fast.hip -- split NN path for nets with exactly one LSTM layer (all
+// three reference nets: fc -> lstm -> fc -> fc -> fc).
+//
+// NeuralNetClass_exe (neural_nets.c:44-168) is recurrent only through the LSTM
+// state; the layers before the LSTM and the LSTM's input half of every gate
+// (rc_Krows_8x16's first affine, affine.c:377-384) depend on the frame's
+// context alone.  So a chunk runs as
+//   proj_kernel  : every (stream, NN step) row in parallel -- prefix FC
+//                  layers + Wx.x -> exact int32 gate partial sums gx;
+//                  16-row MFMA tiles = 16 consecutive steps of one stream (their
+//                  context windows overlap: 36 feature frames feed 16 rows)
+//   recur_kernel : per 16-stream tile, the steps in order -- Wh.h + gx, gate
+//                  epilogue (shift_64b, bias, clamp/wrap, sigmoid/tanh), cell
+//                  and hidden update (lstm.c:106-115, h after all groups: T6),
+//                  the FC layers after the LSTM, post-processing, triggers.
+// All weights of each kernel are staged once per workgroup into LDS as MFMA
+// A-fragments.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nnsp_dev.h"
+#include "nnsp_kabi.h"
+#include "nnsp_nn.h"
+
+using namespace nnsp;
+
+#define P_ASTRIDE 264   // int16 per row of a proj activation buffer
+#define P_UNION 1440    // 36 frames x 40 features (int16)
+#define R_STRIDE 136    // int16 per row of recur h / activation buffers
+#define R_CW 128        // int32 per row of the c buffer
+
+struct ProjWave {
+    int16_t uni[P_UNION + 32];
+    int16_t act[2][16][P_ASTRIDE];
+};
+
+__device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, int bytes) {
+    const int4* s = reinterpret_cast<const int4*>(src);
+    int4* d = reinterpret_cast<int4*>(dst);
+    for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
+}
+
+// One FC layer on a 16-row tile: B from an LDS buffer (row stride in_stride),
+// A fragments from LDS, output to an LDS buffer (row stride out_stride).
+__device__ __forceinline__ void fc_tile(const NnImage& img, const NnLayer& Ly, const uint8_t* A,
+                                        const int16_t* in, int in_stride, int16_t* out, int out_stride,
+                                        const int16_t* tt, int lane) {
+    v4i bh[4], bl[4];
+    load_b<4>(in, in_stride, Ly.nkt, lane, bh, bl);
+    const int sc = lane & 15, q = lane >> 4;
+    for (int rt = 0; rt < Ly.nrt; ++rt) {
+        v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+            if (kt < Ly.nkt) {
+                const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * Ly.nkt + kt) * 1024 + 16 * lane);
+                ah = mfma8(w, bh[kt], ah);
+                al = mfma8(w, bl[kt], al);
+            }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int row = 16 * rt + 4 * q + i;
+            if (row >= Ly.rows) continue;
+            const int32_t sum = (ah[i] << 8) + al[i] + img.wsum[Ly.ep_off + row];
+            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
+            if (Ly.act == ACT_LINEAR)
+                reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
+            else
+                out[sc * out_stride + row] = act16(Ly.act, v, tt);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// proj_kernel
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* W = smem;                                           // staged A fragments
+    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    ProjWave* pw = reinterpret_cast<ProjWave*>(smem + r.a_lds_bytes + 768);
+    stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    ProjWave& P = pw[wv];
+    const int sc = lane & 15, q = lane >> 4;
+    const NnLayer& LL = img.L[r.li];
+    const int ntps = (r.nstep_max + 15) / 16;
+    const long long ntiles = (long long)r.S * ntps;
+    const int rows = LL.rows;
+    for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
+         tile += (long long)gridDim.x * (blockDim.x >> 6)) {
+        const int s = (int)(tile / ntps), j0 = 16 * (int)(tile - (long long)s * ntps);
+        const int phase = 1 - reinterpret_cast<const NnPost*>(r.post)[s].slides;
+        const int t0 = 2 * j0 + phase;            // NN frame of row 0
+        // ---- union of the 16 context windows: V[t0 .. t0+35], V = prev5 ++ feats
+        for (int c = lane; c < 180; c += 64) {
+            const int fr = c / 5, part = c - 5 * fr, idx = t0 + fr;
+            int4 v = make_int4(0, 0, 0, 0);
+            if (idx < 5)
+                v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part);
+            else if (idx - 5 < r.T)
+                v = *reinterpret_cast<const int4*>(r.feats + ((size_t)s * r.T + idx - 5) * 40 + 8 * part);
+            *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
+        }
+        wave_lds_sync();
+        // ---- prefix FC layers (row p's context = uni[80p .. 80p+239])
+        const int16_t* in = P.uni;
+        int in_stride = 80;
+        for (int i = 0; i < r.li; ++i) {
+            const NnLayer& Ly = img.L[i];
+            int16_t* out = &P.act[i & 1][0][0];
+            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), in, in_stride, out, P_ASTRIDE, tt, lane);
+            wave_lds_sync();
+            in = out;
+            in_stride = P_ASTRIDE;
+        }
+        // ---- LSTM input half: gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
+        {
+            v4i bh[4], bl[4];
+            load_b<4>(in, in_stride, LL.nkt, lane, bh, bl);
+            const uint8_t* A = W + (LL.a_off - r.a_off);
+            const int j = j0 + sc;
+            const bool act = j < r.nstep_max && 2 * j + phase < r.T;
+            int32_t* dst = r.gx + ((size_t)s * r.nstep_max + j) * rows + 4 * q;
+            for (int rt = 0; rt < LL.nrt; ++rt) {
+                v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
+#pragma unroll
+                for (int kt = 0; kt < 4; ++kt)
+                    if (kt < LL.nkt) {
+                        const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * LL.nkt + kt) * 1024 + 16 * lane);
+                        ah = mfma8(w, bh[kt], ah);
+                        al = mfma8(w, bl[kt], al);
+                    }
+                int4 o;
+                o.x = (ah[0] << 8) + al[0] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 0];
+                o.y = (ah[1] << 8) + al[1] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 1];
+                o.z = (ah[2] << 8) + al[2] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 2];
+                o.w = (ah[3] << 8) + al[3] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 3];
+                if (act) *reinterpret_cast<int4*>(dst + 16 * rt) = o;
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// recur_kernel
+// ---------------------------------------------------------------------------
+struct RecWave {
+    int16_t h[16][R_STRIDE];
+    int16_t act[2][16][R_STRIDE];
+    int32_t c[16][R_CW];
+    int32_t active[16];
+    int32_t phase[16];
+};
+
+template <int NRT>
+__global__ __launch_bounds__(256) void recur_kernel(NnImage img, FastRun r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t* W = smem;
+    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    RecWave* rw = reinterpret_cast<RecWave*>(smem + r.a_lds_bytes + 768);
+    stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    RecWave& R = rw[wv];
+    const int sc = lane & 15, q = lane >> 4;
+    const int s0 = (blockIdx.x * (blockDim.x >> 6) + wv) * 16;
+    const int s = s0 + sc;
+    const bool valid = s < r.S;
+    const NnLayer& LL = img.L[r.li];
+    const int N = LL.N, rows = LL.rows, nrt = LL.nrt;
+    // ---- LSTM state in (rows of NN_MAX_W)
+    for (int idx = lane; idx < 16 * N; idx += 64) {
+        const int st = idx / N, u = idx - st * N, gs = s0 + st;
+        const bool ok = gs < r.S;
+        R.h[st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
+        R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
+    }
+    PostState ps = {};
+    if (lane < 16) {
+        if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
+        R.phase[lane] = valid ? 1 - ps.slides : 0;
+    }
+    __syncthreads();   // weights staged, per-wave state loaded
+    const int phase = R.phase[sc];
+    const int T = r.T;
+    const int nsteps = (T + 1) / 2;
+    if (lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
+    const uint8_t* Ar = W;   // LSTM recurrent fragments come first in the staged region
+    // gate partial sums (independent of h): step j+1's are loaded while step j
+    // finishes its FC layers and post-processing
+    v4i gxv[NRT];
+    auto load_gx = [&](int jj) {
+        const bool ok = valid && 2 * jj + phase < T;
+        const int32_t* gsrc = r.gx + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * rows + 4 * q;
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt)
+            if (rt < nrt) gxv[rt] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
+    };
+    load_gx(0);
+    for (int j = 0; j < nsteps; ++j) {
+        const int t = 2 * j + phase;
+        const bool active = valid && t < T;
+        if (lane < 16) R.active[lane] = active;
+        v4i bh[2], bl[2];
+        load_b<2>(&R.h[0][0], R_STRIDE, LL.nkt_r, lane, bh, bl);
+        // ---- LSTM (lstm.c:48-124): per row tile = 4 units x gates i,j,f,o
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) {
+            if (rt < nrt) {
+            v4i hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+                if (kt < LL.nkt_r) {
+                    const v4i w = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * LL.nkt_r + kt) * 1024 + 16 * lane);
+                    hh = mfma8(w, bh[kt], hh);
+                    hl = mfma8(w, bl[kt], hl);
+                }
+            const int u = 4 * rt + q;
+            if (u < N) {
+                int16_t g[4];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * rt + 4 * q + i;
+                    const int32_t sx = gxv[rt][i];
+                    const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[LL.ep_off + row];
+                    int64_t pre;
+                    if (img.acc32)
+                        pre = (int64_t)wadd(shift32(sx, LL.xs_sh), sh);
+                    else
+                        pre = shift64((int64_t)sx, LL.xs_sh) + (int64_t)sh;
+                    const int32_t v = affine_out(pre, img.bias[LL.ep_off + row], LL, img.acc32);
+                    g[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                }
+                const int32_t c_old = R.c[sc][u];
+                const int32_t c_new = sat32(((int64_t)g[0] * g[1] + (int64_t)g[2] * c_old) >> 15);
+                const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
+                if (active) R.c[sc][u] = c_new;
+                R.act[0][sc][u] = hv;
+            }
+            }
+        }
+        if (j + 1 < nsteps) load_gx(j + 1);
+        wave_lds_sync();
+        for (int idx = lane; idx < 16 * N; idx += 64) {   // h := output (T6)
+            const int st = idx / N, u = idx - st * N;
+            if (R.active[st]) R.h[st][u] = R.act[0][st][u];
+        }
+        // ---- FC layers after the LSTM
+        int cur = 0;
+        for (int i = r.li + 1; i < img.nl; ++i) {
+            const NnLayer& Ly = img.L[i];
+            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), &R.act[cur][0][0], R_STRIDE,
+                    &R.act[cur ^ 1][0][0], R_STRIDE, tt, lane);
+            wave_lds_sync();
+            cur ^= 1;
+        }
+        // ---- outputs and post-processing (nn_speech.c:92-124)
+        const int16_t* fin = &R.act[cur][sc][0];
+        const NnLayer& LO = img.L[img.nl - 1];
+        const int nout = LO.N;
+        const bool lin = LO.act == ACT_LINEAR;
+        if (active && r.logits) {
+            int32_t* dst = r.logits + ((size_t)s * T + t) * nout;
+            for (int o = q; o < nout; o += 4)
+                dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
+        }
+        if (lane < 16 && active) {
+            const LogitRow lg = {fin, lin};
+            post_proc(ps, img, lg);
+            if (r.trig) {
+                r.trig[(size_t)s * T + t] = ps.trigger;
+                if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+            }
+        }
+        wave_lds_sync();
+    }
+    // ---- state out
+    for (int idx = lane; idx < 16 * N; idx += 64) {
+        const int st = idx / N, u = idx - st * N, gs = s0 + st;
+        if (gs < r.S) {
+            r.h[(size_t)gs * NN_MAX_W + u] = R.h[st][u];
+            r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
+        }
+    }
+    if (lane < 16 && valid) {
+        ps.slides = (int16_t)(ps.slides ^ (T & 1));
+        reinterpret_cast<PostState*>(r.post)[s] = ps;
+    }
+}
+
+extern "C" {
+
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int waves) {
+    if (which == 0) return (size_t)a_bytes + 768 + (size_t)waves * sizeof(ProjWave);
+    return (size_t)a_bytes + 768 + (size_t)waves * sizeof(RecWave);
+}
+
+int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
+    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4);
+    hipLaunchKernelGGL(proj_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, *img, *r);
+    return hipGetLastError() == hipSuccess ? 0 : (int)hipGetLastError();
+}
+
+int nnspk_launch_recur(const NnImage* img, const FastRun* r, int waves, void* stream) {
+    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, waves);
+    const int tiles = (r->S + 15) / 16;
+    const int blocks = (tiles + waves - 1) / waves;
+    const int nrt = img->L[r->li].nrt;
+    if (nrt <= 8)
+        hipLaunchKernelGGL(recur_kernel<8>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+    else if (nrt <= 16)
+        hipLaunchKernelGGL(recur_kernel<16>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+    else if (nrt <= 18)
+        hipLaunchKernelGGL(recur_kernel<18>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+    else
+        hipLaunchKernelGGL(recur_kernel<32>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+int nnspk_set_lds_limit(void) {
+    // allow up to 160 KiB of dynamic LDS for the split kernels
+    hipError_t e = hipFuncSetAttribute((const void*)proj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return (int)e;
+    const void* ks[4] = {(const void*)recur_kernel<8>, (const void*)recur_kernel<16>,
+                         (const void*)recur_kernel<18>, (const void*)recur_kernel<32>};
+    for (int i = 0; i < 4; ++i) {
+        e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        if (e != hipSuccess) return (int)e;
+    }
+    return 0;
+}
+
+}  // extern "C"

@@ -65,6 +65,21 @@ typedef struct {
     int32_t out_stride, pad;
 } NnRun;
 
+/* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
+typedef struct {
+    int32_t S, T, li, nstep_max;
+    int32_t a_lds_bytes, pad;
+    int64_t a_off;            /* byte offset in NnImage.A of the LDS-staged region */
+    const int16_t *feats;     /* [S][T][40] */
+    const int16_t *prev5;     /* [S][5][40] */
+    void *post;               /* [S] NnPost */
+    int32_t *gx;              /* [S][nstep_max][LSTM rows] exact Wx.x sums */
+    int16_t *h;               /* [S][NN_MAX_W] */
+    int32_t *c;               /* [S][NN_MAX_W] */
+    int16_t *trig;            /* [S][T] */
+    int32_t *logits;          /* [S][T][nout] or NULL */
+} FastRun;
+
 /* 32-byte device post-processing state, one per stream */
 typedef struct {
     int16_t slides, trigger, argmax_last, pad0;
@@ -92,6 +107,10 @@ int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
                             void *stream);
 int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
                             int n, void *stream);
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int waves);
+int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, void *stream);
+int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, void *stream);
+int nnspk_set_lds_limit(void);
 int nnspk_malloc(void **p, size_t n);
 int nnspk_free(void *p);
 int nnspk_memset(void *p, int v, size_t n, void *stream);

@@ -15,10 +15,9 @@
 
 #include "nnsp_dev.h"
 #include "nnsp_kabi.h"
+#include "nnsp_nn.h"
 
 using namespace nnsp;
-
-typedef int v4i __attribute__((ext_vector_type(4)));
 
 // ============================================================================
 // Front end
@@ -34,7 +33,10 @@ struct FeLane {
     Tw3 t1, t2, t3;
     int32_t A1[4], A2[4], B1[4];
     int rk[4], rn[4];
-    int mstart, mend, moff;
+    // Mel: this lane's segment (<= 12 coefficients of one bank) and, for lanes
+    // 0..39, which segments make up bank 'lane'
+    int32_t mc[12];
+    int mj0, mn, mfirst, mcnt;
 };
 
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
@@ -50,13 +52,16 @@ __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
         L.rk[m] = rev8(k);
         L.rn[m] = rev8((256 - k) & 255);
     }
-    // Mel bank 'lane' inside the packed [start, end, coef...] table
-    int off = 0;
-    L.mstart = 1; L.mend = 0; L.moff = 0;
-    for (int b = 0; b < 40; ++b) {
-        const int st = nnsp_tbl_mel[off], en = nnsp_tbl_mel[off + 1];
-        if (b == lane) { L.mstart = st; L.mend = en; L.moff = off + 2; }
-        off += 2 + (en - st + 1);
+    const int* sg = nnsp_tbl_melseg + 4 * lane;
+    L.mj0 = sg[1];
+    L.mn = sg[2];
+    for (int i = 0; i < 12; ++i) L.mc[i] = i < L.mn ? nnsp_tbl_mel[sg[3] + i] : 0;
+    L.mfirst = 0;
+    L.mcnt = 0;
+    for (int k = 0; k < 64; ++k) {
+        const int b = nnsp_tbl_melseg[4 * k];
+        if (b == lane && L.mcnt == 0) L.mfirst = k;
+        if (b == lane) ++L.mcnt;
     }
 }
 
@@ -136,32 +141,38 @@ __device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeLane& L
 __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_FRAME_DW];
     __shared__ int32_t Ps[4][264];
+    __shared__ int64_t Ms[4][64];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int32_t* X = Xs[wv];
     int32_t* P = Ps[wv];
+    int64_t* Mp = Ms[wv];
     FeLane L;
     fe_lane_init(L, lane);
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
-    const long long nfr = (long long)a.S * a.T;
-    for (long long f = (long long)blockIdx.x * 4 + wv; f < nfr; f += (long long)gridDim.x * 4) {
-        const int s = (int)(f / a.T), t = (int)(f - (long long)s * a.T);
+    const unsigned nfr = (unsigned)a.S * (unsigned)a.T;   // host guarantees < 2^31
+    const unsigned stride = gridDim.x * 4u;
+    // 16-byte chunk 'lane' (< 60) of frame f's 480-sample window: frames t-2..t
+    auto window_src = [&](unsigned f) -> const int4* {
+        const int s = (int)(f / (unsigned)a.T), t = (int)(f - (unsigned)s * (unsigned)a.T);
+        const int fi = t - 2 + lane / 20, off = (lane % 20) * 8;
+        return reinterpret_cast<const int4*>(fi >= 0 ? a.pcm + ((size_t)s * a.T + fi) * 160 + off
+                                                     : a.tail + (size_t)s * 320 + (fi + 2) * 160 + off);
+    };
+    unsigned f = blockIdx.x * 4u + wv;
+    int4 nxt = make_int4(0, 0, 0, 0);
+    if (f < nfr && lane < 60) nxt = *window_src(f);
+    for (; f < nfr; f += stride) {
+        const int4 raw = nxt;
+        if (f + stride < nfr && lane < 60) nxt = *window_src(f + stride);   // prefetch
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30
-        if (lane < 60) {
-            const int fi = t - 2 + lane / 20, off = (lane % 20) * 8;
-            const int16_t* src = fi >= 0 ? a.pcm + ((size_t)s * a.T + fi) * 160 + off
-                                         : a.tail + (size_t)s * 320 + (fi + 2) * 160 + off;
-            const int4 raw = *reinterpret_cast<const int4*>(src);
+        {
             const int16_t* sm = reinterpret_cast<const int16_t*>(&raw);
             int32_t xv[8];
-            for (int j = 0; j < 8; ++j) xv[j] = (int32_t)L.win[j] * (int32_t)sm[j];
+            for (int j = 0; j < 8; ++j) xv[j] = (int32_t)L.win[j] * (int32_t)sm[j];   // win = 0 past lane 59
             int32_t* q = X + cidx(4 * lane);
             *reinterpret_cast<int4*>(q) = make_int4(xv[0], xv[1], xv[2], xv[3]);
             *reinterpret_cast<int4*>(q + 4) = make_int4(xv[4], xv[5], xv[6], xv[7]);
-        } else {
-            int32_t* q = X + cidx(4 * lane);
-            *reinterpret_cast<int4*>(q) = make_int4(0, 0, 0, 0);
-            *reinterpret_cast<int4*>(q + 4) = make_int4(0, 0, 0, 0);
         }
         wave_lds_sync();
         wave_cfft256(X, L, lane);
@@ -180,11 +191,19 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
             }
         }
         wave_lds_sync();
-        // ---- Mel (melSpecProc.c:6-27), log10 (fixlog10.c:53-61), normalise
+        // ---- Mel (melSpecProc.c:6-27): lane segments of <= 12 MACs, then per bank
+        {
+            int64_t mac = 0;
+#pragma unroll
+            for (int i = 0; i < 12; ++i)
+                if (i < L.mn) mac += (int64_t)L.mc[i] * P[L.mj0 + i];
+            Mp[lane] = mac;
+        }
+        wave_lds_sync();
+        // ---- log10 (fixlog10.c:53-61), normalise (feature_module.c:67-73)
         if (lane < 40) {
             int64_t mac = 0;
-            int o = L.moff;
-            for (int j = L.mstart; j <= L.mend; ++j, ++o) mac += (int64_t)nnsp_tbl_mel[o] * P[j];
+            for (int k = 0; k < L.mcnt; ++k) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15(sat32(mac >> 15));
             if (a.dbg_log) a.dbg_log[(size_t)f * 40 + lane] = lg;
             const int64_t d = (int64_t)lg - mean;
@@ -209,56 +228,6 @@ struct alignas(16) NnLds {
     int32_t slides[16];
     int32_t active[16];
 };
-
-// 16 int16 activations -> hi / lo' int8 planes: x = 256*hi + lo' + 128
-__device__ __forceinline__ void split_hilo(const int16_t* p, v4i& hi, v4i& lo) {
-    const int4 a = *reinterpret_cast<const int4*>(p);
-    const int4 b = *reinterpret_cast<const int4*>(p + 8);
-    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
-    hi.x = (int)__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, HS);
-    hi.y = (int)__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, HS);
-    hi.z = (int)__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, HS);
-    hi.w = (int)__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, HS);
-    lo.x = (int)(__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, LS) ^ 0x80808080u);
-    lo.y = (int)(__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, LS) ^ 0x80808080u);
-    lo.z = (int)(__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, LS) ^ 0x80808080u);
-    lo.w = (int)(__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, LS) ^ 0x80808080u);
-}
-
-__device__ __forceinline__ v4i mfma8(v4i a, v4i b, v4i c) {
-    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ v4i load_frag(const uint8_t* base, int lane) {
-    return *reinterpret_cast<const v4i*>(base + 16 * lane);
-}
-
-// Fixed-point epilogue of affine_Krows (is_out=1): exact sum + bias, shift,
-// clamp (acc64) or wrap (acc32).  'pre' is the int64/int32 pre-bias value.
-__device__ __forceinline__ int32_t affine_out(int64_t pre, int16_t b, const NnLayer& Ly, int acc32) {
-    if (acc32) {
-        int32_t s = (int32_t)pre;
-        if (Ly.has_bias) s = wadd(s, Ly.bias_sh >= 0 ? wshl(b, Ly.bias_sh) : ((int32_t)b >> -Ly.bias_sh));
-        return shift32(s, Ly.out_sh);
-    }
-    int64_t s = pre;
-    if (Ly.has_bias) s += Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
-    return sat32(shift64(s, Ly.out_sh));
-}
-
-__device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) {
-    return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15(v, tt) : sigmoid_q15(v, tt));
-}
-
-// Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
-template <int MAXKT>
-__device__ __forceinline__ void load_b(const int16_t* buf, int stride, int nkt, int lane,
-                                       v4i (&bh)[MAXKT], v4i (&bl)[MAXKT]) {
-    const int sc = lane & 15, q = lane >> 4;
-#pragma unroll
-    for (int kt = 0; kt < MAXKT; ++kt)
-        if (kt < nkt) split_hilo(buf + sc * stride + 64 * kt + 16 * q, bh[kt], bl[kt]);
-}
 
 __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
                               int16_t* out, const int16_t* tt, int lane) {
@@ -341,51 +310,6 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
         const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
         if (commit) cbuf[sc * NN_CW + u] = c_new;
         out[sc * NN_ASTRIDE + u] = hv;
-    }
-}
-
-// Post-processing for one stream (nn_speech.c:146-227); lane-private state.
-struct PostState {
-    int16_t slides, trigger, argmax_last, pad0;
-    int16_t counts[8];
-    int16_t outputs[3], pad1;
-};
-
-__device__ __forceinline__ int argmax_lw(const int32_t* v, int n) {
-    int am = 0;
-    int32_t m = v[0];
-    for (int i = 1; i < n; ++i)
-        if (v[i] >= m) { m = v[i]; am = i; }
-    return am;
-}
-
-__device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, const int32_t* lg) {
-    if (img.nn_id == 0) {  // s2i_post_proc
-        ps.trigger = 0;
-        ps.outputs[0] = ps.outputs[1] = ps.outputs[2] = 0;
-        const int am = argmax_lw(lg, 7);
-        if (ps.argmax_last == 0 || ps.argmax_last == am) {
-            if (am != 0) {
-                ps.counts[am] = (int16_t)(ps.counts[am] + 1);
-                if (ps.counts[am] > img.th_count) {
-                    ps.trigger = 1;
-                    ps.outputs[0] = (int16_t)am;
-                    ps.outputs[1] = (int16_t)argmax_lw(lg + 7, 17);
-                    ps.outputs[2] = (int16_t)argmax_lw(lg + 24, 17);
-                }
-            }
-        } else {
-            for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
-        }
-        ps.argmax_last = (int16_t)am;
-    } else {  // binary_post_proc (T7: logits overwritten by exp2 values)
-        const int32_t mx = lg[0] > lg[1] ? lg[0] : lg[1];
-        int32_t e[2];
-        for (int i = 0; i < 2; ++i) e[i] = pwr2_q15(sat32(((int64_t)wsub(lg[i], mx) * 0xB8AA) >> 15));
-        const int32_t den = wadd(e[0], e[1]);
-        const int32_t lim = (int32_t)(((int64_t)(32768 - img.thresh_prob) * den) >> 15);
-        ps.counts[0] = e[0] <= lim ? (int16_t)(ps.counts[0] + 1) : (int16_t)0;
-        ps.trigger = ps.counts[0] >= img.th_count ? 1 : 0;
     }
 }
 
@@ -484,9 +408,7 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
             }
         }
         if (r.mode != NN_MODE_DIRECT && lane < 16 && active) {
-            int32_t lg[64];
-            for (int o = 0; o < nout && o < 64; ++o)
-                lg[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
+            const LogitRow lg = {fin, lin};
             post_proc(ps, img, lg);
             if (r.trig) {
                 r.trig[(size_t)s * T + t] = ps.trigger;
@@ -616,7 +538,7 @@ __global__ void k_act(int type, const int32_t* x, void* y, int n) {
 __global__ void k_scalar(int op, const int32_t* in, int32_t* out, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (op == 3) {
-        if (i == 0) out[0] = argmax_lw(in, n);
+        if (i == 0) out[0] = argmax_lw(in, n, 0);
         return;
     }
     if (i >= n) return;
@@ -639,10 +561,11 @@ __global__ void k_post(int nn_id, int thresh_prob, int th_count, void* post, int
     PostState* ps = reinterpret_cast<PostState*>(post);
     NnImage im;
     im.nn_id = nn_id; im.thresh_prob = thresh_prob; im.th_count = th_count;
-    int32_t lg[41];
-    const int n = nn_id == 0 ? 41 : 2;
-    for (int i = 0; i < n; ++i) lg[i] = est[i];
-    post_proc(*ps, im, lg);
+    int32_t lg[2] = {est[0], est[1]};
+    if (nn_id == 0)
+        post_proc(*ps, im, est);
+    else
+        post_proc(*ps, im, lg);
     if (nn_id != 0) {
         const int32_t mx = lg[0] > lg[1] ? lg[0] : lg[1];
         for (int i = 0; i < 2; ++i) est[i] = pwr2_q15(sat32(((int64_t)wsub(lg[i], mx) * 0xB8AA) >> 15));

@@ -1,0 +1,119 @@
+// nnsp_nn.h -- shared NN building blocks (int8 MFMA with hi/lo activation
+// planes, the affine_Krows fixed-point epilogue, activations, NNSPClass
+// post-processing) used by the fused and the split NN kernels.
+#pragma once
+#include "nnsp_dev.h"
+#include "nnsp_kabi.h"
+
+namespace nnsp {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+// 16 int16 activations -> hi / lo' int8 planes: x = 256*hi + lo' + 128
+__device__ __forceinline__ void split_hilo(const int16_t* p, v4i& hi, v4i& lo) {
+    const int4 a = *reinterpret_cast<const int4*>(p);
+    const int4 b = *reinterpret_cast<const int4*>(p + 8);
+    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
+    hi.x = (int)__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, HS);
+    hi.y = (int)__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, HS);
+    hi.z = (int)__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, HS);
+    hi.w = (int)__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, HS);
+    lo.x = (int)(__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, LS) ^ 0x80808080u);
+    lo.y = (int)(__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, LS) ^ 0x80808080u);
+    lo.z = (int)(__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, LS) ^ 0x80808080u);
+    lo.w = (int)(__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, LS) ^ 0x80808080u);
+}
+
+__device__ __forceinline__ v4i mfma8(v4i a, v4i b, v4i c) {
+    return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ v4i load_frag(const uint8_t* base, int lane) {
+    return *reinterpret_cast<const v4i*>(base + 16 * lane);
+}
+
+// Fixed-point epilogue of affine_Krows (is_out=1): exact sum + bias, shift,
+// clamp (acc64) or wrap (acc32).  'pre' is the int64/int32 pre-bias value.
+__device__ __forceinline__ int32_t affine_out(int64_t pre, int16_t b, const NnLayer& Ly, int acc32) {
+    if (acc32) {
+        int32_t s = (int32_t)pre;
+        if (Ly.has_bias) s = wadd(s, Ly.bias_sh >= 0 ? wshl(b, Ly.bias_sh) : ((int32_t)b >> -Ly.bias_sh));
+        return shift32(s, Ly.out_sh);
+    }
+    int64_t s = pre;
+    if (Ly.has_bias) s += Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
+    return sat32(shift64(s, Ly.out_sh));
+}
+
+__device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) {
+    return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15(v, tt) : sigmoid_q15(v, tt));
+}
+
+// Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
+template <int MAXKT>
+__device__ __forceinline__ void load_b(const int16_t* buf, int stride, int nkt, int lane,
+                                       v4i (&bh)[MAXKT], v4i (&bl)[MAXKT]) {
+    const int sc = lane & 15, q = lane >> 4;
+#pragma unroll
+    for (int kt = 0; kt < MAXKT; ++kt)
+        if (kt < nkt) split_hilo(buf + sc * stride + 64 * kt + 16 * q, bh[kt], bl[kt]);
+}
+
+// Post-processing for one stream (nn_speech.c:146-227); lane-private state.
+struct PostState {
+    int16_t slides, trigger, argmax_last, pad0;
+    int16_t counts[8];
+    int16_t outputs[3], pad1;
+};
+
+template <typename LG>
+__device__ __forceinline__ int argmax_lw(const LG& v, int n, int off = 0) {
+    int am = 0;
+    int32_t m = v[off];
+    for (int i = 1; i < n; ++i)
+        if (v[off + i] >= m) { m = v[off + i]; am = i; }
+    return am;
+}
+
+// logits view over an LDS row: int32 (linear last layer) or int16
+struct LogitRow {
+    const int16_t* p;
+    bool lin;
+    __device__ __forceinline__ int32_t operator[](int i) const {
+        return lin ? reinterpret_cast<const int32_t*>(p)[i] : (int32_t)p[i];
+    }
+};
+
+template <typename LG>
+__device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, const LG& lg) {
+    if (img.nn_id == 0) {  // s2i_post_proc
+        ps.trigger = 0;
+        ps.outputs[0] = ps.outputs[1] = ps.outputs[2] = 0;
+        const int am = argmax_lw(lg, 7);
+        if (ps.argmax_last == 0 || ps.argmax_last == am) {
+            if (am != 0) {
+                ps.counts[am] = (int16_t)(ps.counts[am] + 1);
+                if (ps.counts[am] > img.th_count) {
+                    ps.trigger = 1;
+                    ps.outputs[0] = (int16_t)am;
+                    ps.outputs[1] = (int16_t)argmax_lw(lg, 17, 7);
+                    ps.outputs[2] = (int16_t)argmax_lw(lg, 17, 24);
+                }
+            }
+        } else {
+            for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
+        }
+        ps.argmax_last = (int16_t)am;
+    } else {  // binary_post_proc (T7: logits overwritten by exp2 values)
+        const int32_t mx = lg[0] > lg[1] ? lg[0] : lg[1];
+        int32_t e[2];
+        for (int i = 0; i < 2; ++i) e[i] = pwr2_q15(sat32(((int64_t)wsub(lg[i], mx) * 0xB8AA) >> 15));
+        const int32_t den = wadd(e[0], e[1]);
+        const int32_t lim = (int32_t)(((int64_t)(32768 - img.thresh_prob) * den) >> 15);
+        ps.counts[0] = e[0] <= lim ? (int16_t)(ps.counts[0] + 1) : (int16_t)0;
+        ps.trigger = ps.counts[0] >= img.th_count ? 1 : 0;
+    }
+}
+
+
+}  // namespace nnsp

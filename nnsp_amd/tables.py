@@ -113,6 +113,33 @@ def rfft512_split_coefs() -> np.ndarray:
     return np.stack([a[32 * k], a[32 * k + 1], b[32 * k]], 1).astype(np.int32)
 
 
+def mel_segments(max_len: int = 12, lanes: int = 64) -> np.ndarray:
+    """Work split of the 40-bank Mel sum over the 64 lanes of a wave.
+
+    Each row = (bank, first bin, n coefficients <= max_len, offset of the first
+    coefficient in the packed table); banks wider than max_len are cut into
+    near-equal segments.  Rows past the last segment have n = 0.  The kernel
+    adds the int64 partial sums of a bank's segments in segment order, which
+    equals the reference's sequential sum (integer addition)."""
+    t = mel_bank_packed().astype(np.int64)
+    segs, off = [], 0
+    for b in range(N_MEL):
+        st, en = int(t[off]), int(t[off + 1])
+        n = en - st + 1
+        k = -(-n // max_len)
+        base, extra = divmod(n, k)
+        j, c = st, off + 2
+        for i in range(k):
+            m = base + (1 if i < extra else 0)
+            segs.append((b, j, m, c))
+            j += m
+            c += m
+        off += 2 + n
+    assert len(segs) <= lanes, len(segs)
+    segs += [(N_MEL, 0, 0, 0)] * (lanes - len(segs))
+    return np.asarray(segs, dtype=np.int32)
+
+
 def bitrev8() -> np.ndarray:
     return np.array([int(f"{i:08b}"[::-1], 2) for i in range(256)], dtype=np.int32)
 
@@ -139,6 +166,7 @@ def header_text() -> str:
         _c_array("int16_t", "nnsp_tbl_tanh", tanh_interp()),
         _c_array("int32_t", "nnsp_tbl_tw256", cfft256_twiddles(), 6),
         _c_array("int32_t", "nnsp_tbl_split", rfft512_split_coefs(), 6),
+        _c_array("int32_t", "nnsp_tbl_melseg", mel_segments(), 4),
         "#endif\n",
     ]
     return "\n".join(parts)

@@ -48,8 +48,20 @@ def _compare(name, acc32, S, chunks, seed=3):
 
 @pytest.mark.parametrize("name", NETS)
 @pytest.mark.parametrize("acc32", [False, True])
-def test_batch_matches_oracle(name, acc32):
+@pytest.mark.parametrize("path", ["split", "fused"])
+def test_batch_matches_oracle(name, acc32, path, monkeypatch):
+    # split = proj_kernel + recur_kernel (default for one-LSTM nets);
+    # fused = the general per-step nn_kernel (any fc/lstm stack)
+    if path == "fused":
+        monkeypatch.setenv("NNSP_FUSED_NN", "1")
+    else:
+        monkeypatch.delenv("NNSP_FUSED_NN", raising=False)
     _compare(name, acc32, S=37, chunks=[24, 7, 1, 10])
+
+
+@pytest.mark.parametrize("name", NETS)
+def test_many_streams_one_long_chunk(name):
+    _compare(name, False, S=600, chunks=[61, 3])
 
 
 @pytest.mark.parametrize("name", NETS)
