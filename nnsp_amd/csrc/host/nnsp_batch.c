@@ -52,13 +52,10 @@ static void plan_fast(nnsp_batch *b)
     const int a_proj = (int)g->L[li].ar_off;
     const int a_rec = (int)(b->im.a_bytes - (size_t)g->L[li].ar_off);
     if (nnspk_fast_lds_bytes(0, a_proj, 4) > LDS_MAX) return;
-    int maxw = 0;
-    for (int w = 1; w <= 4; ++w)
-        if (nnspk_fast_lds_bytes(1, a_rec, w) <= LDS_MAX) maxw = w;
-    if (!maxw) return;
+    if (nnspk_fast_lds_bytes(1, a_rec, 1) > LDS_MAX) return;
+    /* tiles per 4-wave group in one workgroup: 2 once there are >= 2 tiles per CU */
     const int tiles = (b->S + 15) / 16;
-    int w = (tiles + 255) / 256;
-    b->rec_waves = w < 1 ? 1 : (w > maxw ? maxw : w);
+    b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2) <= LDS_MAX) ? 2 : 1;
     b->li = li;
     b->nstep_max = (b->Tmax + 1) / 2;
     const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);

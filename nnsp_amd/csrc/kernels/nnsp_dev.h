@@ -137,18 +137,18 @@ __device__ __forceinline__ int32_t log10_q15(int32_t x) {
 
 // ---- activations (activation.c) --------------------------------------------
 __device__ __forceinline__ int16_t tanh_q15(int32_t x, const int16_t* tbl) {   // :31-69
+    // branch-free form: the segment index is always in range (only |x| =
+    // INT32_MIN, unreachable here, would index out of the reference's table)
+    // and the (value, slope) pair is one 32-bit load
     const bool neg = x < 0;
     const int32_t a = neg ? wsub(0, x) : x;
-    int16_t y;
-    if (a >= (5 << 15)) {
-        y = 0x7fff;
-    } else {
-        int32_t kx = wsub(a, 512) >> 10;
-        kx = kx < 0 ? 0 : (kx > 191 ? 191 : kx);
-        const int32_t dx = a - 512 - (kx << 10);
-        const int32_t v = tbl[2 * kx] + ((dx * tbl[2 * kx + 1]) >> 15);
-        y = (int16_t)(v > 0 ? v : 0);
-    }
+    int32_t kx = wsub(a, 512) >> 10;
+    kx = kx < 0 ? 0 : (kx > 191 ? 191 : kx);
+    const int32_t dx = wsub(wsub(a, 512), kx << 10);
+    const uint32_t pr = reinterpret_cast<const uint32_t*>(tbl)[kx];
+    const int32_t v = (int32_t)(int16_t)(pr & 0xffff) +
+                      ((int32_t)((uint32_t)dx * (uint32_t)(int32_t)(int16_t)(pr >> 16)) >> 15);
+    const int16_t y = a >= (5 << 15) ? (int16_t)0x7fff : (int16_t)(v > 0 ? v : 0);
     return neg ? (int16_t)-y : y;
 }
 __device__ __forceinline__ int16_t sigmoid_q15(int32_t x, const int16_t* tbl) {   // :72-87

@@ -146,147 +146,176 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
 }
 
 // ---------------------------------------------------------------------------
-// recur_kernel
+// recur_kernel: one 16-stream tile per RG waves (row tiles dealt round-robin),
+// TPW tiles per workgroup; weights staged once per workgroup.
 // ---------------------------------------------------------------------------
-struct RecWave {
-    int16_t h[16][R_STRIDE];
-    int16_t act[2][16][R_STRIDE];
+#define RG 4
+
+struct RecTile {
+    int16_t h[2][16][R_STRIDE];     // LSTM h, ping-pong across steps
+    int16_t act[2][16][R_STRIDE];   // FC activations, ping-pong across layers
     int32_t c[16][R_CW];
-    int32_t active[16];
     int32_t phase[16];
+    int32_t pad[16];
 };
 
-template <int NRT>
-__global__ __launch_bounds__(256) void recur_kernel(NnImage img, FastRun r) {
+template <int RPW>   // LSTM row tiles per wave = ceil(nrt / RG)
+__global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    RecWave* rw = reinterpret_cast<RecWave*>(smem + r.a_lds_bytes + 768);
+    RecTile* tiles = reinterpret_cast<RecTile*>(smem + r.a_lds_bytes + 768);
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    RecWave& R = rw[wv];
+    const int tpw = blockDim.x / (64 * RG);
+    const int tl = wv / RG, g = wv - tl * RG;   // tile in workgroup, wave in tile
+    RecTile& R = tiles[tl];
     const int sc = lane & 15, q = lane >> 4;
-    const int s0 = (blockIdx.x * (blockDim.x >> 6) + wv) * 16;
+    const int s0 = (blockIdx.x * tpw + tl) * 16;
     const int s = s0 + sc;
     const bool valid = s < r.S;
     const NnLayer& LL = img.L[r.li];
     const int N = LL.N, rows = LL.rows, nrt = LL.nrt;
-    // ---- LSTM state in (rows of NN_MAX_W)
-    for (int idx = lane; idx < 16 * N; idx += 64) {
+    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
         const int st = idx / N, u = idx - st * N, gs = s0 + st;
         const bool ok = gs < r.S;
-        R.h[st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
+        R.h[0][st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
         R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
     }
     PostState ps = {};
-    if (lane < 16) {
+    if (g == 0 && lane < 16) {
         if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
         R.phase[lane] = valid ? 1 - ps.slides : 0;
     }
-    __syncthreads();   // weights staged, per-wave state loaded
+    __syncthreads();
     const int phase = R.phase[sc];
     const int T = r.T;
     const int nsteps = (T + 1) / 2;
-    if (lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
-    const uint8_t* Ar = W;   // LSTM recurrent fragments come first in the staged region
-    // gate partial sums (independent of h): step j+1's are loaded while step j
-    // finishes its FC layers and post-processing
-    v4i gxv[NRT];
+    if (g == 0 && lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
+    const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
+    v4i gxv[RPW];
     auto load_gx = [&](int jj) {
         const bool ok = valid && 2 * jj + phase < T;
         const int32_t* gsrc = r.gx + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * rows + 4 * q;
 #pragma unroll
-        for (int rt = 0; rt < NRT; ++rt)
-            if (rt < nrt) gxv[rt] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
+        for (int k = 0; k < RPW; ++k) {
+            const int rt = g + RG * k;
+            if (rt < nrt) gxv[k] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
+        }
     };
     load_gx(0);
+    int hb = 0;
     for (int j = 0; j < nsteps; ++j) {
         const int t = 2 * j + phase;
         const bool active = valid && t < T;
-        if (lane < 16) R.active[lane] = active;
         v4i bh[2], bl[2];
-        load_b<2>(&R.h[0][0], R_STRIDE, LL.nkt_r, lane, bh, bl);
-        // ---- LSTM (lstm.c:48-124): per row tile = 4 units x gates i,j,f,o
+        load_b<2>(&R.h[hb][0][0], R_STRIDE, LL.nkt_r, lane, bh, bl);
+        // ---- LSTM (lstm.c:48-124): row tile = 4 units x gates i, j, f, o
 #pragma unroll
-        for (int rt = 0; rt < NRT; ++rt) {
+        for (int k = 0; k < RPW; ++k) {
+            const int rt = g + RG * k;
             if (rt < nrt) {
-            v4i hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
+                v4i hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
 #pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
-                if (kt < LL.nkt_r) {
-                    const v4i w = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * LL.nkt_r + kt) * 1024 + 16 * lane);
-                    hh = mfma8(w, bh[kt], hh);
-                    hl = mfma8(w, bl[kt], hl);
-                }
-            const int u = 4 * rt + q;
-            if (u < N) {
-                int16_t g[4];
+                for (int kt = 0; kt < 2; ++kt)
+                    if (kt < LL.nkt_r) {
+                        const v4i w = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * LL.nkt_r + kt) * 1024 + 16 * lane);
+                        hh = mfma8(w, bh[kt], hh);
+                        hl = mfma8(w, bl[kt], hl);
+                    }
+                const int u = 4 * rt + q;
+                if (u < N) {
+                    int16_t gt[4];
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = 16 * rt + 4 * q + i;
-                    const int32_t sx = gxv[rt][i];
-                    const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[LL.ep_off + row];
-                    int64_t pre;
-                    if (img.acc32)
-                        pre = (int64_t)wadd(shift32(sx, LL.xs_sh), sh);
-                    else
-                        pre = shift64((int64_t)sx, LL.xs_sh) + (int64_t)sh;
-                    const int32_t v = affine_out(pre, img.bias[LL.ep_off + row], LL, img.acc32);
-                    g[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = 16 * rt + 4 * q + i;
+                        const int32_t sx = gxv[k][i];
+                        const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[LL.ep_off + row];
+                        int64_t pre;
+                        if (img.acc32)
+                            pre = (int64_t)wadd(shift32(sx, LL.xs_sh), sh);
+                        else
+                            pre = shift64((int64_t)sx, LL.xs_sh) + (int64_t)sh;
+                        const int32_t v = affine_out(pre, img.bias[LL.ep_off + row], LL, img.acc32);
+                        gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                    }
+                    const int32_t c_old = R.c[sc][u];
+                    const int32_t c_new = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old) >> 15);
+                    const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * gt[3]) >> 15);
+                    if (active) R.c[sc][u] = c_new;
+                    R.h[hb ^ 1][sc][u] = active ? hv : R.h[hb][sc][u];   // h after all groups (T6)
                 }
-                const int32_t c_old = R.c[sc][u];
-                const int32_t c_new = sat32(((int64_t)g[0] * g[1] + (int64_t)g[2] * c_old) >> 15);
-                const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
-                if (active) R.c[sc][u] = c_new;
-                R.act[0][sc][u] = hv;
-            }
             }
         }
         if (j + 1 < nsteps) load_gx(j + 1);
-        wave_lds_sync();
-        for (int idx = lane; idx < 16 * N; idx += 64) {   // h := output (T6)
-            const int st = idx / N, u = idx - st * N;
-            if (R.active[st]) R.h[st][u] = R.act[0][st][u];
-        }
-        // ---- FC layers after the LSTM
+        __syncthreads();
+        hb ^= 1;
+        // ---- FC layers after the LSTM (rows tiles dealt over the RG waves)
+        const int16_t* in = &R.h[hb][0][0];
         int cur = 0;
         for (int i = r.li + 1; i < img.nl; ++i) {
             const NnLayer& Ly = img.L[i];
-            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), &R.act[cur][0][0], R_STRIDE,
-                    &R.act[cur ^ 1][0][0], R_STRIDE, tt, lane);
-            wave_lds_sync();
+            const uint8_t* A = W + (Ly.a_off - r.a_off);
+            int16_t* out = &R.act[cur][0][0];
+            v4i fh[2], fl[2];
+            load_b<2>(in, R_STRIDE, Ly.nkt, lane, fh, fl);
+            for (int rt = g; rt < Ly.nrt; rt += RG) {
+                v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+                    if (kt < Ly.nkt) {
+                        const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * Ly.nkt + kt) * 1024 + 16 * lane);
+                        ah = mfma8(w, fh[kt], ah);
+                        al = mfma8(w, fl[kt], al);
+                    }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int row = 16 * rt + 4 * q + e;
+                    if (row >= Ly.rows) continue;
+                    const int32_t sum = (ah[e] << 8) + al[e] + img.wsum[Ly.ep_off + row];
+                    const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
+                    if (Ly.act == ACT_LINEAR)
+                        reinterpret_cast<int32_t*>(out + sc * R_STRIDE)[row] = v;
+                    else
+                        out[sc * R_STRIDE + row] = act16(Ly.act, v, tt);
+                }
+            }
+            __syncthreads();
+            in = out;
             cur ^= 1;
         }
-        // ---- outputs and post-processing (nn_speech.c:92-124)
-        const int16_t* fin = &R.act[cur][sc][0];
-        const NnLayer& LO = img.L[img.nl - 1];
-        const int nout = LO.N;
-        const bool lin = LO.act == ACT_LINEAR;
-        if (active && r.logits) {
-            int32_t* dst = r.logits + ((size_t)s * T + t) * nout;
-            for (int o = q; o < nout; o += 4)
-                dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
-        }
-        if (lane < 16 && active) {
-            const LogitRow lg = {fin, lin};
-            post_proc(ps, img, lg);
-            if (r.trig) {
-                r.trig[(size_t)s * T + t] = ps.trigger;
-                if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+        // ---- outputs and post-processing (nn_speech.c:92-124), wave 0 of the tile
+        if (g == 0) {
+            const int16_t* fin = in + sc * R_STRIDE;
+            const NnLayer& LO = img.L[img.nl - 1];
+            const int nout = LO.N;
+            const bool lin = LO.act == ACT_LINEAR;
+            if (active && r.logits) {
+                int32_t* dst = r.logits + ((size_t)s * T + t) * nout;
+                for (int o = q; o < nout; o += 4)
+                    dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
+            }
+            if (lane < 16 && active) {
+                const LogitRow lg = {fin, lin};
+                post_proc(ps, img, lg);
+                if (r.trig) {
+                    r.trig[(size_t)s * T + t] = ps.trigger;
+                    if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+                }
             }
         }
-        wave_lds_sync();
+        __syncthreads();
     }
     // ---- state out
-    for (int idx = lane; idx < 16 * N; idx += 64) {
+    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
         const int st = idx / N, u = idx - st * N, gs = s0 + st;
         if (gs < r.S) {
-            r.h[(size_t)gs * NN_MAX_W + u] = R.h[st][u];
+            r.h[(size_t)gs * NN_MAX_W + u] = R.h[hb][st][u];
             r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
         }
     }
-    if (lane < 16 && valid) {
+    if (g == 0 && lane < 16 && valid) {
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
@@ -294,30 +323,33 @@ __global__ __launch_bounds__(256) void recur_kernel(NnImage img, FastRun r) {
 
 extern "C" {
 
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int waves) {
-    if (which == 0) return (size_t)a_bytes + 768 + (size_t)waves * sizeof(ProjWave);
-    return (size_t)a_bytes + 768 + (size_t)waves * sizeof(RecWave);
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units) {
+    // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
+    if (which == 0) return (size_t)a_bytes + 768 + (size_t)units * sizeof(ProjWave);
+    return (size_t)a_bytes + 768 + (size_t)units * sizeof(RecTile);
 }
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4);
     hipLaunchKernelGGL(proj_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, *img, *r);
-    return hipGetLastError() == hipSuccess ? 0 : (int)hipGetLastError();
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
 }
 
-int nnspk_launch_recur(const NnImage* img, const FastRun* r, int waves, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, waves);
+int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
+    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw);
     const int tiles = (r->S + 15) / 16;
-    const int blocks = (tiles + waves - 1) / waves;
-    const int nrt = img->L[r->li].nrt;
-    if (nrt <= 8)
-        hipLaunchKernelGGL(recur_kernel<8>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
-    else if (nrt <= 16)
-        hipLaunchKernelGGL(recur_kernel<16>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
-    else if (nrt <= 18)
-        hipLaunchKernelGGL(recur_kernel<18>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+    const int blocks = (tiles + tpw - 1) / tpw;
+    const int rpw = (img->L[r->li].nrt + RG - 1) / RG;
+    const dim3 grid(blocks), blk(64 * RG * tpw);
+    if (rpw <= 2)
+        hipLaunchKernelGGL(recur_kernel<2>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+    else if (rpw <= 4)
+        hipLaunchKernelGGL(recur_kernel<4>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+    else if (rpw <= 5)
+        hipLaunchKernelGGL(recur_kernel<5>, grid, blk, lds, (hipStream_t)stream, *img, *r);
     else
-        hipLaunchKernelGGL(recur_kernel<32>, dim3(blocks), dim3(64 * waves), lds, (hipStream_t)stream, *img, *r);
+        hipLaunchKernelGGL(recur_kernel<8>, grid, blk, lds, (hipStream_t)stream, *img, *r);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -326,8 +358,8 @@ int nnspk_set_lds_limit(void) {
     // allow up to 160 KiB of dynamic LDS for the split kernels
     hipError_t e = hipFuncSetAttribute((const void*)proj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
-    const void* ks[4] = {(const void*)recur_kernel<8>, (const void*)recur_kernel<16>,
-                         (const void*)recur_kernel<18>, (const void*)recur_kernel<32>};
+    const void* ks[4] = {(const void*)recur_kernel<2>, (const void*)recur_kernel<4>,
+                         (const void*)recur_kernel<5>, (const void*)recur_kernel<8>};
     for (int i = 0; i < 4; ++i) {
         e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;

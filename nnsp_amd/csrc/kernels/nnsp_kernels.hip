@@ -29,33 +29,54 @@ using namespace nnsp;
 __device__ __forceinline__ int cidx(int c) { return 2 * c + 32 * (c >> 6); }
 
 struct FeLane {
-    int16_t win[8];
-    Tw3 t1, t2, t3;
-    int32_t A1[4], A2[4], B1[4];
-    int rk[4], rn[4];
-    // Mel: this lane's segment (<= 12 coefficients of one bank) and, for lanes
-    // 0..39, which segments make up bank 'lane'
-    int32_t mc[12];
-    int mj0, mn, mfirst, mcnt;
+    uint32_t win[4];      // window taps 8*lane .. 8*lane+7 as int16 pairs (0 past lane 59)
+    uint32_t mc[6];       // Mel segment coefficients as int16 pairs
+    int rk[4], rn[4];     // bit-reversed slots of bins k and 256-k, k = lane + 64m
+    int mj0, mfirst, mcnt;
 };
 
+// Block-shared constant tables (LDS).
+struct FeTables {
+    int32_t tw[384];      // twiddleCoef_256_q31: (cos, sin) pairs
+    int4 split[256];      // per bin k: (A_re, A_im, B_re, 0) of realCoefA/BQ31 at 16k
+    uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
+};
+
+__device__ __forceinline__ void fe_tables_init(FeTables& T) {
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) T.tw[i] = nnsp_tbl_tw256[i];
+    for (int k = threadIdx.x; k < 256; k += blockDim.x)
+        T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
+    for (int i = threadIdx.x; i < 128; i += blockDim.x)
+        T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
+}
+
+__device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int k) {
+    Tw3 t;
+    const int2 a = *reinterpret_cast<const int2*>(&T.tw[2 * k]);
+    const int2 b = *reinterpret_cast<const int2*>(&T.tw[4 * k]);
+    const int2 c = *reinterpret_cast<const int2*>(&T.tw[6 * k]);
+    t.c1 = a.x; t.s1 = a.y; t.c2 = b.x; t.s2 = b.y; t.c3 = c.x; t.s3 = c.y;
+    return t;
+}
+
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
-    for (int j = 0; j < 8; ++j) L.win[j] = lane < 60 ? nnsp_tbl_window[8 * lane + j] : 0;
-    L.t1 = load_tw3(lane);
-    L.t2 = load_tw3(4 * (lane & 15));
-    L.t3 = load_tw3(16 * (lane & 3));
+    for (int j = 0; j < 4; ++j)
+        L.win[j] = lane < 60 ? ((uint32_t)(uint16_t)nnsp_tbl_window[8 * lane + 2 * j] |
+                                ((uint32_t)(uint16_t)nnsp_tbl_window[8 * lane + 2 * j + 1] << 16))
+                             : 0u;
     for (int m = 0; m < 4; ++m) {
         const int k = lane + 64 * m;
-        L.A1[m] = nnsp_tbl_split[3 * k];
-        L.A2[m] = nnsp_tbl_split[3 * k + 1];
-        L.B1[m] = nnsp_tbl_split[3 * k + 2];
         L.rk[m] = rev8(k);
         L.rn[m] = rev8((256 - k) & 255);
     }
     const int* sg = nnsp_tbl_melseg + 4 * lane;
     L.mj0 = sg[1];
-    L.mn = sg[2];
-    for (int i = 0; i < 12; ++i) L.mc[i] = i < L.mn ? nnsp_tbl_mel[sg[3] + i] : 0;
+    const int mn = sg[2];
+    for (int i = 0; i < 6; ++i) {
+        const int lo = 2 * i < mn ? nnsp_tbl_mel[sg[3] + 2 * i] : 0;
+        const int hi = 2 * i + 1 < mn ? nnsp_tbl_mel[sg[3] + 2 * i + 1] : 0;
+        L.mc[i] = (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+    }
     L.mfirst = 0;
     L.mcnt = 0;
     for (int k = 0; k < 64; ++k) {
@@ -65,8 +86,23 @@ __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
     }
 }
 
+// log10 with the (value, slope) table in LDS (fixlog10.c:31-61, bit_frac_in 15)
+__device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp) {
+    if (x == 0) x = 1;
+    const uint32_t m = (uint32_t)x & 0x7FFFFFFFu;
+    const int sh = m ? 15 - (31 - __clz((int)m)) : 0;
+    const int32_t y = sh >= 0 ? wshl(x, sh) : (x >> -sh);
+    int32_t kx = (y - 32768) >> 8;
+    const int32_t dx = (y - 32768) - (kx << 8);
+    kx = kx < 0 ? 0 : (kx > 127 ? 127 : kx);
+    const uint32_t pr = logp[kx];
+    int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (((int32_t)(int16_t)(pr >> 16) * dx) >> 15);
+    v = (int32_t)(((int64_t)v * 0x3796) >> 15);
+    return wadd(v, 0x2688 * -sh);
+}
+
 // In-place radix-4 cFFT (arm_radix4_butterfly_q31) of one frame held in LDS.
-__device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int lane) {
+__device__ __forceinline__ void wave_cfft256(int32_t* X, const FeTables& TB, int lane) {
     // stage 1: butterfly i0 = lane, stride 64
     {
         int32_t v[8];
@@ -74,7 +110,7 @@ __device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int la
             const int2 p = *reinterpret_cast<const int2*>(X + cidx(lane + 64 * m));
             v[2 * m] = p.x; v[2 * m + 1] = p.y;
         }
-        bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t1);
+        bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, lane));
         for (int m = 0; m < 4; ++m)
             *reinterpret_cast<int2*>(X + cidx(lane + 64 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
     }
@@ -87,7 +123,7 @@ __device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int la
             const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 16 * m));
             v[2 * m] = p.x; v[2 * m + 1] = p.y;
         }
-        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t2);
+        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 4 * (lane & 15)));
         for (int m = 0; m < 4; ++m)
             *reinterpret_cast<int2*>(X + cidx(i0 + 16 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
     }
@@ -100,7 +136,7 @@ __device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int la
             const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 4 * m));
             v[2 * m] = p.x; v[2 * m + 1] = p.y;
         }
-        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], L.t3);
+        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 16 * (lane & 3)));
         for (int m = 0; m < 4; ++m)
             *reinterpret_cast<int2*>(X + cidx(i0 + 4 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
     }
@@ -120,28 +156,30 @@ __device__ __forceinline__ void wave_cfft256(int32_t* X, const FeLane& L, int la
 }
 
 // Split of bin k = lane + 64m from the (not yet bit-reversed) cFFT output Y.
-// Lane 0 / m 0 produces DC (re0) and Nyquist (reN) instead.
-__device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeLane& L, int lane, int m,
-                                               int32_t& re, int32_t& im, int32_t& reN) {
-    if (lane == 0 && m == 0) {
-        const int2 z0 = *reinterpret_cast<const int2*>(X + cidx(0));
-        re = wadd(z0.x, z0.y) >> 1;
-        im = 0;
-        reN = wsub(z0.x, z0.y) >> 1;
-        return;
-    }
+// (k = 0 yields a don't-care value; DC / Nyquist come from wave_split_dc.)
+__device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeLane& L, const FeTables& TB,
+                                               int lane, int m, int32_t& re, int32_t& im) {
+    const int4 cf = TB.split[lane + 64 * m];
     const int2 zk = *reinterpret_cast<const int2*>(X + cidx(L.rk[m]));
     const int2 zn = *reinterpret_cast<const int2*>(X + cidx(L.rn[m]));
-    split_bin(zk.x, zk.y, zn.x, zn.y, L.A1[m], L.A2[m], L.B1[m], re, im);
-    reN = 0;
+    split_bin(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re, im);
+}
+
+// DC and Nyquist bins: (p0 + p1) >> 1, (p0 - p1) >> 1 (arm_split_rfft_q31 tail)
+__device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int32_t& nyq) {
+    const int2 z0 = *reinterpret_cast<const int2*>(X + cidx(0));
+    dc = wadd(z0.x, z0.y) >> 1;
+    nyq = wsub(z0.x, z0.y) >> 1;
 }
 
 // One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.
 // 'buf' supplies the 480 samples (frames t-2, t-1, t) in 8-sample chunks.
 __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_FRAME_DW];
-    __shared__ int32_t Ps[4][264];
+    __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
     __shared__ int64_t Ms[4][64];
+    __shared__ __attribute__((aligned(16))) FeTables TB;
+    fe_tables_init(TB);
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     int32_t* X = Xs[wv];
     int32_t* P = Ps[wv];
@@ -150,6 +188,7 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     fe_lane_init(L, lane);
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
+    __syncthreads();
     const unsigned nfr = (unsigned)a.S * (unsigned)a.T;   // host guarantees < 2^31
     const unsigned stride = gridDim.x * 4u;
     // 16-byte chunk 'lane' (< 60) of frame f's 480-sample window: frames t-2..t
@@ -167,36 +206,54 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
         if (f + stride < nfr && lane < 60) nxt = *window_src(f + stride);   // prefetch
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30
         {
-            const int16_t* sm = reinterpret_cast<const int16_t*>(&raw);
+            const uint32_t rw[4] = {(uint32_t)raw.x, (uint32_t)raw.y, (uint32_t)raw.z, (uint32_t)raw.w};
             int32_t xv[8];
-            for (int j = 0; j < 8; ++j) xv[j] = (int32_t)L.win[j] * (int32_t)sm[j];   // win = 0 past lane 59
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {   // win = 0 past lane 59
+                xv[2 * j] = (int32_t)(int16_t)(L.win[j] & 0xffff) * (int32_t)(int16_t)(rw[j] & 0xffff);
+                xv[2 * j + 1] = (int32_t)(int16_t)(L.win[j] >> 16) * (int32_t)(int16_t)(rw[j] >> 16);
+            }
             int32_t* q = X + cidx(4 * lane);
             *reinterpret_cast<int4*>(q) = make_int4(xv[0], xv[1], xv[2], xv[3]);
             *reinterpret_cast<int4*>(q + 4) = make_int4(xv[4], xv[5], xv[6], xv[7]);
         }
         wave_lds_sync();
-        wave_cfft256(X, L, lane);
+        wave_cfft256(X, TB, lane);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
+#pragma unroll
         for (int m = 0; m < 4; ++m) {
-            int32_t re, im, reN;
-            wave_split_bin(X, L, lane, m, re, im, reN);
+            int32_t re, im;
+            wave_split_bin(X, L, TB, lane, m, re, im);
             P[lane + 64 * m] = pspec_of(re, im);
-            if (lane == 0 && m == 0) P[256] = pspec_of(reN, 0);
             if (a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)f * 1024;
                 const int k = lane + 64 * m;
-                ds[2 * k] = re; ds[2 * k + 1] = im;
-                if (k) { ds[1024 - 2 * k] = re; ds[1024 - 2 * k + 1] = wsub(0, im); }
-                else { ds[512] = reN; ds[513] = 0; }
+                if (k) {
+                    ds[2 * k] = re; ds[2 * k + 1] = im;
+                    ds[1024 - 2 * k] = re; ds[1024 - 2 * k + 1] = wsub(0, im);
+                }
+            }
+        }
+        if (lane == 0) {
+            int32_t dc, nyq;
+            wave_split_dc(X, dc, nyq);
+            P[0] = pspec_of(dc, 0);
+            P[256] = pspec_of(nyq, 0);
+            if (a.dbg_spec) {
+                int32_t* ds = a.dbg_spec + (size_t)f * 1024;
+                ds[0] = dc; ds[1] = 0; ds[512] = nyq; ds[513] = 0;
             }
         }
         wave_lds_sync();
-        // ---- Mel (melSpecProc.c:6-27): lane segments of <= 12 MACs, then per bank
+        // ---- Mel (melSpecProc.c:6-27): lane segments of <= 12 MACs (zero-padded), then per bank
         {
             int64_t mac = 0;
 #pragma unroll
-            for (int i = 0; i < 12; ++i)
-                if (i < L.mn) mac += (int64_t)L.mc[i] * P[L.mj0 + i];
+            for (int i = 0; i < 6; ++i) {
+                const int2 pv = make_int2(P[L.mj0 + 2 * i], P[L.mj0 + 2 * i + 1]);
+                mac += (int64_t)(int16_t)(L.mc[i] & 0xffff) * pv.x;
+                mac += (int64_t)(int16_t)(L.mc[i] >> 16) * pv.y;
+            }
             Mp[lane] = mac;
         }
         wave_lds_sync();
@@ -204,10 +261,10 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
         if (lane < 40) {
             int64_t mac = 0;
             for (int k = 0; k < L.mcnt; ++k) mac += Mp[L.mfirst + k];
-            const int32_t lg = log10_q15(sat32(mac >> 15));
+            const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
             if (a.dbg_log) a.dbg_log[(size_t)f * 40 + lane] = lg;
             const int64_t d = (int64_t)lg - mean;
-            a.feats[(size_t)f * 40 + lane] = sat16((d * stdR) >> a.norm_shift);  // feature_module.c:67-73
+            a.feats[(size_t)f * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
         }
         wave_lds_sync();
     }
@@ -467,9 +524,12 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
 // ============================================================================
 __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
     __shared__ __attribute__((aligned(16))) int32_t X[FE_FRAME_DW];
+    __shared__ __attribute__((aligned(16))) FeTables TB;
+    fe_tables_init(TB);
     const int lane = threadIdx.x;
     FeLane L;
     fe_lane_init(L, lane);
+    __syncthreads();
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
         int32_t* xb = x + (size_t)b * 512;
         for (int c = lane; c < 256; c += 64) {
@@ -477,15 +537,21 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
             X[cidx(c) + 1] = xb[2 * c + 1];
         }
         wave_lds_sync();
-        wave_cfft256(X, L, lane);
+        wave_cfft256(X, TB, lane);
         int32_t* yb = y + (size_t)b * 1024;
         for (int m = 0; m < 4; ++m) {
-            int32_t re, im, reN;
-            wave_split_bin(X, L, lane, m, re, im, reN);
+            int32_t re, im;
+            wave_split_bin(X, L, TB, lane, m, re, im);
             const int k = lane + 64 * m;
-            yb[2 * k] = re; yb[2 * k + 1] = im;
-            if (k) { yb[1024 - 2 * k] = re; yb[1024 - 2 * k + 1] = wsub(0, im); }
-            else { yb[512] = reN; yb[513] = 0; }
+            if (k) {
+                yb[2 * k] = re; yb[2 * k + 1] = im;
+                yb[1024 - 2 * k] = re; yb[1024 - 2 * k + 1] = wsub(0, im);
+            }
+        }
+        if (lane == 0) {
+            int32_t dc, nyq;
+            wave_split_dc(X, dc, nyq);
+            yb[0] = dc; yb[1] = 0; yb[512] = nyq; yb[513] = 0;
         }
         // pSrc holds the bit-reversed cFFT output afterwards (in-place CMSIS)
         for (int c = lane; c < 256; c += 64) {

@@ -149,7 +149,8 @@ def _c_array(ctype: str, name: str, vals, per_line: int = 12) -> str:
     lines = []
     for i in range(0, len(vals), per_line):
         lines.append("    " + ", ".join(str(v) for v in vals[i:i + per_line]) + ",")
-    return f"static const {ctype} {name}[{len(vals)}] = {{\n" + "\n".join(lines) + "\n};\n"
+    return (f"static const {ctype} {name}[{len(vals)}] __attribute__((aligned(16))) = {{\n"
+            + "\n".join(lines) + "\n};\n")
 
 
 def header_text() -> str:
