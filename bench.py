@@ -1,12 +1,17 @@
 #!/usr/bin/env python3
 """Throughput benchmark of the ns-nnsp hot path on MI355X.
 
-Metric (BASELINE.json): audio frames/s (16 kHz, 10 ms hop) per node, bit-exact
-vs the reference.  One frame = 160 samples of one stream.  A "step" is one
-chunk of --frames frames (default 100 = 1 s of audio) for every stream of the
-GPU's shard; streams carry their state across steps (continuous audio).  Input
-PCM is generated on the device (SplitMix64, oracle.synthetic_pcm) before the
-timed region; nothing crosses PCIe inside it.
+Metric (BASELINE.json): audio frames/s (16 kHz, 10 ms hop) per node at
+1/2/4/8 GPUs, bit-exact vs the reference.  One frame = 160 samples of one
+stream.  The default workload is BASELINE configs[4], the one the 1/2/4/8-GPU
+curve is quoted on: the full VAD -> Hi-Galaxy KWS -> S2I cascade
+(nnCntrlClass_exec per frame) with 32768 streams per GPU (262144 on 8 GPUs).
+--net vad|kws|s2i runs configs[1..3] (one net, 8192 streams/GPU).
+
+A "step" is one chunk of --frames frames (default 100 = 1 s of audio) for
+every stream of the GPU's shard; streams carry their state across steps
+(continuous audio).  Input PCM is generated on the device (SplitMix64,
+oracle.synthetic_pcm) before the timed region; nothing crosses PCIe inside it.
 
 Multi-GPU: one process per GPU (torch.distributed, RCCL backend); every rank
 owns its own shard of --streams streams (weak scaling, no data-path
@@ -30,6 +35,7 @@ NN_MACS_PER_INFERENCE = {"vad": 14616, "kws": 56448, "s2i": 72072}
 FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out
 
 WORKLOADS = {  # BASELINE.json configs
+    "cascade": "configs[4]: VAD->Hi-Galaxy KWS->S2I cascade, 32768 streams/GPU (262144 on 8 GPUs)",
     "vad": "configs[1]: VAD net, 8192 streams/GPU, Mel front end + int8xint16 FC/LSTM, 64b accum",
     "kws": "configs[2]: Hi-Galaxy KWS net, 8192 streams/GPU",
     "s2i": "configs[3]: S2I RNN, 8192 streams/GPU",
@@ -55,17 +61,22 @@ def cpu_baseline(net: str, acc32: bool, seconds: float = 1.5, procs: int | None 
 
 def _cpu_worker(net: str, acc32: bool, seconds: float, idx: int) -> int:
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from oracle import OracleNet, synthetic_pcm
+    from oracle import OracleCascade, OracleNet, synthetic_pcm
 
     from nnsp_amd.nets import synth_net
 
-    orc = OracleNet(synth_net(net), acc32=acc32)
     S, T = 32, 100
-    st = orc.new_states(S)
+    if net == "cascade":
+        orc = OracleCascade({n: OracleNet(synth_net(n), acc32=acc32) for n in ("vad", "kws", "s2i")})
+        st = orc.new_states(S)
+        run = lambda pcm: orc.run(pcm, st)  # noqa: E731
+    else:
+        orc = OracleNet(synth_net(net), acc32=acc32)
+        st = orc.new_states(S)
+        run = lambda pcm: orc.run(pcm, st, want_logits=False, want_feats=False)  # noqa: E731
     frames, t0, c = 0, time.perf_counter(), 0
     while time.perf_counter() - t0 < seconds:
-        pcm = synthetic_pcm(S, T, s0=idx * S, t0=c * T)
-        orc.run(pcm, st, want_logits=False, want_feats=False)
+        run(synthetic_pcm(S, T, s0=idx * S, t0=c * T))
         frames += S * T
         c += 1
     return frames
@@ -76,8 +87,10 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--net", default="vad", choices=sorted(WORKLOADS))
-    ap.add_argument("--streams", type=int, default=8192, help="streams per GPU")
+    ap.add_argument("--net", default="cascade", choices=sorted(WORKLOADS))
+    ap.add_argument("--streams", type=int, default=0,
+                    help="streams per GPU (default 32768 for the cascade, 8192 for one net)")
+    ap.add_argument("--window", type=int, default=-1, help="cascade frames per round (-1: library default)")
     ap.add_argument("--frames", type=int, default=100, help="frames per step (chunk)")
     ap.add_argument("--acc32", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -103,29 +116,61 @@ def main() -> None:
     from nnsp_amd.engine import NNSPBatch, device_info
 
     _lib.check(_lib.lib().nnsp_set_device(local if world > 1 else 0), "set_device")
-    S, T, K, W = args.streams, args.frames, args.steps, args.warmup
-    eng = NNSPBatch(args.net, S, T, acc32=args.acc32)
+    S = args.streams or (32768 if args.net == "cascade" else 8192)
+    T, K, W = args.frames, args.steps, args.warmup
+    cascade = args.net == "cascade"
+    if cascade:
+        from nnsp_amd.engine import NNSPCascade
+
+        nets = {n: NNSPBatch(n, S, T, acc32=args.acc32) for n in ("vad", "kws", "s2i")}
+        eng = NNSPCascade(nets)
+        if args.window >= 0:
+            eng.set_window(args.window)
+    else:
+        eng = NNSPBatch(args.net, S, T, acc32=args.acc32)
     # inputs resident in HBM before timing: one chunk buffer per step
     bufs = [torch.empty((S, T, 160), dtype=torch.int16, device="cuda") for _ in range(W + K)]
     for i, b in enumerate(bufs):
         _lib.check(_lib.lib().nnsp_synth_pcm(b.data_ptr(), S, T, 0x4E4E5350, rank * S, i * T, 4096,
                                              eng.stream), "synth_pcm")
     trig = torch.empty((S, T), dtype=torch.int16, device="cuda")
+    out3 = torch.empty((S, T, 3), dtype=torch.int16, device="cuda")
+
+    def step(buf):
+        if cascade:   # per frame: the NNSP_ID that ran, its trigger and outputs
+            eng.exec_device(buf.data_ptr(), T, None, trig.data_ptr(), out3.data_ptr())
+        else:
+            eng.exec_device(buf.data_ptr(), T, trig.data_ptr())
+
     eng.sync()
     torch.cuda.synchronize()
     for i in range(W):
-        eng.exec_device(bufs[i].data_ptr(), T, trig.data_ptr())
+        step(bufs[i])
     eng.sync()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    fe_ms = nn_ms = 0.0
+    kt = {}            # kernel -> total ms over the timed steps
+    kframes = {}       # kernel -> frames (fe) or NN frames it processed
+    rounds = 0
     t0 = time.perf_counter()
     for i in range(K):
-        eng.exec_device(bufs[W + i].data_ptr(), T, trig.data_ptr())
-        f, n = eng.last_timing()   # syncs the stream: per-step kernel times
-        fe_ms += f
-        nn_ms += n
+        step(bufs[W + i])
+        if cascade:
+            r, _, _ = eng.last_stats()
+            rounds += r
+            for n in ("vad", "kws", "s2i"):
+                f, fe, nn = eng.net_stats(n)
+                kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + fe
+                kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + f
+                kt[f"nn_{n}"] = kt.get(f"nn_{n}", 0.0) + nn
+                kframes[f"nn_{n}"] = kframes.get(f"nn_{n}", 0) + f
+        else:
+            f, n = eng.last_timing()   # syncs the stream: per-step kernel times
+            kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + f
+            kt[f"nn_{args.net}"] = kt.get(f"nn_{args.net}", 0.0) + n
+            kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
+            kframes[f"nn_{args.net}"] = kframes.get(f"nn_{args.net}", 0) + S * T
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -139,16 +184,20 @@ def main() -> None:
 
     if rank == 0:
         info = device_info()
-        # dominant kernel: the front end (VALU-bound integer work)
-        fe_avg_s = fe_ms / K / 1e3
-        nn_avg_s = nn_ms / K / 1e3
-        dom = "fe_kernel" if fe_avg_s >= nn_avg_s else "nn_kernel"
         cu, clk = info["compute_units"], info["clock_khz"] * 1e3
         valu_peak = cu * 128 * clk / 1e12          # int32 VALU lane-ops/s (4 SIMD32 per CU)
+        mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
+        dom = max(kt, key=kt.get)                  # dominant kernel by device time
+        dom_s = kt[dom] / 1e3
         if dom == "fe_kernel":
-            achieved = S * T * FE_MULS_PER_FRAME / fe_avg_s / 1e12
+            achieved = kframes[dom] * FE_MULS_PER_FRAME / dom_s / 1e12
+            work = "integer multiplies (SURVEY 8(d): 5912 per frame)"
+            peak, bound = valu_peak, "valu"
         else:
-            achieved = S * T / 2 * NN_MACS_PER_INFERENCE[args.net] * 2 / nn_avg_s / 1e12
+            n = dom[3:]
+            achieved = kframes[dom] / 2 * NN_MACS_PER_INFERENCE[n] * 2 / dom_s / 1e12
+            work = f"{n} int8xint16 MACs x2 ops (NN runs every 2nd frame)"
+            peak, bound = mfma_peak, "mfma"
         traffic = None
         try:
             with open(args.profile_json) as f:
@@ -157,6 +206,7 @@ def main() -> None:
                 traffic = pj.get("fe_kernel_hbm_bytes_per_launch")
         except Exception:
             pass
+        fe_s = kt["fe_kernel"] / 1e3
         out = {
             "metric": "audio frames/sec (16 kHz, 10 ms hop) per node; bit-exact vs ref",
             "value": value,
@@ -173,17 +223,20 @@ def main() -> None:
             "config": {"workload": WORKLOADS[args.net], "net": args.net, "streams_per_gpu": S,
                        "frames_per_step": T, "accumulator": "32b" if args.acc32 else "64b",
                        "parallelism": f"stream shards x{world}"},
-            "kernels_ms_per_step": {"fe_kernel": fe_ms / K, "nn_kernel": nn_ms / K},
-            "roofline": {"kernel": dom, "bound": "valu",
-                         "achieved": achieved, "peak": valu_peak, "unit": "Tops/s",
-                         "frac": achieved / valu_peak,
-                         "work": ("integer multiplies (SURVEY 8(d): 5912 per frame)" if dom == "fe_kernel"
-                                  else "int8xint16 MAC x2 ops"),
+            "kernels_ms_per_step": {k: v / K for k, v in kt.items()},
+            "frames_scheduled_per_step": {k: v // K for k, v in kframes.items()},
+            "roofline": {"kernel": dom, "bound": bound,
+                         "achieved": achieved, "peak": peak, "unit": "Tops/s",
+                         "frac": achieved / peak, "work": work,
                          "traffic": traffic,
-                         "hbm_achieved_GBps": S * T * FE_HBM_BYTES_PER_FRAME / fe_avg_s / 1e9,
+                         "hbm_achieved_GBps": kframes["fe_kernel"] * FE_HBM_BYTES_PER_FRAME / fe_s / 1e9,
                          "hbm_peak_GBps": 8000.0},
             "device": info,
         }
+        if cascade:
+            out["cascade"] = {"rounds_per_step": rounds / K,
+                              "speculation_overhead": sum(kframes[f"nn_{n}"] for n in ("vad", "kws", "s2i"))
+                              / (S * T * K) - 1.0}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.net, args.acc32, args.cpu_seconds)
         print(json.dumps(out))

@@ -1,0 +1,88 @@
+/*
+ * nnsp_cascade.h -- batched VAD -> KWS -> S2I cascade on MI355X
+ * (libnnsp_mi355x.so).
+ *
+ * The batched counterpart of the reference's nnCntrlClass
+ * (evb/src/nnCntrlClass.h:35-58, nnCntrlClass.c:57-272): per stream, every
+ * 10 ms frame goes to the net at the stream's current sequence position; a
+ * VAD detection moves on to the next position; KWS moves forward on a
+ * detection and back on its timeout; S2I moves on after a detection or its
+ * timeout.  The departing net is reset (NNSPClass_reset) on each move.  KWS and
+ * S2I read the PCM frame that lies frs_vbufBk frames in the past (PcmBufClass,
+ * 100-frame voice buffer).
+ *
+ * A cascade drives three nnsp_batch objects of the same stream count, indexed
+ * by NNSP_ID (s2i_id = 0, vad_id = 1, kws_galaxy_id = 2,
+ * nnsp_identification.h).  Their thresholds come from the batches
+ * (nnsp_batch_create).  Per stream and frame, the net that ran, the trigger it
+ * returned and NNSPClass.outputs are bit-identical to calling the reference's
+ * nnCntrlClass_exec on that stream's frames in order.
+ */
+#ifndef NNSP_CASCADE_H
+#define NNSP_CASCADE_H
+#include <stdint.h>
+
+#include "nnsp_batch.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct nnsp_cascade nnsp_cascade;
+
+/* The ParamCntrlClass fields (nnCntrlClass.h:12-31) that the nets do not
+ * already carry: look-back frames and timeouts of S2I and KWS. */
+typedef struct {
+    int16_t frs_vbufBk_s2i;      /* 0..99 */
+    int16_t thresh_timeout_s2i;  /* >= 1 */
+    int16_t frs_vbufBk_kws;      /* 0..99 */
+    int16_t thresh_timeout_kws;  /* >= 1 */
+} nnsp_cascade_params;
+
+/* nnCntrlClass_init: nets[NNSP_ID] (all with the same n_streams and a
+ * max_frames the chunks will not exceed), seq = NNSP_ID per sequence position
+ * (pt_seq_cntrl, len 1..8).  Every stream starts at position 0 with all nets
+ * reset.  The nets stay owned by the caller and must outlive the cascade. */
+int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq,
+                        int len_seq, const nnsp_cascade_params *params);
+void nnsp_cascade_destroy(nnsp_cascade *c);
+
+/* nnCntrlClass_reset on the streams with mask[s] != 0 (NULL: all): timeout
+ * counters, all three nets and the PCM history; the position is kept. */
+int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask);
+
+/* One chunk of T frames: pcm [S][T][160] int16.  Outputs per frame (NULL
+ * skips): net_ran [S][T] int8 = NNSP_ID that ran, detected [S][T] int16 = its
+ * NNSPClass_exec return, outputs3 [S][T][3] int16 = its NNSPClass.outputs.
+ * _device: device pointers, asynchronous on nnsp_cascade_stream (it blocks on
+ * the host only for the per-round list lengths). */
+int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
+                      int16_t *detected, int16_t *outputs3);
+int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
+                             int16_t *detected, int16_t *outputs3);
+int nnsp_cascade_sync(nnsp_cascade *c);
+
+/* Scheduling knob (results do not depend on it): each round runs every
+ * listed stream for at most this many frames (0: to the chunk end).  Smaller
+ * windows waste less work past a net switch but take more rounds.  Default 12
+ * (environment NNSP_CASCADE_WINDOW overrides it at create time). */
+int nnsp_cascade_set_window(nnsp_cascade *c, int frames);
+void *nnsp_cascade_stream(nnsp_cascade *c);
+
+/* Last chunk: rounds run, frames scheduled on the nets (>= S*T; the excess is
+ * work past a switch that the switch discarded), device time in ms. */
+int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run, float *ms);
+
+/* Last chunk, one net (NNSP_ID): frames scheduled on it, and the device time
+ * of its front-end kernel and of its NN kernels (proj + recur), summed over
+ * the rounds. */
+int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms,
+                                float *nn_ms);
+
+/* current_pos_seq of every stream -> host int8 [S]. */
+int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

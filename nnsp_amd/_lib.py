@@ -70,6 +70,12 @@ class NNSPClass(C.Structure):
                 ("num_dnsmpl", C.c_int16), ("outputs", C.c_int16 * 3), ("argmax_last", C.c_int16)]
 
 
+class CascadeParams(C.Structure):
+    """nnsp_cascade_params (include/nnsp_cascade.h), ParamCntrlClass subset."""
+    _fields_ = [("frs_vbufBk_s2i", C.c_int16), ("thresh_timeout_s2i", C.c_int16),
+                ("frs_vbufBk_kws", C.c_int16), ("thresh_timeout_kws", C.c_int16)]
+
+
 class PostState(C.Structure):
     _fields_ = [("slides", C.c_int16), ("trigger", C.c_int16), ("argmax_last", C.c_int16),
                 ("pad0", C.c_int16), ("counts_category", C.c_int16 * 8),
@@ -97,6 +103,18 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_batch_state_bytes": (C.c_size_t, [P]),
         "nnsp_batch_get_state": (I, [P, P, I, I]),
         "nnsp_batch_set_state": (I, [P, P, I, I]),
+        "nnsp_cascade_create": (I, [C.POINTER(P), P, P, I, P]),
+        "nnsp_cascade_destroy": (None, [P]),
+        "nnsp_cascade_reset": (I, [P, P]),
+        "nnsp_cascade_exec": (I, [P, P, I, P, P, P]),
+        "nnsp_cascade_exec_device": (I, [P, P, I, P, P, P]),
+        "nnsp_cascade_sync": (I, [P]),
+        "nnsp_cascade_set_window": (I, [P, I]),
+        "nnsp_cascade_stream": (P, [P]),
+        "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
+        "nnsp_cascade_positions": (I, [P, P]),
+        "nnsp_cascade_last_net_stats": (I, [P, I, C.POINTER(C.c_longlong), C.POINTER(C.c_float),
+                                            C.POINTER(C.c_float)]),
         "nnsp_synth_pcm": (I, [P, I, I, C.c_uint64, I, C.c_int64, I, P]),
         "nnsp_device_count": (I, [C.POINTER(I)]),
         "nnsp_set_device": (I, [I]),

@@ -13,26 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include "../../../include/nnsp_batch.h"
 #include "nnsp_host.h"
-
-struct nnsp_batch {
-    int S, Tmax, nout, out_linear, norm_shift;
-    nnsp_image im;
-    void *stream;
-    void *ev[3];
-    int32_t *d_mean, *d_stdR;
-    int16_t *d_tail, *d_prev5, *d_h;
-    int32_t *d_c;
-    NnPost *d_post;
-    int16_t *d_feats, *d_pcm, *d_trig;
-    int32_t *d_logits;
-    uint8_t *d_mask;
-    int last_T;
-    /* split NN path (one LSTM layer) */
-    int fast, li, nstep_max, rec_waves, proj_blocks;
-    int32_t *d_gx;
-};
 
 #define LDS_MAX (160 * 1024)
 
@@ -179,12 +160,16 @@ static int ensure(void **p, size_t bytes)
     return nnspk_malloc(p, bytes);
 }
 
-int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits)
+int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
+                   const nnsp_segment *seg, void *stream, int timed)
 {
-    if (!b || !pcm || T <= 0 || T > b->Tmax) {
-        nnsp_set_error("nnsp_batch_exec: T must be in 1..%d", b ? b->Tmax : 0);
-        return NNSP_EINVAL;
+    static const nnsp_segment whole = {0};
+    if (!seg) seg = &whole;
+    if (seg->list && !b->fast) {
+        nnsp_set_error("stream segments need the split NN path (one LSTM layer)");
+        return NNSP_EUNSUPPORTED;
     }
+    if (seg->list && seg->n_list <= 0) return 0;
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
     fa.pcm = pcm;
@@ -195,9 +180,16 @@ int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *tr
     fa.stdR = b->d_stdR;
     fa.norm_shift = b->norm_shift;
     fa.feats = b->d_feats;
-    TRY(nnspk_event_record(b->ev[0], b->stream));
-    TRY(nnspk_launch_fe(&fa, b->stream));
-    TRY(nnspk_event_record(b->ev[1], b->stream));
+    fa.list = seg->list;
+    fa.n_list = seg->n_list;
+    fa.seg_begin = seg->seg_begin;
+    fa.lookback = seg->lookback;
+    fa.hist = seg->hist;
+    fa.hist_frames = seg->hist_frames;
+    fa.seg_len = seg->seg_len;
+    if (timed) TRY(nnspk_event_record(b->ev[0], stream));
+    TRY(nnspk_launch_fe(&fa, stream));
+    if (timed) TRY(nnspk_event_record(b->ev[1], stream));
     if (b->fast) {
         FastRun f;
         memset(&f, 0, sizeof f);
@@ -213,13 +205,25 @@ int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *tr
         f.c = b->d_c;
         f.trig = trig;
         f.logits = logits;
+        f.out3 = seg->out3;
+        f.list = seg->list;
+        f.n_list = seg->n_list;
+        f.seg_begin = seg->seg_begin;
+        f.seg_len = seg->seg_len;
         const NnLayer *LL = &b->im.img.L[b->li];
         f.a_off = 0;
         f.a_lds_bytes = (int)LL->ar_off;
-        TRY(nnspk_launch_proj(&b->im.img, &f, b->proj_blocks, b->stream));
+        int blocks = b->proj_blocks;
+        if (seg->list) {   /* size the grid to the listed streams */
+            const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
+            const long long pt = (long long)seg->n_list * ((W / 2 + 1 + 15) / 16);
+            const long long need = (pt + 3) / 4;
+            if (need < blocks) blocks = (int)need;
+        }
+        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, stream));
         f.a_off = LL->ar_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
-        TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, b->stream));
+        TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, stream));
     } else {
         NnRun r;
         memset(&r, 0, sizeof r);
@@ -234,12 +238,24 @@ int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *tr
         r.post = b->d_post;
         r.trig = trig;
         r.logits = logits;
-        TRY(nnspk_launch_nn(&b->im.img, &r, b->stream));
+        TRY(nnspk_launch_nn(&b->im.img, &r, stream));
     }
-    TRY(nnspk_event_record(b->ev[2], b->stream));
+    if (timed) TRY(nnspk_event_record(b->ev[2], stream));
     /* carry the context (slots 1..5) and the PCM tail (last 320 samples) */
-    TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, b->stream));
-    TRY(nnspk_launch_tail_roll(b->d_tail, pcm, b->S, T, b->stream));
+    TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, seg->list, seg->n_list, seg->seg_begin,
+                              seg->seg_len, stream));
+    TRY(nnspk_launch_tail_roll(b->d_tail, pcm, b->S, T, seg->list, seg->n_list, seg->seg_begin, seg->seg_len,
+                               seg->lookback, seg->hist, seg->hist_frames, stream));
+    return 0;
+}
+
+int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits)
+{
+    if (!b || !pcm || T <= 0 || T > b->Tmax) {
+        nnsp_set_error("nnsp_batch_exec: T must be in 1..%d", b ? b->Tmax : 0);
+        return NNSP_EINVAL;
+    }
+    TRY(nnsp_batch_run(b, pcm, T, trig, logits, NULL, b->stream, 1));
     b->last_T = T;
     return 0;
 }

@@ -6,6 +6,7 @@
 
 #include "../../../include/nnsp_api.h"
 #include "../kernels/nnsp_kabi.h"
+#include "../../../include/nnsp_batch.h"
 
 /* error codes (negative: argument/validation; positive: HIP runtime) */
 #define NNSP_EINVAL (-1)
@@ -41,6 +42,40 @@ void nnsp_image_free(nnsp_image *im);
 
 /* activation function pointer -> device enum (-1 unknown) */
 int nnsp_act_of(void *(*fn)(void *, int32_t *, int));
+
+/* the batch engine's internals, shared with the cascade (nnsp_cascade.c) */
+struct nnsp_batch {
+    int S, Tmax, nout, out_linear, norm_shift;
+    nnsp_image im;
+    void *stream;
+    void *ev[3];
+    int32_t *d_mean, *d_stdR;
+    int16_t *d_tail, *d_prev5, *d_h;
+    int32_t *d_c;
+    NnPost *d_post;
+    int16_t *d_feats, *d_pcm, *d_trig;
+    int32_t *d_logits;
+    uint8_t *d_mask;
+    int last_T;
+    /* split NN path (one LSTM layer) */
+    int fast, li, nstep_max, rec_waves, proj_blocks;
+    int32_t *d_gx;
+};
+
+/* One segment launch of a batch: the streams list[0..n_list) (NULL: all),
+ * frames seg_begin[s]..T-1 (NULL: 0), input frame t = chunk frame t - lookback
+ * (earlier frames from hist [S][hist_frames][160]); out3 [S][T][3] optional. */
+typedef struct {
+    const int32_t *list;
+    const int32_t *seg_begin;
+    const int16_t *hist;
+    int16_t *out3;
+    int n_list, lookback, hist_frames;
+    int seg_len;              /* > 0: segments end at min(T, seg_begin + seg_len) */
+} nnsp_segment;
+
+int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
+                   const nnsp_segment *seg, void *stream, int timed);
 
 void nnsp_set_error(const char *fmt, ...);
 const char *nnsp_last_error(void);

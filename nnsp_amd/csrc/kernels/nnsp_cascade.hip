@@ -1,0 +1,206 @@
+// nnsp_cascade.hip -- control kernels of the batched VAD -> KWS -> S2I cascade
+// (nnCntrlClass_exec, reference evb/src/nnCntrlClass.c:152-272).
+//
+// A chunk of T frames runs in rounds.  In a round every still-running stream
+// executes ONE net (the one at its current sequence position) speculatively
+// from its segment start to the end of the chunk (proj/recur/fe kernels with a
+// stream list).  casc_control_kernel then replays the controller's per-frame
+// logic over that segment's triggers: timeout counters, detection, the next
+// sequence position and the NNSPClass_reset of the departing net.  At the first
+// frame that moves the stream to a different net state, the segment is cut:
+// the departing net is reset (its normFeatContext slot 5 keeps the feature of
+// that frame -- FeatureClass_setDefault leaves slot 5 alone, trap T4) and the
+// stream is listed for the next round from the following frame.  Everything
+// the departing net computed past the cut is discarded by the reset.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nnsp_kabi.h"
+
+namespace {
+
+inline int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
+
+// Append s to list[n] for every lane with want; one atomic per wave and net.
+__device__ __forceinline__ void list_push(const CascArgs& a, int n, int s, bool want) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool mine = want && n == k;
+        const unsigned long long m = __ballot(mine);
+        if (!m) continue;
+        const int leader = __ffsll((long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&a.counts[k], __popcll(m));
+        base = __shfl(base, leader);
+        if (mine) a.list[k][base + __popcll(m & ((1ull << lane) - 1ull))] = s;
+    }
+}
+
+__device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned long long v) {
+    // per net: wave-reduce, one atomic per wave
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long x = n == k ? v : 0ull;
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        if ((threadIdx.x & 63) == 0 && x && a.frames) atomicAdd(&a.frames[k], x);
+    }
+}
+
+__global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool ok_s = s < a.S;
+    int n = 0;
+    if (ok_s) {
+        a.seg_begin[s] = 0;
+        n = a.seq[a.st[s].pos];
+    }
+    list_push(a, n, s, ok_s);
+    add_frames(a, n, ok_s ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, a.T) : a.T) : 0ull);
+}
+
+__global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int T = a.T;
+    bool want = false;
+    int n_next = 0, b_next = T;
+    if (s < a.S && a.seg_begin[s] < T) {
+        const int b = a.seg_begin[s];
+        const int e = a.seg_len > 0 ? min(T, b + a.seg_len) : T;   // this round's segment b..e-1
+        CascState st = a.st[s];
+        const int n = a.seq[st.pos];   // the net that ran this round (fixed over the segment)
+        const int16_t* tr = a.trig[n] + (size_t)s * T;
+        int cut = -1;
+        b_next = e;   // no switch: carry on in the same net next round (if e < T)
+        for (int t = b; t < e; ++t) {
+            const int16_t det = tr[t];
+            const size_t f = (size_t)s * T + t;
+            if (a.net_ran) a.net_ran[f] = (int8_t)n;
+            if (a.detected) a.detected[f] = det;
+            if (a.outputs3) {
+                const int16_t* o = a.out3[n] + f * 3;
+                a.outputs3[f * 3 + 0] = o[0];
+                a.outputs3[f * 3 + 1] = o[1];
+                a.outputs3[f * 3 + 2] = o[2];
+            }
+            bool move = false, rst = false;
+            int np = st.pos;
+            if (n == 0) {   // s2i (nnCntrlClass.c:173-200)
+                st.cnt_s2i = (uint16_t)((st.cnt_s2i + 1) % a.timeout_s2i);
+                if (det || st.cnt_s2i == a.timeout_s2i - 1) {
+                    np = (st.pos + 1) % a.len_seq;
+                    move = true;
+                    if (det || n != a.seq[np]) {
+                        st.cnt_s2i = 0;
+                        rst = true;
+                    }
+                }
+            } else if (n == 2) {   // kws (nnCntrlClass.c:203-236)
+                st.cnt_kws = (uint16_t)((st.cnt_kws + 1) % a.timeout_kws);
+                if (det || st.cnt_kws == a.timeout_kws - 1) {
+                    np = det ? (st.pos + 1) % a.len_seq : (st.pos - 1) % a.len_seq;
+                    if (np < 0) np += a.len_seq;
+                    move = true;
+                    if (det || n != a.seq[np]) {
+                        st.cnt_kws = 0;
+                        rst = true;
+                    }
+                }
+            } else if (det) {   // vad (nnCntrlClass.c:238-262)
+                np = (st.pos + 1) % a.len_seq;
+                move = rst = true;
+            }
+            if (move) st.pos = (int16_t)np;   // no reset: same net, same state, keep going
+            if (rst) {
+                cut = t;
+                break;
+            }
+        }
+        if (cut >= 0) {
+            // NNSPClass_reset of the departing net; slot 5 = this frame's feature (T4)
+            a.reset_mask[n][s] = 1;
+            const int4* src = reinterpret_cast<const int4*>(a.feats[n] + ((size_t)s * T + cut) * 40);
+            int4* dst = reinterpret_cast<int4*>(a.prev5[n] + ((size_t)s * 5 + 4) * 40);
+#pragma unroll
+            for (int k = 0; k < 5; ++k) dst[k] = src[k];
+            b_next = cut + 1;
+        }
+        a.st[s] = st;
+        a.seg_begin[s] = b_next;
+        if (b_next < T) {
+            want = true;
+            n_next = a.seq[st.pos];
+        }
+    }
+    list_push(a, n_next, s, want);
+    add_frames(a, n_next,
+               want ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, T - b_next) : T - b_next) : 0ull);
+}
+
+// nnCntrlClass_reset's controller part + PcmBufClass_reset (nnCntrlClass.c:132-150,
+// PcmBufClass.c:19-28): timeout counters and the PCM history; the sequence
+// position is kept, as the reference does.
+__global__ __launch_bounds__(256) void casc_reset_kernel(CascState* st, int16_t* hist, int H, const uint8_t* mask,
+                                                        int S) {
+    const int s = blockIdx.x;
+    if (s >= S || (mask && !mask[s])) return;
+    if (threadIdx.x == 0) {
+        st[s].cnt_kws = 0;
+        st[s].cnt_s2i = 0;
+    }
+    int4* h = reinterpret_cast<int4*>(hist + (size_t)s * H * 160);
+    for (int i = threadIdx.x; i < H * 20; i += blockDim.x) h[i] = make_int4(0, 0, 0, 0);
+}
+
+// dst := last H frames of (src ++ pcm chunk), per stream (int4 = 8 samples).
+__global__ __launch_bounds__(256) void hist_roll_kernel(int16_t* dst, const int16_t* src, const int16_t* pcm, int S,
+                                                       int T, int H) {
+    const long long n = (long long)S * H * 20;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (long long)gridDim.x * blockDim.x) {
+        const int s = (int)(i / (H * 20));
+        const int r = (int)(i - (long long)s * H * 20);
+        const int k = r / 20, c = r % 20;   // history frame k, chunk c
+        const int j = T + k;                // index into src(H) ++ pcm(T)
+        const int4* p = j < H ? reinterpret_cast<const int4*>(src + ((size_t)s * H + j) * 160) + c
+                              : reinterpret_cast<const int4*>(pcm + ((size_t)s * T + j - H) * 160) + c;
+        reinterpret_cast<int4*>(dst + ((size_t)s * H + k) * 160)[c] = *p;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int nnspk_launch_casc_begin(const CascArgs* a, void* stream) {
+    if (a->S <= 0) return 0;
+    hipLaunchKernelGGL(casc_begin_kernel, dim3((a->S + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_casc_control(const CascArgs* a, void* stream) {
+    if (a->S <= 0) return 0;
+    hipLaunchKernelGGL(casc_control_kernel, dim3((a->S + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_casc_reset(CascState* st, int16_t* hist, int hist_frames, const uint8_t* mask, int S,
+                            void* stream) {
+    if (S <= 0) return 0;
+    hipLaunchKernelGGL(casc_reset_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, st, hist, hist_frames, mask,
+                       S);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_hist_roll(int16_t* dst, const int16_t* src, const int16_t* pcm, int S, int T, int hist_frames,
+                           void* stream) {
+    if (S <= 0 || hist_frames <= 0) return 0;
+    const long long n = (long long)S * hist_frames * 20;
+    long long blocks = (n + 255) / 256;
+    if (blocks > 256 * 32) blocks = 256 * 32;
+    hipLaunchKernelGGL(hist_roll_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, dst, src, pcm,
+                       S, T, hist_frames);
+    return ok(hipGetLastError());
+}
+
+}  // extern "C"

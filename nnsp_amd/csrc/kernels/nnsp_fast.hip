@@ -86,22 +86,28 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     ProjWave& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
     const NnLayer& LL = img.L[r.li];
-    const int ntps = (r.nstep_max + 15) / 16;
-    const long long ntiles = (long long)r.S * ntps;
+    const int wsteps = r.seg_len > 0 ? min(r.nstep_max, (r.seg_len + 1) / 2) : r.nstep_max;
+    const int ntps = (wsteps + 15) / 16;
+    const int nrow = r.list ? r.n_list : r.S;
+    const long long ntiles = (long long)nrow * ntps;
     const int rows = LL.rows;
     for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
          tile += (long long)gridDim.x * (blockDim.x >> 6)) {
-        const int s = (int)(tile / ntps), j0 = 16 * (int)(tile - (long long)s * ntps);
+        const int i_row = (int)(tile / ntps), j0 = 16 * (int)(tile - (long long)i_row * ntps);
+        const int s = r.list ? r.list[i_row] : i_row;
+        const int b = r.seg_begin ? r.seg_begin[s] : 0;   // segment: frames b..e-1
+        const int L = (r.seg_len > 0 ? min(r.T, b + r.seg_len) : r.T) - b;
         const int phase = 1 - reinterpret_cast<const NnPost*>(r.post)[s].slides;
-        const int t0 = 2 * j0 + phase;            // NN frame of row 0
-        // ---- union of the 16 context windows: V[t0 .. t0+35], V = prev5 ++ feats
+        const int t0 = 2 * j0 + phase;            // segment-relative NN frame of row 0
+        if (t0 >= L) continue;                    // wave-uniform
+        // ---- union of the 16 context windows: V[t0 .. t0+35], V = prev5 ++ feats[b..T)
         for (int c = lane; c < 180; c += 64) {
             const int fr = c / 5, part = c - 5 * fr, idx = t0 + fr;
             int4 v = make_int4(0, 0, 0, 0);
             if (idx < 5)
                 v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part);
-            else if (idx - 5 < r.T)
-                v = *reinterpret_cast<const int4*>(r.feats + ((size_t)s * r.T + idx - 5) * 40 + 8 * part);
+            else if (idx - 5 < L)
+                v = *reinterpret_cast<const int4*>(r.feats + ((size_t)s * r.T + b + idx - 5) * 40 + 8 * part);
             *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
         }
         wave_lds_sync();
@@ -122,7 +128,7 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
             load_b<4>(in, in_stride, LL.nkt, lane, bh, bl);
             const uint8_t* A = W + (LL.a_off - r.a_off);
             const int j = j0 + sc;
-            const bool act = j < r.nstep_max && 2 * j + phase < r.T;
+            const bool act = j < r.nstep_max && 2 * j + phase < L;
             int32_t* dst = r.gx + ((size_t)s * r.nstep_max + j) * rows + 4 * q;
             for (int rt = 0; rt < LL.nrt; ++rt) {
                 v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
@@ -156,7 +162,9 @@ struct RecTile {
     int16_t act[2][16][R_STRIDE];   // FC activations, ping-pong across layers
     int32_t c[16][R_CW];
     int32_t phase[16];
-    int32_t pad[16];
+    int32_t nst[16];    // NN steps of each stream's segment
+    int32_t beg[16];    // segment start frame
+    int32_t end[16];    // segment end frame (exclusive)
 };
 
 template <int RPW>   // LSTM row tiles per wave = ceil(nrt / RG)
@@ -172,31 +180,49 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     const int tl = wv / RG, g = wv - tl * RG;   // tile in workgroup, wave in tile
     RecTile& R = tiles[tl];
     const int sc = lane & 15, q = lane >> 4;
-    const int s0 = (blockIdx.x * tpw + tl) * 16;
-    const int s = s0 + sc;
-    const bool valid = s < r.S;
+    // tile = 16 consecutive entries of the stream list (identity when list == NULL)
+    const int nrow = r.list ? r.n_list : r.S;
+    const int i0 = (blockIdx.x * tpw + tl) * 16;
+    auto sid = [&](int i) { return r.list ? r.list[i] : i; };
+    const bool valid = i0 + sc < nrow;
+    const int s = valid ? sid(i0 + sc) : 0;
     const NnLayer& LL = img.L[r.li];
     const int N = LL.N, rows = LL.rows, nrt = LL.nrt;
     for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
-        const int st = idx / N, u = idx - st * N, gs = s0 + st;
-        const bool ok = gs < r.S;
+        const int st = idx / N, u = idx - st * N;
+        const bool ok = i0 + st < nrow;
+        const int gs = ok ? sid(i0 + st) : 0;
         R.h[0][st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
         R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
     }
+    const int T = r.T;
     PostState ps = {};
     if (g == 0 && lane < 16) {
+        const int b = valid && r.seg_begin ? r.seg_begin[s] : 0;
+        const int e = r.seg_len > 0 ? min(T, b + r.seg_len) : T;
         if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
-        R.phase[lane] = valid ? 1 - ps.slides : 0;
+        const int ph = valid ? 1 - ps.slides : 0;
+        R.phase[lane] = ph;
+        R.beg[lane] = b;
+        R.end[lane] = e;
+        R.nst[lane] = valid && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
     }
     __syncthreads();
     const int phase = R.phase[sc];
-    const int T = r.T;
-    const int nsteps = (T + 1) / 2;
-    if (g == 0 && lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
+    const int b = R.beg[sc];
+    const int e = R.end[sc];   // segment: frames b..e-1
+    int nsteps = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
+    if (g == 0 && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
+        if (r.trig) r.trig[(size_t)s * T + b] = ps.trigger;
+        if (r.out3)
+            for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
+    }
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
     v4i gxv[RPW];
     auto load_gx = [&](int jj) {
-        const bool ok = valid && 2 * jj + phase < T;
+        const bool ok = valid && b + 2 * jj + phase < e;
         const int32_t* gsrc = r.gx + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * rows + 4 * q;
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {
@@ -207,8 +233,8 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     load_gx(0);
     int hb = 0;
     for (int j = 0; j < nsteps; ++j) {
-        const int t = 2 * j + phase;
-        const bool active = valid && t < T;
+        const int t = b + 2 * j + phase;
+        const bool active = valid && t < e;
         v4i bh[2], bl[2];
         load_b<2>(&R.h[hb][0][0], R_STRIDE, LL.nkt_r, lane, bh, bl);
         // ---- LSTM (lstm.c:48-124): row tile = 4 units x gates i, j, f, o
@@ -301,22 +327,26 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
                 post_proc(ps, img, lg);
                 if (r.trig) {
                     r.trig[(size_t)s * T + t] = ps.trigger;
-                    if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+                    if (t + 1 < e) r.trig[(size_t)s * T + t + 1] = ps.trigger;
                 }
+                if (r.out3)
+                    for (int f = t; f < min(t + 2, e); ++f)
+                        for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + f) * 3 + o] = ps.outputs[o];
             }
         }
         __syncthreads();
     }
     // ---- state out
     for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
-        const int st = idx / N, u = idx - st * N, gs = s0 + st;
-        if (gs < r.S) {
+        const int st = idx / N, u = idx - st * N;
+        if (i0 + st < nrow) {
+            const int gs = sid(i0 + st);
             r.h[(size_t)gs * NN_MAX_W + u] = R.h[hb][st][u];
             r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
         }
     }
-    if (g == 0 && lane < 16 && valid) {
-        ps.slides = (int16_t)(ps.slides ^ (T & 1));
+    if (g == 0 && lane < 16 && valid && b < e) {
+        ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
 }
@@ -338,7 +368,9 @@ int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* st
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw);
-    const int tiles = (r->S + 15) / 16;
+    const int nrow = r->list ? r->n_list : r->S;
+    if (nrow <= 0) return 0;
+    const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
     const int rpw = (img->L[r->li].nrt + RG - 1) / RG;
     const dim3 grid(blocks), blk(64 * RG * tpw);

@@ -28,6 +28,15 @@ typedef struct {
     int16_t *feats;      /* [S][T][40] normalised log-Mel (context slot 5) */
     int32_t *dbg_spec;   /* optional [S*T][1024] rfft output */
     int32_t *dbg_log;    /* optional [S*T][40] log10 Mel (FeatureClass.feature) */
+    /* segments (cascade): run only the streams list[0..n_list) (NULL: all S),
+     * frames seg_begin[s]..T-1 (NULL: 0), input frame t read from chunk frame
+     * t - lookback (negative: hist [S][H][160] frame H + t - lookback, H =
+     * hist_frames >= lookback) */
+    const int32_t *list;
+    const int32_t *seg_begin;
+    const int16_t *hist;
+    int32_t n_list, lookback, hist_frames;
+    int32_t seg_len;          /* > 0: a segment ends at min(T, seg_begin + seg_len) */
 } FeArgs;
 
 typedef struct {
@@ -78,6 +87,10 @@ typedef struct {
     int32_t *c;               /* [S][NN_MAX_W] */
     int16_t *trig;            /* [S][T] */
     int32_t *logits;          /* [S][T][nout] or NULL */
+    int16_t *out3;            /* [S][T][3] NNSPClass.outputs after each frame, or NULL */
+    const int32_t *list;      /* segments, as FeArgs */
+    const int32_t *seg_begin;
+    int32_t n_list, seg_len;  /* seg_len as FeArgs */
 } FastRun;
 
 /* 32-byte device post-processing state, one per stream */
@@ -90,8 +103,11 @@ typedef struct {
 /* launch layer (nnsp_kernels.hip) */
 int nnspk_launch_fe(const FeArgs *a, void *stream);
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
-int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, void *stream);
-int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, void *stream);
+int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
+                          int n_list, const int32_t *seg_begin, int seg_len, void *stream);
+int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, const int32_t *list,
+                           int n_list, const int32_t *seg_begin, int seg_len, int lookback,
+                           const int16_t *hist, int hist_frames, void *stream);
 int nnspk_launch_synth_pcm(int16_t *out, int S, int T, unsigned long long seed, int s0,
                            long long t0, int amp, void *stream);
 int nnspk_launch_rfft(int32_t *x, int32_t *y, int n, void *stream);
@@ -129,6 +145,41 @@ int nnspk_event_destroy(void *e);
 int nnspk_event_record(void *e, void *stream);
 int nnspk_event_elapsed(float *ms, void *a, void *b);
 int nnspk_device_info(int *cus, int *clock_khz, char *name, int name_len);
+
+
+/* ---- VAD -> KWS -> S2I cascade (nnCntrlClass, evb/src/nnCntrlClass.c:152-272) ---- */
+typedef struct {
+    int16_t pos;              /* current_pos_seq */
+    uint16_t cnt_kws;         /* cnt_timeout_kws */
+    uint16_t cnt_s2i;         /* cnt_timeout_s2i */
+    int16_t pad;
+} CascState;
+
+typedef struct {
+    int32_t S, T, len_seq, timeout_kws, timeout_s2i;
+    int32_t seg_len;          /* frames per round and stream (0: to the chunk end) */
+    int16_t seq[8];           /* net id per sequence position (0 s2i, 1 vad, 2 kws) */
+    CascState *st;            /* [S] */
+    int32_t *seg_begin;       /* [S] first frame of this round's segment (T: done) */
+    const int16_t *trig[3];   /* per net id: [S][T] triggers of the round's segments */
+    const int16_t *out3[3];   /* per net id: [S][T][3] NNSPClass.outputs after each frame */
+    const int16_t *feats[3];  /* per net id: [S][T][40] */
+    int16_t *prev5[3];        /* per net id: [S][5][40] */
+    uint8_t *reset_mask[3];   /* per net id: [S] NNSPClass_reset requests */
+    int32_t *list[3];         /* per net id: next round's streams */
+    int32_t *counts;          /* [3] next round's list lengths */
+    unsigned long long *frames; /* [3] frames scheduled per net id (speculation included) */
+    int8_t *net_ran;          /* [S][T] or NULL */
+    int16_t *detected;        /* [S][T] or NULL */
+    int16_t *outputs3;        /* [S][T][3] or NULL */
+} CascArgs;
+
+int nnspk_launch_casc_begin(const CascArgs *a, void *stream);
+int nnspk_launch_casc_control(const CascArgs *a, void *stream);
+int nnspk_launch_casc_reset(CascState *st, int16_t *hist, int hist_frames, const uint8_t *mask, int S,
+                            void *stream);
+int nnspk_launch_hist_roll(int16_t *dst, const int16_t *src, const int16_t *pcm, int S, int T,
+                           int hist_frames, void *stream);
 
 #ifdef __cplusplus
 }

@@ -189,21 +189,45 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
-    const unsigned nfr = (unsigned)a.S * (unsigned)a.T;   // host guarantees < 2^31
+    const unsigned nrow = a.list ? (unsigned)a.n_list : (unsigned)a.S;
+    const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    const unsigned nfr = nrow * W;   // host guarantees < 2^31
     const unsigned stride = gridDim.x * 4u;
-    // 16-byte chunk 'lane' (< 60) of frame f's 480-sample window: frames t-2..t
-    auto window_src = [&](unsigned f) -> const int4* {
-        const int s = (int)(f / (unsigned)a.T), t = (int)(f - (unsigned)s * (unsigned)a.T);
+    // frame f = (row, k): stream s, segment start b, t = b + k (valid below T);
+    // lane (< 60) loads 16-byte chunk 'lane' of the 480-sample window (input
+    // frames t-2..t; before b: the tail)
+    auto frame_of = [&](unsigned f, int& s, int& t, int& b) {
+        const unsigned i = f / W;
+        s = a.list ? a.list[i] : (int)i;
+        b = a.seg_begin ? a.seg_begin[s] : 0;
+        t = b + (int)(f - i * W);
+        if (t >= a.T) b = t + 1;   // past the chunk: skip
+    };
+    auto window_src = [&](int s, int t, int b) -> const int4* {
         const int fi = t - 2 + lane / 20, off = (lane % 20) * 8;
-        return reinterpret_cast<const int4*>(fi >= 0 ? a.pcm + ((size_t)s * a.T + fi) * 160 + off
-                                                     : a.tail + (size_t)s * 320 + (fi + 2) * 160 + off);
+        if (fi < b) return reinterpret_cast<const int4*>(a.tail + (size_t)s * 320 + (fi - b + 2) * 160 + off);
+        const int x = fi - a.lookback;
+        return reinterpret_cast<const int4*>(x >= 0 ? a.pcm + ((size_t)s * a.T + x) * 160 + off
+                                                    : a.hist + ((size_t)s * a.hist_frames + a.hist_frames + x) * 160 + off);
     };
     unsigned f = blockIdx.x * 4u + wv;
     int4 nxt = make_int4(0, 0, 0, 0);
-    if (f < nfr && lane < 60) nxt = *window_src(f);
+    if (f < nfr && lane < 60) {
+        int s0, t0, b0;
+        frame_of(f, s0, t0, b0);
+        if (t0 >= b0) nxt = *window_src(s0, t0, b0);
+    }
     for (; f < nfr; f += stride) {
+        int s, t, b;
+        frame_of(f, s, t, b);
         const int4 raw = nxt;
-        if (f + stride < nfr && lane < 60) nxt = *window_src(f + stride);   // prefetch
+        if (f + stride < nfr && lane < 60) {   // prefetch the next frame's window
+            int s1, t1, b1;
+            frame_of(f + stride, s1, t1, b1);
+            if (t1 >= b1) nxt = *window_src(s1, t1, b1);
+        }
+        if (t < b) continue;   // before this stream's segment (wave-uniform)
+        const unsigned fo = (unsigned)s * (unsigned)a.T + (unsigned)t;   // output frame index
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30
         {
             const uint32_t rw[4] = {(uint32_t)raw.x, (uint32_t)raw.y, (uint32_t)raw.z, (uint32_t)raw.w};
@@ -226,7 +250,7 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
             wave_split_bin(X, L, TB, lane, m, re, im);
             P[lane + 64 * m] = pspec_of(re, im);
             if (a.dbg_spec) {
-                int32_t* ds = a.dbg_spec + (size_t)f * 1024;
+                int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 const int k = lane + 64 * m;
                 if (k) {
                     ds[2 * k] = re; ds[2 * k + 1] = im;
@@ -240,7 +264,7 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
             P[0] = pspec_of(dc, 0);
             P[256] = pspec_of(nyq, 0);
             if (a.dbg_spec) {
-                int32_t* ds = a.dbg_spec + (size_t)f * 1024;
+                int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 ds[0] = dc; ds[1] = 0; ds[512] = nyq; ds[513] = 0;
             }
         }
@@ -262,9 +286,9 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
             int64_t mac = 0;
             for (int k = 0; k < L.mcnt; ++k) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
-            if (a.dbg_log) a.dbg_log[(size_t)f * 40 + lane] = lg;
+            if (a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
             const int64_t d = (int64_t)lg - mean;
-            a.feats[(size_t)f * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
+            a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
         }
         wave_lds_sync();
     }
@@ -491,29 +515,47 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
     }
 }
 
-// prev5 := V[T..T+4] after the chunk; one block per stream, read all then write.
-__global__ __launch_bounds__(64) void ctx_roll_kernel(int16_t* prev5, const int16_t* feats, int S, int T) {
-    const int s = blockIdx.x, c = threadIdx.x;   // c: 8-int16 chunk of the 5x40 context
-    if (s >= S) return;
+// prev5 := last 5 frames of V = prev5 ++ feats[b..T) after the segment; one
+// block per stream, read all then write.
+__global__ __launch_bounds__(64) void ctx_roll_kernel(int16_t* prev5, const int16_t* feats, int S, int T,
+                                                     const int32_t* list, int n_list, const int32_t* seg_begin,
+                                                     int seg_len) {
+    const int i = blockIdx.x, c = threadIdx.x;   // c: 8-int16 chunk of the 5x40 context
+    if (i >= (list ? n_list : S)) return;
+    const int s = list ? list[i] : i;
+    const int b = seg_begin ? seg_begin[s] : 0;
+    const int L = (seg_len > 0 ? min(T, b + seg_len) : T) - b;
+    if (L <= 0) return;
     int4 v = make_int4(0, 0, 0, 0);
     if (c < 25) {
-        const int m = c / 5, part = c % 5, idx = T + m;
+        const int m = c / 5, part = c % 5, idx = L + m;
         v = idx < 5 ? *reinterpret_cast<const int4*>(prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part)
-                    : *reinterpret_cast<const int4*>(feats + ((size_t)s * T + idx - 5) * 40 + 8 * part);
+                    : *reinterpret_cast<const int4*>(feats + ((size_t)s * T + b + idx - 5) * 40 + 8 * part);
     }
     __syncthreads();
     if (c < 25) *reinterpret_cast<int4*>(prev5 + (size_t)s * 200 + 8 * c) = v;
 }
 
-// tail := last 320 samples of (tail ++ chunk), read all before writing.
-__global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int16_t* pcm, int S, int T) {
-    const int s = blockIdx.x;
-    if (s >= S) return;
+// tail := last 320 samples of (tail ++ input frames b..T-1), read all before writing.
+__global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int16_t* pcm, int S, int T,
+                                                      const int32_t* list, int n_list, const int32_t* seg_begin,
+                                                      int seg_len, int lookback, const int16_t* hist, int H) {
+    const int i = blockIdx.x;
+    if (i >= (list ? n_list : S)) return;
+    const int s = list ? list[i] : i;
+    const int b = seg_begin ? seg_begin[s] : 0;
+    const int L = (seg_len > 0 ? min(T, b + seg_len) : T) - b;
+    if (L <= 0) return;
     int16_t v[5];
     for (int k = 0; k < 5; ++k) {
-        const int i = threadIdx.x + 64 * k;
-        const long long pos = 160LL * T + i;   // index into tail(320) ++ pcm(160 T)
-        v[k] = pos < 320 ? tail[(size_t)s * 320 + pos] : pcm[(size_t)s * T * 160 + (pos - 320)];
+        const long long pos = 160LL * L + threadIdx.x + 64 * k;   // index into tail(320) ++ input(160 L)
+        if (pos < 320) {
+            v[k] = tail[(size_t)s * 320 + pos];
+        } else {
+            const long long n = pos - 320;
+            const int x = b + (int)(n / 160) - lookback, o = (int)(n % 160);
+            v[k] = x >= 0 ? pcm[((size_t)s * T + x) * 160 + o] : hist[((size_t)s * H + H + x) * 160 + o];
+        }
     }
     __syncthreads();
     for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
@@ -694,8 +736,10 @@ static int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 extern "C" {
 
 int nnspk_launch_fe(const FeArgs* a, void* stream) {
-    if (a->S <= 0 || a->T <= 0) return 0;
-    const long long nfr = (long long)a->S * a->T;
+    const int nrow = a->list ? a->n_list : a->S;
+    if (nrow <= 0 || a->T <= 0) return 0;
+    const int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
+    const long long nfr = (long long)nrow * W;
     long long blocks = (nfr + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
@@ -708,13 +752,22 @@ int nnspk_launch_nn(const NnImage* img, const NnRun* r, void* stream) {
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_ctx_roll(int16_t* prev5, const int16_t* feats, int S, int T, void* stream) {
-    hipLaunchKernelGGL(ctx_roll_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, prev5, feats, S, T);
+int nnspk_launch_ctx_roll(int16_t* prev5, const int16_t* feats, int S, int T, const int32_t* list, int n_list,
+                          const int32_t* seg_begin, int seg_len, void* stream) {
+    const int n = list ? n_list : S;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(ctx_roll_kernel, dim3(n), dim3(64), 0, (hipStream_t)stream, prev5, feats, S, T, list, n_list,
+                       seg_begin, seg_len);
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_tail_roll(int16_t* tail, const int16_t* pcm, int S, int T, void* stream) {
-    hipLaunchKernelGGL(tail_roll_kernel, dim3(S), dim3(64), 0, (hipStream_t)stream, tail, pcm, S, T);
+int nnspk_launch_tail_roll(int16_t* tail, const int16_t* pcm, int S, int T, const int32_t* list, int n_list,
+                           const int32_t* seg_begin, int seg_len, int lookback, const int16_t* hist,
+                           int hist_frames, void* stream) {
+    const int n = list ? n_list : S;
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(tail_roll_kernel, dim3(n), dim3(64), 0, (hipStream_t)stream, tail, pcm, S, T, list, n_list,
+                       seg_begin, seg_len, lookback, hist, hist_frames);
     return ok(hipGetLastError());
 }
 

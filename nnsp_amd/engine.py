@@ -15,7 +15,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from .nets import NN_ID, THRESH_CNTS, THRESH_PROB, NetData, synth_net
+from .nets import LOOKBACK, NN_ID, THRESH_CNTS, THRESH_PROB, TIMEOUT, NetData, synth_net
 
 
 class NNSPBatch:
@@ -94,6 +94,84 @@ class NNSPBatch:
     def set_state(self, buf: np.ndarray) -> None:
         buf = np.ascontiguousarray(buf, np.uint8)
         _lib.check(_lib.lib().nnsp_batch_set_state(self.h, _lib.ptr(buf), 0, self.S), "set_state")
+
+
+class NNSPCascade:
+    """Batched nnCntrlClass (evb/src/nnCntrlClass.c:57-272): three NNSPBatch
+    objects (s2i, vad, kws; same stream count) driven by the VAD -> KWS -> S2I
+    sequence controller.  ``seq`` lists NNSP_IDs per position (default
+    vad, kws, s2i as in the reference's main)."""
+
+    def __init__(self, nets: dict, seq=(1, 2, 0), lookback_s2i: int = LOOKBACK,
+                 timeout_s2i: int = TIMEOUT, lookback_kws: int = LOOKBACK, timeout_kws: int = TIMEOUT):
+        self.nets = nets   # keep the batches alive
+        order = [nets["s2i"], nets["vad"], nets["kws"]]
+        self.S, self.Tmax = order[0].S, min(b.Tmax for b in order)
+        arr = (C.c_void_p * 3)(*[b.h.value for b in order])
+        sq = np.ascontiguousarray(seq, np.int8)
+        prm = _lib.CascadeParams(lookback_s2i, timeout_s2i, lookback_kws, timeout_kws)
+        h = C.c_void_p()
+        _lib.check(_lib.lib().nnsp_cascade_create(C.byref(h), C.addressof(arr), _lib.ptr(sq), len(sq),
+                                                  C.addressof(prm)), "nnsp_cascade_create")
+        self.h = h
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            _lib.lib().nnsp_cascade_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, mask: np.ndarray | None = None) -> None:
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        _lib.check(_lib.lib().nnsp_cascade_reset(self.h, _lib.ptr(m)), "nnsp_cascade_reset")
+
+    def exec(self, pcm: np.ndarray):
+        """pcm [S][T][160] -> net_ran [S][T] int8, detected [S][T] int16, outputs3 [S][T][3]."""
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        S, T, F = pcm.shape
+        assert S == self.S and F == 160 and 1 <= T <= self.Tmax
+        ran = np.zeros((S, T), np.int8)
+        det = np.zeros((S, T), np.int16)
+        o3 = np.zeros((S, T, 3), np.int16)
+        _lib.check(_lib.lib().nnsp_cascade_exec(self.h, _lib.ptr(pcm), T, _lib.ptr(ran), _lib.ptr(det),
+                                                _lib.ptr(o3)), "nnsp_cascade_exec")
+        return ran, det, o3
+
+    def exec_device(self, pcm_ptr: int, T: int, ran_ptr=None, det_ptr=None, o3_ptr=None) -> None:
+        _lib.check(_lib.lib().nnsp_cascade_exec_device(self.h, pcm_ptr, T, ran_ptr, det_ptr, o3_ptr),
+                   "nnsp_cascade_exec_device")
+
+    def sync(self) -> None:
+        _lib.check(_lib.lib().nnsp_cascade_sync(self.h), "nnsp_cascade_sync")
+
+    def set_window(self, frames: int) -> None:
+        _lib.check(_lib.lib().nnsp_cascade_set_window(self.h, frames), "nnsp_cascade_set_window")
+
+    @property
+    def stream(self) -> int:
+        return _lib.lib().nnsp_cascade_stream(self.h)
+
+    def last_stats(self) -> tuple[int, int, float]:
+        r, f, ms = C.c_int(), C.c_longlong(), C.c_float()
+        _lib.check(_lib.lib().nnsp_cascade_last_stats(self.h, C.byref(r), C.byref(f), C.byref(ms)), "stats")
+        return r.value, f.value, ms.value
+
+    def net_stats(self, name: str) -> tuple[int, float, float]:
+        """(frames scheduled, fe ms, nn ms) of one net in the last chunk."""
+        f, fe, nn = C.c_longlong(), C.c_float(), C.c_float()
+        _lib.check(_lib.lib().nnsp_cascade_last_net_stats(self.h, NN_ID[name], C.byref(f), C.byref(fe),
+                                                          C.byref(nn)), "net_stats")
+        return f.value, fe.value, nn.value
+
+    def positions(self) -> np.ndarray:
+        pos = np.zeros(self.S, np.int8)
+        _lib.check(_lib.lib().nnsp_cascade_positions(self.h, _lib.ptr(pos)), "positions")
+        return pos
 
 
 def device_info() -> dict:

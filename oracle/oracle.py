@@ -132,6 +132,43 @@ class OracleNet:
         return out
 
 
+class OracleCascade:
+    """or_cascade (nnCntrlClass restatement) over S streams; nets by nn id."""
+
+    def __init__(self, nets: dict, seq=(1, 2, 0), lookback_s2i=80, timeout_s2i=1000,
+                 lookback_kws=80, timeout_kws=1000):
+        self.nets = nets
+        c = or_cascade_cfg()
+        for i, name in enumerate(("s2i", "vad", "kws")):
+            c.net[i] = C.addressof(nets[name].net)
+            c.cfg[i] = nets[name].cfg
+        for i, v in enumerate(seq):
+            c.seq[i] = v
+        c.len_seq = len(seq)
+        c.lookback_kws, c.lookback_s2i = lookback_kws, lookback_s2i
+        c.timeout_kws, c.timeout_s2i = timeout_kws, timeout_s2i
+        self.cfg = c
+        self.st = None
+
+    def new_states(self, S: int) -> np.ndarray:
+        st = np.zeros((S, lib().or_sizeof_cascade()), np.uint8)
+        for s in range(S):
+            lib().or_cascade_reset(C.c_void_p(st[s].ctypes.data), C.byref(self.cfg))
+        return st
+
+    def run(self, pcm: np.ndarray, states: np.ndarray | None = None):
+        """pcm [S][T][160] -> net_ran [S][T] int8, detected [S][T], outputs3 [S][T][3], states."""
+        pcm = np.ascontiguousarray(pcm, np.int16)
+        S, T, _ = pcm.shape
+        if states is None:
+            states = self.new_states(S)
+        ran = np.zeros((S, T), np.int8)
+        det = np.zeros((S, T), np.int16)
+        o3 = np.zeros((S, T, 3), np.int16)
+        lib().or_run_cascade(C.byref(self.cfg), p(states), S, T, p(pcm), p(ran), p(det), p(o3))
+        return ran, det, o3, states
+
+
 def rfft512(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     x = np.ascontiguousarray(x, np.int32).copy()
     xi = np.zeros(514, np.int32)

@@ -1,0 +1,104 @@
+"""GPU parity of the batched VAD -> KWS -> S2I cascade (nnCntrlClass,
+evb/src/nnCntrlClass.c:152-272) against the CPU oracle's or_run_cascade.
+
+Per stream and frame: the net that ran, its trigger and NNSPClass.outputs must
+match bit-exactly, across chunk boundaries (the speculative per-round segments
+are cut at each switch), with look-back into earlier chunks, timeouts and
+partial resets (nnCntrlClass_reset keeps the sequence position).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from oracle import OracleCascade, OracleNet, lib, synthetic_pcm
+
+from nnsp_amd.engine import NNSPBatch, NNSPCascade
+from nnsp_amd.nets import synth_net
+
+pytestmark = pytest.mark.gpu
+
+POS_OFF = 100 * 160 * 2 + 4   # or_cascade.pos_seq (nnsp_oracle.h: ring, idx_set, idx_latest)
+
+# (thresh_prob, th_count) per net: low enough that every stage triggers
+TH = {"lively": {"vad": (3000, 1), "kws": (8000, 1), "s2i": (12000, 1)},
+      "slow": {"vad": (8000, 1), "kws": (16383, 2), "s2i": (16383, 2)}}
+
+
+def _pcm(S, T, seed):
+    pcm = synthetic_pcm(S, T, seed=0x4E4E5350 + seed)
+    rng = np.random.default_rng(seed)
+    pcm[1::4] = (pcm[1::4].astype(np.int32) * 5).clip(-32768, 32767).astype(np.int16)
+    pcm[2::6] //= 32
+    quiet = rng.integers(0, T, S // 3)
+    for s, t in zip(range(0, S, 3), quiet):   # silence gaps
+        pcm[s, t:t + 40] = 0
+    return pcm
+
+
+def _build(th, S, Tmax, acc32, seq, lb_s2i, to_s2i, lb_kws, to_kws):
+    onets, gnets = {}, {}
+    for name in ("vad", "kws", "s2i"):
+        data = synth_net(name, 1234)
+        thr, cnt = th[name]
+        onets[name] = OracleNet(data, acc32=acc32, thresh_prob=thr, th_count=cnt)
+        gnets[name] = NNSPBatch(data, S, Tmax, acc32=acc32, thresh_prob=thr, th_count=cnt)
+    oc = OracleCascade(onets, seq, lb_s2i, to_s2i, lb_kws, to_kws)
+    gc = NNSPCascade(gnets, seq, lb_s2i, to_s2i, lb_kws, to_kws)
+    return oc, gc, gnets
+
+
+def _check(oc, gc, pcm, chunks, reset_at=None, reset_mask=None):
+    S = pcm.shape[0]
+    st = oc.new_states(S)
+    t0 = 0
+    switches = 0
+    for i, Tc in enumerate(chunks):
+        if reset_at is not None and i == reset_at:
+            gc.reset(reset_mask)
+            for s in np.nonzero(reset_mask)[0]:   # nnCntrlClass_reset: position kept
+                pos = st[s, POS_OFF:POS_OFF + 2].copy()
+                lib().or_cascade_reset(C.c_void_p(st[s].ctypes.data), C.byref(oc.cfg))
+                st[s, POS_OFF:POS_OFF + 2] = pos
+        seg = pcm[:, t0:t0 + Tc]
+        o_ran, o_det, o_o3, st = oc.run(seg, st)
+        g_ran, g_det, g_o3 = gc.exec(seg)
+        np.testing.assert_array_equal(g_ran, o_ran, err_msg=f"net_ran chunk@{t0}")
+        np.testing.assert_array_equal(g_det, o_det, err_msg=f"detected chunk@{t0}")
+        np.testing.assert_array_equal(g_o3, o_o3, err_msg=f"outputs3 chunk@{t0}")
+        switches += int((np.diff(o_ran.astype(np.int32), axis=1) != 0).sum())
+        t0 += Tc
+    pos = st[:, POS_OFF:POS_OFF + 2].copy().view(np.int16)[:, 0]
+    np.testing.assert_array_equal(gc.positions(), pos.astype(np.int8))
+    return switches
+
+
+@pytest.mark.parametrize("th", ["lively", "slow"])
+@pytest.mark.parametrize("acc32", [False, True])
+@pytest.mark.parametrize("window", [32, 0])
+def test_cascade_matches_oracle(th, acc32, window):
+    S, chunks = 150, [100, 37, 1, 63]
+    oc, gc, _ = _build(TH[th], S, max(chunks), acc32, (1, 2, 0), 80, 60, 80, 50)
+    gc.set_window(window)
+    sw = _check(oc, gc, _pcm(S, sum(chunks), 11), chunks)
+    assert sw > 50, "cascade never switched nets: test is vacuous"
+    r, frames, _ = gc.last_stats()
+    assert r >= 1 and frames >= S * chunks[-1]
+
+
+def test_cascade_short_lookback_timeouts_and_order():
+    # odd look-backs, tiny timeouts (counter wrap), a different sequence order
+    S, chunks = 70, [30, 30, 17, 50]
+    oc, gc, _ = _build(TH["slow"], S, 50, False, (1, 0, 2), 17, 7, 3, 5)
+    gc.set_window(5)
+    sw = _check(oc, gc, _pcm(S, sum(chunks), 5), chunks)
+    assert sw > 50
+
+
+def test_cascade_partial_reset():
+    S, chunks = 64, [40, 40, 40]
+    oc, gc, _ = _build(TH["lively"], S, 40, False, (1, 2, 0), 80, 60, 80, 50)
+    gc.set_window(1)
+    mask = np.zeros(S, np.uint8)
+    mask[::3] = 1
+    _check(oc, gc, _pcm(S, sum(chunks), 9), chunks, reset_at=2, reset_mask=mask)
