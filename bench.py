@@ -152,6 +152,7 @@ def main() -> None:
     torch.cuda.synchronize()
     kt = {}            # kernel -> total ms over the timed steps
     kframes = {}       # kernel -> frames (fe) or NN frames it processed
+    klaunch = {}       # kernel -> launches
     rounds = 0
     t0 = time.perf_counter()
     for i in range(K):
@@ -160,17 +161,21 @@ def main() -> None:
             r, _, _ = eng.last_stats()
             rounds += r
             for n in ("vad", "kws", "s2i"):
-                f, fe, nn = eng.net_stats(n)
+                f, fe, nn, nl = eng.net_stats(n)
                 kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + fe
                 kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + f
+                klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + nl
                 kt[f"nn_{n}"] = kt.get(f"nn_{n}", 0.0) + nn
                 kframes[f"nn_{n}"] = kframes.get(f"nn_{n}", 0) + f
+                klaunch[f"nn_{n}"] = klaunch.get(f"nn_{n}", 0) + nl
         else:
             f, n = eng.last_timing()   # syncs the stream: per-step kernel times
             kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + f
             kt[f"nn_{args.net}"] = kt.get(f"nn_{args.net}", 0.0) + n
             kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
             kframes[f"nn_{args.net}"] = kframes.get(f"nn_{args.net}", 0) + S * T
+            klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + 1
+            klaunch[f"nn_{args.net}"] = klaunch.get(f"nn_{args.net}", 0) + 1
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -188,22 +193,25 @@ def main() -> None:
         valu_peak = cu * 128 * clk / 1e12          # int32 VALU lane-ops/s (4 SIMD32 per CU)
         mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
         dom = max(kt, key=kt.get)                  # dominant kernel by device time
-        dom_s = kt[dom] / 1e3
+        launches = klaunch[dom]
+        avg_launch_s = kt[dom] / 1e3 / launches    # HIP-event time on the engine's stream
+        units = kframes[dom] / launches            # frames per launch
         if dom == "fe_kernel":
-            achieved = kframes[dom] * FE_MULS_PER_FRAME / dom_s / 1e12
-            work = "integer multiplies (SURVEY 8(d): 5912 per frame)"
+            per_unit = FE_MULS_PER_FRAME
+            work = "integer multiplies (SURVEY 8(d): 5912 per frame) x frames per launch"
             peak, bound = valu_peak, "valu"
         else:
             n = dom[3:]
-            achieved = kframes[dom] / 2 * NN_MACS_PER_INFERENCE[n] * 2 / dom_s / 1e12
-            work = f"{n} int8xint16 MACs x2 ops (NN runs every 2nd frame)"
+            per_unit = NN_MACS_PER_INFERENCE[n]    # one inference per 2 frames, 2 ops per MAC
+            work = f"{n} int8xint16 MACs x2 ops x inferences (frames/2) per launch"
             peak, bound = mfma_peak, "mfma"
+        achieved = units * per_unit / avg_launch_s / 1e12
         traffic = None
         try:
             with open(args.profile_json) as f:
                 pj = json.load(f)
-            if pj.get("net") == args.net and pj.get("streams") == S and pj.get("frames") == T:
-                traffic = pj.get("fe_kernel_hbm_bytes_per_launch")
+            if pj.get("workload") == args.net and pj.get("streams") == S and pj.get("frames") == T:
+                traffic = pj["kernels"][dom]["hbm_bytes_per_launch"]
         except Exception:
             pass
         fe_s = kt["fe_kernel"] / 1e3
@@ -228,7 +236,9 @@ def main() -> None:
             "roofline": {"kernel": dom, "bound": bound,
                          "achieved": achieved, "peak": peak, "unit": "Tops/s",
                          "frac": achieved / peak, "work": work,
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC, profiles/)",
+                         "launches_per_step": launches / K, "avg_launch_ms": avg_launch_s * 1e3,
+                         "frames_per_launch": units,
                          "hbm_achieved_GBps": kframes["fe_kernel"] * FE_HBM_BYTES_PER_FRAME / fe_s / 1e9,
                          "hbm_peak_GBps": 8000.0},
             "device": info,

@@ -73,11 +73,12 @@ void *nnsp_cascade_stream(nnsp_cascade *c);
  * work past a switch that the switch discarded), device time in ms. */
 int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run, float *ms);
 
-/* Last chunk, one net (NNSP_ID): frames scheduled on it, and the device time
- * of its front-end kernel and of its NN kernels (proj + recur), summed over
- * the rounds. */
+/* Last chunk, one net (NNSP_ID): frames scheduled on it, the device time of
+ * its front-end kernel and of its NN kernels (proj + recur) summed over the
+ * rounds, and the number of rounds it ran in (one launch of each kernel per
+ * round). */
 int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms,
-                                float *nn_ms);
+                                float *nn_ms, int *launches);
 
 /* current_pos_seq of every stream -> host int8 [S]. */
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);

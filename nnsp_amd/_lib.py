@@ -114,7 +114,7 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),
         "nnsp_cascade_last_net_stats": (I, [P, I, C.POINTER(C.c_longlong), C.POINTER(C.c_float),
-                                            C.POINTER(C.c_float)]),
+                                            C.POINTER(C.c_float), C.POINTER(I)]),
         "nnsp_synth_pcm": (I, [P, I, I, C.c_uint64, I, C.c_int64, I, P]),
         "nnsp_device_count": (I, [C.POINTER(I)]),
         "nnsp_set_device": (I, [I]),

@@ -45,6 +45,7 @@ struct nnsp_cascade {
     int last_rounds;
     int window;                     /* frames per stream and round (0: to the chunk end) */
     float fe_ms[3], nn_ms[3];       /* last chunk, per net id: device time of fe / proj+recur */
+    int runs[3];                    /* last chunk, per net id: segment runs (fe launches) */
 };
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
@@ -188,7 +189,10 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     TRY(nnspk_event_record(c->ev[0], c->stream));
     TRY(nnspk_memset(c->d_counts, 0, 12, c->stream));
     TRY(nnspk_memset(c->d_frames, 0, 3 * 8, c->stream));
-    for (int n = 0; n < 3; ++n) c->fe_ms[n] = c->nn_ms[n] = 0.f;
+    for (int n = 0; n < 3; ++n) {
+        c->fe_ms[n] = c->nn_ms[n] = 0.f;
+        c->runs[n] = 0;
+    }
     TRY(nnspk_launch_casc_begin(&a, c->stream));
     TRY(nnspk_d2h(cnt, c->d_counts, 12, c->stream));
     TRY(nnspk_sync(c->stream));
@@ -199,6 +203,7 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
         for (int n = 0; n < 3; ++n) {
             ran[n] = cnt[n] > 0;
             if (!cnt[n]) continue;
+            c->runs[n]++;
             nnsp_batch *b = c->net[n];
             nnsp_segment seg;
             memset(&seg, 0, sizeof seg);
@@ -292,7 +297,8 @@ int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run,
     return 0;
 }
 
-int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms, float *nn_ms)
+int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms, float *nn_ms,
+                                int *launches)
 {
     if (!c || nn_id < 0 || nn_id > 2) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
@@ -304,6 +310,7 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
     }
     if (fe_ms) *fe_ms = c->fe_ms[nn_id];
     if (nn_ms) *nn_ms = c->nn_ms[nn_id];
+    if (launches) *launches = c->runs[nn_id];
     return 0;
 }
 

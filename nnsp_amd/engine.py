@@ -161,12 +161,12 @@ class NNSPCascade:
         _lib.check(_lib.lib().nnsp_cascade_last_stats(self.h, C.byref(r), C.byref(f), C.byref(ms)), "stats")
         return r.value, f.value, ms.value
 
-    def net_stats(self, name: str) -> tuple[int, float, float]:
-        """(frames scheduled, fe ms, nn ms) of one net in the last chunk."""
-        f, fe, nn = C.c_longlong(), C.c_float(), C.c_float()
+    def net_stats(self, name: str) -> tuple[int, float, float, int]:
+        """(frames scheduled, fe ms, nn ms, launches) of one net in the last chunk."""
+        f, fe, nn, n = C.c_longlong(), C.c_float(), C.c_float(), C.c_int()
         _lib.check(_lib.lib().nnsp_cascade_last_net_stats(self.h, NN_ID[name], C.byref(f), C.byref(fe),
-                                                          C.byref(nn)), "net_stats")
-        return f.value, fe.value, nn.value
+                                                          C.byref(nn), C.byref(n)), "net_stats")
+        return f.value, fe.value, nn.value, n.value
 
     def positions(self) -> np.ndarray:
         pos = np.zeros(self.S, np.int8)

@@ -11,7 +11,7 @@
  *     and the CMSIS-DSP data sections (tests/test_tables.py);
  *   - post-FFT front end, activations, post-processing, reset logic: pinned
  *     against reference C files compiled here from their own sources
- *     (oracle/_ref, tests/test_oracle_vs_ref.py);
+ *     (oracle/_ref -> tests/golden/ref_stages.npz, tests/test_oracle_pinned.py);
  *   - weight layout: pinned against python/nnsp_pack/c_weight_man.py;
  *   - affine/LSTM MAC kernels (affine.c ARM path needs ARM DSP intrinsics)
  *     and the CMSIS arm_rfft_q31 (binary-only third-party code): restated,
