@@ -32,11 +32,15 @@ static void plan_fast(nnsp_batch *b)
         if (g->L[i].N > 128 || g->L[i].K > 128) return;
     const int a_proj = (int)g->L[li].ar_off;
     const int a_rec = (int)(b->im.a_bytes - (size_t)g->L[li].ar_off);
-    if (nnspk_fast_lds_bytes(0, a_proj, 4) > LDS_MAX) return;
-    if (nnspk_fast_lds_bytes(1, a_rec, 1) > LDS_MAX) return;
+    /* epilogue rows: proj covers layers 0..li, recur li..nl-1 */
+    b->ep_proj = g->L[li].ep_off + 16 * g->L[li].nrt;
+    b->ep_rec_lo = g->L[li].ep_off;
+    b->ep_rec_n = b->im.rows_total - g->L[li].ep_off;
+    if (nnspk_fast_lds_bytes(0, a_proj, 4, b->ep_proj) > LDS_MAX) return;
+    if (nnspk_fast_lds_bytes(1, a_rec, 1, b->ep_rec_n) > LDS_MAX) return;
     /* tiles per 4-wave group in one workgroup: 2 once there are >= 2 tiles per CU */
     const int tiles = (b->S + 15) / 16;
-    b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2) <= LDS_MAX) ? 2 : 1;
+    b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2, b->ep_rec_n) <= LDS_MAX) ? 2 : 1;
     b->li = li;
     b->nstep_max = (b->Tmax + 1) / 2;
     const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);
@@ -112,6 +116,10 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
         if ((e = nnspk_set_lds_limit())) goto fail;
         const size_t rows = (size_t)b->im.img.L[b->li].rows;
         if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
+        if (getenv("NNSP_RECUR_CLOCKS")) { /* development probe of recur_kernel phases */
+            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 8 * 8))) goto fail;
+            if ((e = nnspk_memset(b->d_clk, 0, 64 * 8 * 8, b->stream))) goto fail;
+        }
     }
     if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
     if ((e = nnspk_h2d(b->d_stdR, stdR, 40 * 4, b->stream))) goto fail;
@@ -131,7 +139,7 @@ void nnsp_batch_destroy(nnsp_batch *b)
     if (b->stream) nnspk_sync(b->stream);
     nnsp_image_free(&b->im);
     void *bufs[] = {b->d_mean, b->d_stdR, b->d_tail, b->d_prev5, b->d_h, b->d_c, b->d_post,
-                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx};
+                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx, b->d_clk};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 3; ++i) nnspk_event_destroy(b->ev[i]);
     nnspk_stream_destroy(b->stream);
@@ -210,9 +218,12 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
         f.n_list = seg->n_list;
         f.seg_begin = seg->seg_begin;
         f.seg_len = seg->seg_len;
+        f.dbg_clk = b->d_clk;
         const NnLayer *LL = &b->im.img.L[b->li];
         f.a_off = 0;
         f.a_lds_bytes = (int)LL->ar_off;
+        f.ep_lo = 0;
+        f.ep_n = b->ep_proj;
         int blocks = b->proj_blocks;
         if (seg->list) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
@@ -223,6 +234,8 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
         TRY(nnspk_launch_proj(&b->im.img, &f, blocks, stream));
         f.a_off = LL->ar_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
+        f.ep_lo = b->ep_rec_lo;
+        f.ep_n = b->ep_rec_n;
         TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, stream));
     } else {
         NnRun r;
@@ -340,6 +353,15 @@ int nnsp_batch_get_state(nnsp_batch *b, void *host, int first, int count)
 int nnsp_batch_set_state(nnsp_batch *b, const void *host, int first, int count)
 {
     return state_xfer(b, (void *)host, first, count, 1);
+}
+
+/* development probe (not in the public header): recur_kernel phase clocks of
+ * tile 0 for the last chunk, [64 steps][8] s_memtime values */
+int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
+{
+    if (!b || !out || !b->d_clk) return NNSP_EINVAL;
+    TRY(nnspk_d2h(out, b->d_clk, 64 * 8 * 8, b->stream));
+    return nnspk_sync(b->stream);
 }
 
 int nnsp_synth_pcm(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp, void *stream)

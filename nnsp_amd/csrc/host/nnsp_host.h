@@ -59,7 +59,9 @@ struct nnsp_batch {
     int last_T;
     /* split NN path (one LSTM layer) */
     int fast, li, nstep_max, rec_waves, proj_blocks;
+    int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int32_t *d_gx;
+    long long *d_clk; /* NNSP_RECUR_CLOCKS development probe */
 };
 
 /* One segment launch of a batch: the streams list[0..n_list) (NULL: all),

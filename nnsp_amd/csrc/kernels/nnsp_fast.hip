@@ -29,6 +29,47 @@ using namespace nnsp;
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
 #define R_CW 128        // int32 per row of the c buffer
 
+// per-row epilogue constants, staged into LDS (global loads in the per-step
+// epilogue put an L2 round trip on the recurrence's critical path).  bterm is
+// the bias term affine_Krows_8x16 adds before the output shift (affine.c:190-217):
+// b << (qbit_s - qb) (or >>), 64-bit for acc64, wrapping int32 for acc32.
+struct EpRow {
+    int32_t wsum, wsum_r;
+    int64_t bterm;
+};
+
+__device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, int n) {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int row = lo + i;
+        int li = 0;
+        while (li + 1 < img.nl && img.L[li + 1].ep_off <= row) ++li;
+        const NnLayer& Ly = img.L[li];
+        const int16_t b = img.bias[row];
+        int64_t bt = 0;
+        if (Ly.has_bias) {
+            if (img.acc32)
+                bt = Ly.bias_sh >= 0 ? wshl(b, Ly.bias_sh) : ((int32_t)b >> -Ly.bias_sh);
+            else
+                bt = Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
+        }
+        ep[i] = EpRow{img.wsum[row], img.wsum_r[row], bt};
+    }
+}
+
+// affine_Krows_8x16 output stage with the bias term already folded in:
+// shift_64b + clamp (acc64) or shift_32b (acc32).  rsh/lsh = the layer's
+// output shift split by sign (lsh > 0 never happens for the reference nets).
+template <bool ACC32>
+__device__ __forceinline__ int32_t ep_shift(int64_t pre, int rsh, int lsh) {
+    if (ACC32) {
+        const int32_t v = (int32_t)pre;
+        return __builtin_expect(lsh > 0, 0) ? shift32(v, lsh) : (v >> rsh);
+    }
+    return sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
+}
+
+__host__ __device__ inline size_t ep_bytes(int n) { return ((size_t)n * sizeof(EpRow) + 15) & ~(size_t)15; }
+
 struct ProjWave {
     int16_t uni[P_UNION + 32];
     int16_t act[2][16][P_ASTRIDE];
@@ -43,8 +84,8 @@ __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, 
 // One FC layer on a 16-row tile: B from an LDS buffer (row stride in_stride),
 // A fragments from LDS, output to an LDS buffer (row stride out_stride).
 __device__ __forceinline__ void fc_tile(const NnImage& img, const NnLayer& Ly, const uint8_t* A,
-                                        const int16_t* in, int in_stride, int16_t* out, int out_stride,
-                                        const int16_t* tt, int lane) {
+                                        const EpRow* ep, const int16_t* in, int in_stride, int16_t* out,
+                                        int out_stride, const int16_t* tt, int lane) {
     v4i bh[4], bl[4];
     load_b<4>(in, in_stride, Ly.nkt, lane, bh, bl);
     const int sc = lane & 15, q = lane >> 4;
@@ -61,8 +102,10 @@ __device__ __forceinline__ void fc_tile(const NnImage& img, const NnLayer& Ly, c
         for (int i = 0; i < 4; ++i) {
             const int row = 16 * rt + 4 * q + i;
             if (row >= Ly.rows) continue;
-            const int32_t sum = (ah[i] << 8) + al[i] + img.wsum[Ly.ep_off + row];
-            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
+            const EpRow& er = ep[row];
+            const int32_t sum = (ah[i] << 8) + al[i] + er.wsum;
+            const int32_t v = img.acc32 ? shift32(wadd(sum, (int32_t)er.bterm), Ly.out_sh)
+                                        : sat32(shift64((int64_t)sum + er.bterm, Ly.out_sh));
             if (Ly.act == ACT_LINEAR)
                 reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
             else
@@ -78,8 +121,10 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    ProjWave* pw = reinterpret_cast<ProjWave*>(smem + r.a_lds_bytes + 768);
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
+    ProjWave* pw = reinterpret_cast<ProjWave*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    stage_ep(ep, img, r.ep_lo, r.ep_n);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     __syncthreads();
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -117,7 +162,8 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
         for (int i = 0; i < r.li; ++i) {
             const NnLayer& Ly = img.L[i];
             int16_t* out = &P.act[i & 1][0][0];
-            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), in, in_stride, out, P_ASTRIDE, tt, lane);
+            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in, in_stride, out, P_ASTRIDE,
+                    tt, lane);
             wave_lds_sync();
             in = out;
             in_stride = P_ASTRIDE;
@@ -139,11 +185,12 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
                         ah = mfma8(w, bh[kt], ah);
                         al = mfma8(w, bl[kt], al);
                     }
+                const EpRow* er = ep + (LL.ep_off - r.ep_lo) + 16 * rt + 4 * q;
                 int4 o;
-                o.x = (ah[0] << 8) + al[0] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 0];
-                o.y = (ah[1] << 8) + al[1] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 1];
-                o.z = (ah[2] << 8) + al[2] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 2];
-                o.w = (ah[3] << 8) + al[3] + img.wsum[LL.ep_off + 16 * rt + 4 * q + 3];
+                o.x = (ah[0] << 8) + al[0] + er[0].wsum;
+                o.y = (ah[1] << 8) + al[1] + er[1].wsum;
+                o.z = (ah[2] << 8) + al[2] + er[2].wsum;
+                o.w = (ah[3] << 8) + al[3] + er[3].wsum;
                 if (act) *reinterpret_cast<int4*>(dst + 16 * rt) = o;
             }
         }
@@ -152,14 +199,24 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
 }
 
 // ---------------------------------------------------------------------------
-// recur_kernel: one 16-stream tile per RG waves (row tiles dealt round-robin),
-// TPW tiles per workgroup; weights staged once per workgroup.
+// recur_kernel: one 16-stream tile per RW waves, TPW tiles per workgroup;
+// weights and epilogue constants staged once per workgroup.
+//   waves 0..RG-1 ("LSTM waves"): step j -- Wh.h + gx, gate epilogue, cell and
+//                 hidden update; LSTM row tiles dealt round-robin;
+//   wave  RG      ("tail wave"):  step j-1 -- the FC layers after the LSTM,
+//                 post-processing, trigger / logits / outputs stores.
+// Nothing recurrent depends on the tail, so it runs one step behind the LSTM
+// waves with a single workgroup barrier per step.  h is double-buffered: step
+// j reads h[cur] and writes h[cur^1]; the tail reads h[cur] (step j-1's
+// result) in the same iteration; step j+1 overwrites h[cur] only after the
+// next barrier, which the tail reaches once it is done with it.
 // ---------------------------------------------------------------------------
 #define RG 4
+#define RW (RG + 1)
 
 struct RecTile {
     int16_t h[2][16][R_STRIDE];     // LSTM h, ping-pong across steps
-    int16_t act[2][16][R_STRIDE];   // FC activations, ping-pong across layers
+    int16_t act[2][16][R_STRIDE];   // tail wave: FC activations, ping-pong across layers
     int32_t c[16][R_CW];
     int32_t phase[16];
     int32_t nst[16];    // NN steps of each stream's segment
@@ -167,17 +224,20 @@ struct RecTile {
     int32_t end[16];    // segment end frame (exclusive)
 };
 
-template <int RPW>   // LSTM row tiles per wave = ceil(nrt / RG)
-__global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
+template <int RPW, bool ACC32>   // RPW: LSTM row tiles per wave = ceil(nrt / RG)
+__global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    RecTile* tiles = reinterpret_cast<RecTile*>(smem + r.a_lds_bytes + 768);
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
+    RecTile* tiles = reinterpret_cast<RecTile*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    stage_ep(ep, img, r.ep_lo, r.ep_n);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int tpw = blockDim.x / (64 * RG);
-    const int tl = wv / RG, g = wv - tl * RG;   // tile in workgroup, wave in tile
+    const int tpw = blockDim.x / (64 * RW);
+    const int tl = wv / RW, g = wv - tl * RW;   // tile in workgroup, wave in tile
+    const bool tail = g == RG;
     RecTile& R = tiles[tl];
     const int sc = lane & 15, q = lane >> 4;
     // tile = 16 consecutive entries of the stream list (identity when list == NULL)
@@ -187,8 +247,9 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     const bool valid = i0 + sc < nrow;
     const int s = valid ? sid(i0 + sc) : 0;
     const NnLayer& LL = img.L[r.li];
-    const int N = LL.N, rows = LL.rows, nrt = LL.nrt;
-    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
+    const int N = LL.N, rows = LL.rows, nrt = LL.nrt, nkt_r = LL.nkt_r;
+    const int xs_sh = LL.xs_sh, rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
+    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RW) {
         const int st = idx / N, u = idx - st * N;
         const bool ok = i0 + st < nrow;
         const int gs = ok ? sid(i0 + st) : 0;
@@ -197,7 +258,7 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     }
     const int T = r.T;
     PostState ps = {};
-    if (g == 0 && lane < 16) {
+    if (tail && lane < 16) {
         const int b = valid && r.seg_begin ? r.seg_begin[s] : 0;
         const int e = r.seg_len > 0 ? min(T, b + r.seg_len) : T;
         if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
@@ -214,12 +275,13 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
     int nsteps = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
-    if (g == 0 && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
+    if (tail && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
         if (r.trig) r.trig[(size_t)s * T + b] = ps.trigger;
         if (r.out3)
             for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
     }
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
+    const EpRow* epl = ep + (LL.ep_off - r.ep_lo);
     v4i gxv[RPW];
     auto load_gx = [&](int jj) {
         const bool ok = valid && b + 2 * jj + phase < e;
@@ -230,89 +292,107 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
             if (rt < nrt) gxv[k] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
         }
     };
-    load_gx(0);
-    int hb = 0;
-    for (int j = 0; j < nsteps; ++j) {
-        const int t = b + 2 * j + phase;
-        const bool active = valid && t < e;
-        v4i bh[2], bl[2];
-        load_b<2>(&R.h[hb][0][0], R_STRIDE, LL.nkt_r, lane, bh, bl);
-        // ---- LSTM (lstm.c:48-124): row tile = 4 units x gates i, j, f, o
+    if (!tail) load_gx(0);
+    long long* clk = (r.dbg_clk && blockIdx.x == 0 && tl == 0 && (g == 0 || tail)) ? r.dbg_clk + (tail ? 4 : 0)
+                                                                                     : nullptr;
+#define PROBE(k) \
+    if (clk && j < 64) clk[j * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime()
+    int cur = 0;
+    for (int j = 0; j <= nsteps; ++j) {
+        PROBE(0);
+        if (!tail) {
+            if (j < nsteps) {
+                // ---- LSTM step j (lstm.c:48-124): row tile = 4 units x gates i, j, f, o
+                const int t = b + 2 * j + phase;
+                const bool active = valid && t < e;
+                v4i bh[2], bl[2];
+                load_b<2>(&R.h[cur][0][0], R_STRIDE, nkt_r, lane, bh, bl);
 #pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-            const int rt = g + RG * k;
-            if (rt < nrt) {
-                v4i hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
+                for (int k = 0; k < RPW; ++k) {
+                    const int rt = g + RG * k;
+                    if (rt < nrt) {
+                        v4i hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
 #pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-                    if (kt < LL.nkt_r) {
-                        const v4i w = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * LL.nkt_r + kt) * 1024 + 16 * lane);
-                        hh = mfma8(w, bh[kt], hh);
-                        hl = mfma8(w, bl[kt], hl);
+                        for (int kt = 0; kt < 2; ++kt)
+                            if (kt < nkt_r) {
+                                const v4i w = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * nkt_r + kt) * 1024 + 16 * lane);
+                                hh = mfma8(w, bh[kt], hh);
+                                hl = mfma8(w, bl[kt], hl);
+                            }
+                        const int u = 4 * rt + q;
+                        if (u < N) {
+                            int16_t gt[4];
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const EpRow& er = epl[16 * rt + 4 * q + i];
+                                const int32_t sx = gxv[k][i];
+                                const int32_t sh = (hh[i] << 8) + hl[i] + er.wsum_r;
+                                int64_t pre;
+                                if (ACC32) {
+                                    const int32_t x = __builtin_expect(xs_sh != 0, 0) ? shift32(sx, xs_sh) : sx;
+                                    pre = wadd(wadd(x, sh), (int32_t)er.bterm);
+                                } else {
+                                    const int64_t x = __builtin_expect(xs_sh != 0, 0) ? shift64((int64_t)sx, xs_sh)
+                                                                                      : (int64_t)sx;
+                                    pre = x + sh + er.bterm;
+                                }
+                                const int32_t v = ep_shift<ACC32>(pre, rsh, lsh);
+                                gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                            }
+                            const int32_t c_old = R.c[sc][u];
+                            const int32_t c_new = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old) >> 15);
+                            const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * gt[3]) >> 15);
+                            if (active) R.c[sc][u] = c_new;
+                            R.h[cur ^ 1][sc][u] = active ? hv : R.h[cur][sc][u];   // h after all groups (T6)
+                        }
                     }
-                const int u = 4 * rt + q;
-                if (u < N) {
-                    int16_t gt[4];
+                }
+                if (j + 1 < nsteps) load_gx(j + 1);
+            }
+        } else if (j > 0) {
+            // ---- tail: step j-1's FC layers after the LSTM, outputs, post-processing
+            const int jj = j - 1;
+            const int t = b + 2 * jj + phase;
+            const bool active = valid && t < e;
+            const int16_t* in = &R.h[cur][0][0];
+            int ab = 0;
+            for (int i = r.li + 1; i < img.nl; ++i) {
+                const NnLayer& Ly = img.L[i];
+                const uint8_t* A = W + (Ly.a_off - r.a_off);
+                const EpRow* epi = ep + (Ly.ep_off - r.ep_lo);
+                const int nkt = Ly.nkt, lrt = Ly.nrt, lrows = Ly.rows, act = Ly.act;
+                const int ors = Ly.out_sh < 0 ? -Ly.out_sh : 0, ols = Ly.out_sh > 0 ? Ly.out_sh : 0;
+                int16_t* out = &R.act[ab][0][0];
+                v4i fh[2], fl[2];
+                load_b<2>(in, R_STRIDE, nkt, lane, fh, fl);
+                for (int rt = 0; rt < lrt; ++rt) {
+                    v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const int row = 16 * rt + 4 * q + i;
-                        const int32_t sx = gxv[k][i];
-                        const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[LL.ep_off + row];
-                        int64_t pre;
-                        if (img.acc32)
-                            pre = (int64_t)wadd(shift32(sx, LL.xs_sh), sh);
+                    for (int kt = 0; kt < 2; ++kt)
+                        if (kt < nkt) {
+                            const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * nkt + kt) * 1024 + 16 * lane);
+                            ah = mfma8(w, fh[kt], ah);
+                            al = mfma8(w, fl[kt], al);
+                        }
+#pragma unroll
+                    for (int x = 0; x < 4; ++x) {
+                        const int row = 16 * rt + 4 * q + x;
+                        if (row >= lrows) continue;
+                        const EpRow& er = epi[row];
+                        const int32_t sum = (ah[x] << 8) + al[x] + er.wsum;
+                        const int64_t pre = ACC32 ? (int64_t)wadd(sum, (int32_t)er.bterm) : (int64_t)sum + er.bterm;
+                        const int32_t v = ep_shift<ACC32>(pre, ors, ols);
+                        if (act == ACT_LINEAR)
+                            reinterpret_cast<int32_t*>(out + sc * R_STRIDE)[row] = v;
                         else
-                            pre = shift64((int64_t)sx, LL.xs_sh) + (int64_t)sh;
-                        const int32_t v = affine_out(pre, img.bias[LL.ep_off + row], LL, img.acc32);
-                        gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                            out[sc * R_STRIDE + row] = act16(act, v, tt);
                     }
-                    const int32_t c_old = R.c[sc][u];
-                    const int32_t c_new = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old) >> 15);
-                    const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * gt[3]) >> 15);
-                    if (active) R.c[sc][u] = c_new;
-                    R.h[hb ^ 1][sc][u] = active ? hv : R.h[hb][sc][u];   // h after all groups (T6)
                 }
+                wave_lds_sync();
+                in = out;
+                ab ^= 1;
             }
-        }
-        if (j + 1 < nsteps) load_gx(j + 1);
-        __syncthreads();
-        hb ^= 1;
-        // ---- FC layers after the LSTM (rows tiles dealt over the RG waves)
-        const int16_t* in = &R.h[hb][0][0];
-        int cur = 0;
-        for (int i = r.li + 1; i < img.nl; ++i) {
-            const NnLayer& Ly = img.L[i];
-            const uint8_t* A = W + (Ly.a_off - r.a_off);
-            int16_t* out = &R.act[cur][0][0];
-            v4i fh[2], fl[2];
-            load_b<2>(in, R_STRIDE, Ly.nkt, lane, fh, fl);
-            for (int rt = g; rt < Ly.nrt; rt += RG) {
-                v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
-                    if (kt < Ly.nkt) {
-                        const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * Ly.nkt + kt) * 1024 + 16 * lane);
-                        ah = mfma8(w, fh[kt], ah);
-                        al = mfma8(w, fl[kt], al);
-                    }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int row = 16 * rt + 4 * q + e;
-                    if (row >= Ly.rows) continue;
-                    const int32_t sum = (ah[e] << 8) + al[e] + img.wsum[Ly.ep_off + row];
-                    const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
-                    if (Ly.act == ACT_LINEAR)
-                        reinterpret_cast<int32_t*>(out + sc * R_STRIDE)[row] = v;
-                    else
-                        out[sc * R_STRIDE + row] = act16(Ly.act, v, tt);
-                }
-            }
-            __syncthreads();
-            in = out;
-            cur ^= 1;
-        }
-        // ---- outputs and post-processing (nn_speech.c:92-124), wave 0 of the tile
-        if (g == 0) {
+            // outputs and post-processing (nn_speech.c:92-124)
             const int16_t* fin = in + sc * R_STRIDE;
             const NnLayer& LO = img.L[img.nl - 1];
             const int nout = LO.N;
@@ -334,18 +414,23 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
                         for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + f) * 3 + o] = ps.outputs[o];
             }
         }
+        PROBE(1);
         __syncthreads();
+        PROBE(2);
+        cur ^= 1;
     }
-    // ---- state out
-    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RG) {
+#undef PROBE
+    // ---- state out: the last LSTM step (iteration nsteps-1) wrote the buffer that
+    // became cur at iteration nsteps; the tail-only iteration flipped cur once more
+    for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RW) {
         const int st = idx / N, u = idx - st * N;
         if (i0 + st < nrow) {
             const int gs = sid(i0 + st);
-            r.h[(size_t)gs * NN_MAX_W + u] = R.h[hb][st][u];
+            r.h[(size_t)gs * NN_MAX_W + u] = R.h[cur ^ 1][st][u];
             r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
         }
     }
-    if (g == 0 && lane < 16 && valid && b < e) {
+    if (tail && lane < 16 && valid && b < e) {
         ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
@@ -353,35 +438,45 @@ __global__ __launch_bounds__(512) void recur_kernel(NnImage img, FastRun r) {
 
 extern "C" {
 
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units) {
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows) {
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
-    if (which == 0) return (size_t)a_bytes + 768 + (size_t)units * sizeof(ProjWave);
-    return (size_t)a_bytes + 768 + (size_t)units * sizeof(RecTile);
+    const size_t base = (size_t)a_bytes + 768 + ep_bytes(ep_rows);
+    if (which == 0) return base + (size_t)units * sizeof(ProjWave);
+    return base + (size_t)units * sizeof(RecTile);
 }
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4);
+    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n);
     hipLaunchKernelGGL(proj_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, *img, *r);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw);
+    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n);
     const int nrow = r->list ? r->n_list : r->S;
     if (nrow <= 0) return 0;
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
     const int rpw = (img->L[r->li].nrt + RG - 1) / RG;
-    const dim3 grid(blocks), blk(64 * RG * tpw);
+    const dim3 grid(blocks), blk(64 * RW * tpw);
+    const hipStream_t st = (hipStream_t)stream;
+#define LAUNCH(R_)                                                                        \
+    do {                                                                                  \
+        if (img->acc32)                                                                   \
+            hipLaunchKernelGGL((recur_kernel<R_, true>), grid, blk, lds, st, *img, *r);  \
+        else                                                                              \
+            hipLaunchKernelGGL((recur_kernel<R_, false>), grid, blk, lds, st, *img, *r); \
+    } while (0)
     if (rpw <= 2)
-        hipLaunchKernelGGL(recur_kernel<2>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+        LAUNCH(2);
     else if (rpw <= 4)
-        hipLaunchKernelGGL(recur_kernel<4>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+        LAUNCH(4);
     else if (rpw <= 5)
-        hipLaunchKernelGGL(recur_kernel<5>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+        LAUNCH(5);
     else
-        hipLaunchKernelGGL(recur_kernel<8>, grid, blk, lds, (hipStream_t)stream, *img, *r);
+        LAUNCH(8);
+#undef LAUNCH
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -390,9 +485,11 @@ int nnspk_set_lds_limit(void) {
     // allow up to 160 KiB of dynamic LDS for the split kernels
     hipError_t e = hipFuncSetAttribute((const void*)proj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return (int)e;
-    const void* ks[4] = {(const void*)recur_kernel<2>, (const void*)recur_kernel<4>,
-                         (const void*)recur_kernel<5>, (const void*)recur_kernel<8>};
-    for (int i = 0; i < 4; ++i) {
+    const void* ks[8] = {(const void*)recur_kernel<2, false>, (const void*)recur_kernel<4, false>,
+                         (const void*)recur_kernel<5, false>, (const void*)recur_kernel<8, false>,
+                         (const void*)recur_kernel<2, true>,  (const void*)recur_kernel<4, true>,
+                         (const void*)recur_kernel<5, true>,  (const void*)recur_kernel<8, true>};
+    for (int i = 0; i < 8; ++i) {
         e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         if (e != hipSuccess) return (int)e;
     }

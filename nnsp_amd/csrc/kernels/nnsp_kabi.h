@@ -91,6 +91,8 @@ typedef struct {
     const int32_t *list;      /* segments, as FeArgs */
     const int32_t *seg_begin;
     int32_t n_list, seg_len;  /* seg_len as FeArgs */
+    long long *dbg_clk;       /* development probe: [steps][8] s_memtime of tile 0, or NULL */
+    int32_t ep_lo, ep_n;      /* epilogue rows [ep_lo, ep_lo + ep_n) staged into LDS */
 } FastRun;
 
 /* 32-byte device post-processing state, one per stream */
@@ -123,7 +125,7 @@ int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
                             void *stream);
 int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
                             int n, void *stream);
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int waves);
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows);
 int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, void *stream);
 int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, void *stream);
 int nnspk_set_lds_limit(void);

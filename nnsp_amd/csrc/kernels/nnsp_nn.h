@@ -92,8 +92,15 @@ __device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, con
         const int am = argmax_lw(lg, 7);
         if (ps.argmax_last == 0 || ps.argmax_last == am) {
             if (am != 0) {
-                ps.counts[am] = (int16_t)(ps.counts[am] + 1);
-                if (ps.counts[am] > img.th_count) {
+                // counts[am]++ without a runtime register index (keeps ps in VGPRs)
+                int16_t cam = 0;
+#pragma unroll
+                for (int i = 1; i < 7; ++i)
+                    if (i == am) {
+                        ps.counts[i] = (int16_t)(ps.counts[i] + 1);
+                        cam = ps.counts[i];
+                    }
+                if (cam > img.th_count) {
                     ps.trigger = 1;
                     ps.outputs[0] = (int16_t)am;
                     ps.outputs[1] = (int16_t)argmax_lw(lg, 17, 7);
@@ -101,6 +108,7 @@ __device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, con
                 }
             }
         } else {
+#pragma unroll
             for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
         }
         ps.argmax_last = (int16_t)am;

@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""Development probe: per-phase s_memtime clocks of recur_kernel tile 0
+(NNSP_RECUR_CLOCKS=1).  Prints median cycles per phase of a step."""
+import ctypes as C
+import os
+import sys
+
+os.environ["NNSP_RECUR_CLOCKS"] = "1"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from nnsp_amd import _lib  # noqa: E402
+from nnsp_amd.engine import NNSPBatch  # noqa: E402
+
+net = sys.argv[1] if len(sys.argv) > 1 else "vad"
+S = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
+T = 100
+torch.cuda.set_device(0)
+eng = NNSPBatch(net, S, T)
+pcm = torch.empty((S, T, 160), dtype=torch.int16, device="cuda")
+trig = torch.empty((S, T), dtype=torch.int16, device="cuda")
+L = _lib.lib()
+L.nnsp_batch_debug_clocks.argtypes = [C.c_void_p, C.c_void_p]
+L.nnsp_synth_pcm(C.c_void_p(pcm.data_ptr()), S, T, C.c_uint64(1), 0, C.c_int64(0), 4096, C.c_void_p(eng.stream))
+for _ in range(3):
+    eng.exec_device(pcm.data_ptr(), T, trig.data_ptr())
+fe, nn = eng.last_timing()
+clk = np.zeros((64, 8), np.int64)
+_lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clocks")
+st = clk[:51]
+step = np.diff(st[:, 0])
+print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; step cycles median {np.median(step[1:]):.0f}")
+for nm, k0, k1 in (("lstm work", 1, 0), ("lstm wait", 2, 1), ("tail work", 5, 4), ("tail wait", 6, 5)):
+    d = st[1:50, k1] if False else st[1:50, k0] - st[1:50, k1]
+    print(f"  {nm:10s} median {np.median(d):8.0f}  mean {d.mean():8.0f}")
