@@ -17,6 +17,27 @@
 
 #define LDS_MAX (160 * 1024)
 
+/* Which compiled shape of the split kernels fits this net (nnsp_fast.hip):
+ * FC(tanh, 240 -> N) -> LSTM(N) -> FC(relu6, N) -> FC(relu6, N) -> FC(linear). */
+static int net_shape(const NnImage *g)
+{
+    static const int known[3][3] = {{NN_SHAPE_VAD, 28, 2}, {NN_SHAPE_KWS, 64, 2}, {NN_SHAPE_S2I, 72, 41}};
+    if (g->nl != 5 || g->n_lstm != 1) return NN_SHAPE_GENERIC;
+    const NnLayer *L = g->L;
+    if (L[0].type != NN_FC || L[1].type != NN_LSTM || L[2].type != NN_FC || L[3].type != NN_FC ||
+        L[4].type != NN_FC)
+        return NN_SHAPE_GENERIC;
+    if (L[0].K != 240 || L[0].act != 1 /* tanh */ || L[2].act != 0 /* relu6 */ || L[3].act != 0 ||
+        L[4].act != 3 /* linear */)
+        return NN_SHAPE_GENERIC;
+    const int N = L[1].N;
+    if (L[0].N != N || L[1].K != N || L[2].K != N || L[2].N != N || L[3].K != N || L[3].N != N || L[4].K != N)
+        return NN_SHAPE_GENERIC;
+    for (int i = 0; i < 3; ++i)
+        if (N == known[i][1] && L[4].N == known[i][2]) return known[i][0];
+    return NN_SHAPE_GENERIC;
+}
+
 /* Use the split proj/recur kernels when the net has exactly one LSTM layer,
  * every other layer is FC and the staged weights fit in LDS. */
 static void plan_fast(nnsp_batch *b)
@@ -42,6 +63,7 @@ static void plan_fast(nnsp_batch *b)
     const int tiles = (b->S + 15) / 16;
     b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2, b->ep_rec_n) <= LDS_MAX) ? 2 : 1;
     b->li = li;
+    b->shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
     b->nstep_max = (b->Tmax + 1) / 2;
     const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);
     long long blocks = (ptiles + 3) / 4;
@@ -117,8 +139,8 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
         const size_t rows = (size_t)b->im.img.L[b->li].rows;
         if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
         if (getenv("NNSP_RECUR_CLOCKS")) { /* development probe of recur_kernel phases */
-            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 8 * 8))) goto fail;
-            if ((e = nnspk_memset(b->d_clk, 0, 64 * 8 * 8, b->stream))) goto fail;
+            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 16 * 8))) goto fail;
+            if ((e = nnspk_memset(b->d_clk, 0, 64 * 16 * 8, b->stream))) goto fail;
         }
     }
     if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
@@ -219,6 +241,7 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
         f.seg_begin = seg->seg_begin;
         f.seg_len = seg->seg_len;
         f.dbg_clk = b->d_clk;
+        f.shape = b->shape;
         const NnLayer *LL = &b->im.img.L[b->li];
         f.a_off = 0;
         f.a_lds_bytes = (int)LL->ar_off;
@@ -360,7 +383,7 @@ int nnsp_batch_set_state(nnsp_batch *b, const void *host, int first, int count)
 int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
 {
     if (!b || !out || !b->d_clk) return NNSP_EINVAL;
-    TRY(nnspk_d2h(out, b->d_clk, 64 * 8 * 8, b->stream));
+    TRY(nnspk_d2h(out, b->d_clk, 64 * 16 * 8, b->stream));
     return nnspk_sync(b->stream);
 }
 

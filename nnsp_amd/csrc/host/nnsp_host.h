@@ -60,6 +60,7 @@ struct nnsp_batch {
     /* split NN path (one LSTM layer) */
     int fast, li, nstep_max, rec_waves, proj_blocks;
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
+    int shape;                        /* NN_SHAPE_* compiled split-path shape */
     int32_t *d_gx;
     long long *d_clk; /* NNSP_RECUR_CLOCKS development probe */
 };

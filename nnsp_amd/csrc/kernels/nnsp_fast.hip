@@ -14,7 +14,11 @@
 //                  and hidden update (lstm.c:106-115, h after all groups: T6),
 //                  the FC layers after the LSTM, post-processing, triggers.
 // All weights of each kernel are staged once per workgroup into LDS as MFMA
-// A-fragments.
+// A-fragments, with one folded epilogue constant per output row.
+//
+// Both kernels are compiled per net shape (tile counts known at compile time:
+// loops unroll, LDS loads batch, no per-row branches) for the three reference
+// shapes, plus a generic instantiation that reads the shape at run time.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -29,51 +33,71 @@ using namespace nnsp;
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
 #define R_CW 128        // int32 per row of the c buffer
 
-// per-row epilogue constants, staged into LDS (global loads in the per-step
-// epilogue put an L2 round trip on the recurrence's critical path).  bterm is
-// the bias term affine_Krows_8x16 adds before the output shift (affine.c:190-217):
-// b << (qbit_s - qb) (or >>), 64-bit for acc64, wrapping int32 for acc32.
+// ---------------------------------------------------------------------------
+// Net shapes.  NRT == 0: generic (read from the NnLayer table at run time).
+//   NKR   K tiles (64) of the LSTM input and recurrent halves (N <= 128)
+//   NRT   LSTM row tiles (4N rows / 16)
+//   R0    row tiles of the FC layer before the LSTM (K = 240: 4 K tiles)
+//   R1,R2 row tiles of the two relu6 FC layers after the LSTM (K = N)
+//   R3    row tiles of the linear output layer; NW = N, NOUT = its width
+// ---------------------------------------------------------------------------
+template <int NKR_, int NRT_, int R0_, int R1_, int R2_, int R3_, int NW_, int NOUT_>
+struct Shape {
+    static constexpr bool generic = NRT_ == 0;
+    static constexpr int NKR = NKR_, NRT = NRT_, R0 = R0_, R1 = R1_, R2 = R2_, R3 = R3_, NW = NW_, NOUT = NOUT_;
+    static constexpr int RPW = (NRT_ + 3) / 4;
+};
+using ShapeGen = Shape<0, 0, 0, 0, 0, 0, 0, 0>;
+using ShapeVad = Shape<1, 7, 2, 2, 2, 1, 28, 2>;      // def_nn1_vad.c
+using ShapeKws = Shape<1, 16, 4, 4, 4, 1, 64, 2>;     // def_nn2_kws_galaxy.c
+using ShapeS2i = Shape<2, 18, 5, 5, 5, 3, 72, 41>;    // def_nn0_s2i.c
+
+// ---------------------------------------------------------------------------
+// Folded epilogue constants.  affine_Krows_8x16 (affine.c:74-248) computes
+// s = sum_k W x + (b << (qbit_s - qb)), then shift_64b/32b; the MFMA tiles
+// deliver acc = sum_k W (x - 128) exactly, so per row
+//   cst = 128 * sum_k W + bias term        (int64; int32 wrap for acc32)
+// and the layer output is shift(acc + cst).  For the LSTM input half the proj
+// kernel needs the exact sum only (cst = 128 * sum_k Wx, no bias); the recur
+// kernel folds the bias into the recurrent half (cst = 128 * sum_k Wh + bias).
+// ---------------------------------------------------------------------------
 struct EpRow {
-    int32_t wsum, wsum_r;
-    int64_t bterm;
+    int64_t cst;
 };
 
-__device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, int n) {
+__device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, int n, bool recur) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int row = lo + i;
         int li = 0;
         while (li + 1 < img.nl && img.L[li + 1].ep_off <= row) ++li;
         const NnLayer& Ly = img.L[li];
-        const int16_t b = img.bias[row];
+        const bool lstm = Ly.type == NN_LSTM;
         int64_t bt = 0;
-        if (Ly.has_bias) {
+        if (Ly.has_bias && (recur || !lstm)) {
+            const int16_t b = img.bias[row];
             if (img.acc32)
                 bt = Ly.bias_sh >= 0 ? wshl(b, Ly.bias_sh) : ((int32_t)b >> -Ly.bias_sh);
             else
                 bt = Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
         }
-        ep[i] = EpRow{img.wsum[row], img.wsum_r[row], bt};
+        const int32_t w = lstm && recur ? img.wsum_r[row] : img.wsum[row];
+        ep[i].cst = img.acc32 ? (int64_t)wadd(w, (int32_t)bt) : (int64_t)w + bt;
     }
-}
-
-// affine_Krows_8x16 output stage with the bias term already folded in:
-// shift_64b + clamp (acc64) or shift_32b (acc32).  rsh/lsh = the layer's
-// output shift split by sign (lsh > 0 never happens for the reference nets).
-template <bool ACC32>
-__device__ __forceinline__ int32_t ep_shift(int64_t pre, int rsh, int lsh) {
-    if (ACC32) {
-        const int32_t v = (int32_t)pre;
-        return __builtin_expect(lsh > 0, 0) ? shift32(v, lsh) : (v >> rsh);
-    }
-    return sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
 }
 
 __host__ __device__ inline size_t ep_bytes(int n) { return ((size_t)n * sizeof(EpRow) + 15) & ~(size_t)15; }
 
-struct ProjWave {
-    int16_t uni[P_UNION + 32];
-    int16_t act[2][16][P_ASTRIDE];
-};
+// shift_64b + clamp (acc64) or shift_32b (acc32) of acc + cst.  rsh/lsh = the
+// layer's output shift split by sign (lsh > 0 never happens for the reference nets).
+template <bool ACC32>
+__device__ __forceinline__ int32_t ep_out(int32_t acc, int64_t cst, int rsh, int lsh) {
+    if (ACC32) {
+        const int32_t v = wadd(acc, (int32_t)cst);
+        return __builtin_expect(lsh > 0, 0) ? shift32(v, lsh) : (v >> rsh);
+    }
+    const int64_t v = (int64_t)acc + cst;
+    return sat32(__builtin_expect(lsh > 0, 0) ? shift64(v, lsh) : (v >> rsh));
+}
 
 __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, int bytes) {
     const int4* s = reinterpret_cast<const int4*>(src);
@@ -83,40 +107,56 @@ __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, 
 
 // One FC layer on a 16-row tile: B from an LDS buffer (row stride in_stride),
 // A fragments from LDS, output to an LDS buffer (row stride out_stride).
-__device__ __forceinline__ void fc_tile(const NnImage& img, const NnLayer& Ly, const uint8_t* A,
-                                        const EpRow* ep, const int16_t* in, int in_stride, int16_t* out,
-                                        int out_stride, const int16_t* tt, int lane) {
-    v4i bh[4], bl[4];
-    load_b<4>(in, in_stride, Ly.nkt, lane, bh, bl);
+// NRT/NKT/ROWS > 0 and ACT >= 0 are compile-time; otherwise taken from Ly.
+template <bool ACC32, int NRT, int NKT, int ACT, int ROWS, int MAXKT>
+__device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, const EpRow* ep, const int16_t* in,
+                                         int in_stride, int16_t* out, int out_stride, const int16_t* tt, int lane) {
+    const int nrt = NRT > 0 ? NRT : Ly.nrt;
+    const int nkt = NKT > 0 ? NKT : Ly.nkt;
+    const int act = ACT >= 0 ? ACT : Ly.act;
+    const int rows = ROWS > 0 ? ROWS : Ly.rows;
+    const int rsh = Ly.out_sh < 0 ? -Ly.out_sh : 0, lsh = Ly.out_sh > 0 ? Ly.out_sh : 0;
+    v4i bh[MAXKT], bl[MAXKT];
+    load_b<MAXKT>(in, in_stride, nkt, lane, bh, bl);
     const int sc = lane & 15, q = lane >> 4;
-    for (int rt = 0; rt < Ly.nrt; ++rt) {
+    auto tile = [&](int rt) {
         v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
-            if (kt < Ly.nkt) {
-                const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * Ly.nkt + kt) * 1024 + 16 * lane);
+        for (int kt = 0; kt < MAXKT; ++kt)
+            if (kt < nkt) {
+                const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * nkt + kt) * 1024 + 16 * lane);
                 ah = mfma8(w, bh[kt], ah);
                 al = mfma8(w, bl[kt], al);
             }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = 16 * rt + 4 * q + i;
-            if (row >= Ly.rows) continue;
-            const EpRow& er = ep[row];
-            const int32_t sum = (ah[i] << 8) + al[i] + er.wsum;
-            const int32_t v = img.acc32 ? shift32(wadd(sum, (int32_t)er.bterm), Ly.out_sh)
-                                        : sat32(shift64((int64_t)sum + er.bterm, Ly.out_sh));
-            if (Ly.act == ACT_LINEAR)
-                reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
-            else
-                out[sc * out_stride + row] = act16(Ly.act, v, tt);
+            if (row < rows) {
+                const int32_t v = ep_out<ACC32>((ah[i] << 8) + al[i], ep[row].cst, rsh, lsh);
+                if (act == ACT_LINEAR)
+                    reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
+                else
+                    out[sc * out_stride + row] = act16(act, v, tt);
+            }
         }
+    };
+    if constexpr (NRT > 0) {
+#pragma unroll
+        for (int rt = 0; rt < NRT; ++rt) tile(rt);
+    } else {
+        for (int rt = 0; rt < nrt; ++rt) tile(rt);
     }
 }
 
 // ---------------------------------------------------------------------------
 // proj_kernel
 // ---------------------------------------------------------------------------
+struct ProjWave {
+    int16_t uni[P_UNION + 32];
+    int16_t act[2][16][P_ASTRIDE];
+};
+
+template <class SH, bool ACC32>
 __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
@@ -124,18 +164,21 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
     ProjWave* pw = reinterpret_cast<ProjWave*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
-    stage_ep(ep, img, r.ep_lo, r.ep_n);
+    stage_ep(ep, img, r.ep_lo, r.ep_n, false);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     __syncthreads();
+    constexpr bool GEN = SH::generic;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     ProjWave& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
     const NnLayer& LL = img.L[r.li];
+    const int nrt = GEN ? LL.nrt : SH::NRT;
+    const int nkt = GEN ? LL.nkt : SH::NKR;
+    const int rows = 16 * nrt;   // LSTM rows are padded to whole tiles (4 units per group)
     const int wsteps = r.seg_len > 0 ? min(r.nstep_max, (r.seg_len + 1) / 2) : r.nstep_max;
     const int ntps = (wsteps + 15) / 16;
     const int nrow = r.list ? r.n_list : r.S;
     const long long ntiles = (long long)nrow * ntps;
-    const int rows = LL.rows;
     for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
          tile += (long long)gridDim.x * (blockDim.x >> 6)) {
         const int i_row = (int)(tile / ntps), j0 = 16 * (int)(tile - (long long)i_row * ntps);
@@ -159,39 +202,55 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
         // ---- prefix FC layers (row p's context = uni[80p .. 80p+239])
         const int16_t* in = P.uni;
         int in_stride = 80;
-        for (int i = 0; i < r.li; ++i) {
-            const NnLayer& Ly = img.L[i];
-            int16_t* out = &P.act[i & 1][0][0];
-            fc_tile(img, Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in, in_stride, out, P_ASTRIDE,
-                    tt, lane);
+        if (!GEN) {   // one tanh FC layer, K = 240
+            const NnLayer& L0 = img.L[0];
+            fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
+                                                          in, in_stride, &P.act[0][0][0], P_ASTRIDE, tt, lane);
             wave_lds_sync();
-            in = out;
+            in = &P.act[0][0][0];
             in_stride = P_ASTRIDE;
+        } else {
+            for (int i = 0; i < r.li; ++i) {
+                const NnLayer& Ly = img.L[i];
+                int16_t* out = &P.act[i & 1][0][0];
+                fc_layer<ACC32, 0, 0, -1, 0, 4>(Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in,
+                                                in_stride, out, P_ASTRIDE, tt, lane);
+                wave_lds_sync();
+                in = out;
+                in_stride = P_ASTRIDE;
+            }
         }
         // ---- LSTM input half: gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
         {
-            v4i bh[4], bl[4];
-            load_b<4>(in, in_stride, LL.nkt, lane, bh, bl);
+            v4i bh[2], bl[2];
+            load_b<2>(in, in_stride, nkt, lane, bh, bl);
             const uint8_t* A = W + (LL.a_off - r.a_off);
+            const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
             const int j = j0 + sc;
             const bool act = j < r.nstep_max && 2 * j + phase < L;
             int32_t* dst = r.gx + ((size_t)s * r.nstep_max + j) * rows + 4 * q;
-            for (int rt = 0; rt < LL.nrt; ++rt) {
+            auto tile = [&](int rt) {
                 v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
-                for (int kt = 0; kt < 4; ++kt)
-                    if (kt < LL.nkt) {
-                        const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * LL.nkt + kt) * 1024 + 16 * lane);
+                for (int kt = 0; kt < 2; ++kt)
+                    if (kt < nkt) {
+                        const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * nkt + kt) * 1024 + 16 * lane);
                         ah = mfma8(w, bh[kt], ah);
                         al = mfma8(w, bl[kt], al);
                     }
-                const EpRow* er = ep + (LL.ep_off - r.ep_lo) + 16 * rt + 4 * q;
+                const EpRow* er = epl + 16 * rt;
                 int4 o;
-                o.x = (ah[0] << 8) + al[0] + er[0].wsum;
-                o.y = (ah[1] << 8) + al[1] + er[1].wsum;
-                o.z = (ah[2] << 8) + al[2] + er[2].wsum;
-                o.w = (ah[3] << 8) + al[3] + er[3].wsum;
+                o.x = (ah[0] << 8) + al[0] + (int32_t)er[0].cst;
+                o.y = (ah[1] << 8) + al[1] + (int32_t)er[1].cst;
+                o.z = (ah[2] << 8) + al[2] + (int32_t)er[2].cst;
+                o.w = (ah[3] << 8) + al[3] + (int32_t)er[3].cst;
                 if (act) *reinterpret_cast<int4*>(dst + 16 * rt) = o;
+            };
+            if constexpr (!GEN) {
+#pragma unroll
+                for (int rt = 0; rt < SH::NRT; ++rt) tile(rt);
+            } else {
+                for (int rt = 0; rt < nrt; ++rt) tile(rt);
             }
         }
         wave_lds_sync();
@@ -224,15 +283,23 @@ struct RecTile {
     int32_t end[16];    // segment end frame (exclusive)
 };
 
-template <int RPW, bool ACC32>   // RPW: LSTM row tiles per wave = ceil(nrt / RG)
+// logits of one stream held in registers (post-processing without LDS round trips)
+template <int N>
+struct RegLogits {
+    int32_t v[N];
+    __device__ __forceinline__ int32_t operator[](int i) const { return v[i]; }
+};
+
+template <class SH, int RPW, bool ACC32>   // RPW: LSTM row tiles per wave = ceil(nrt / RG)
 __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr bool GEN = SH::generic;
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
     RecTile* tiles = reinterpret_cast<RecTile*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
-    stage_ep(ep, img, r.ep_lo, r.ep_n);
+    stage_ep(ep, img, r.ep_lo, r.ep_n, true);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tpw = blockDim.x / (64 * RW);
@@ -247,7 +314,10 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     const bool valid = i0 + sc < nrow;
     const int s = valid ? sid(i0 + sc) : 0;
     const NnLayer& LL = img.L[r.li];
-    const int N = LL.N, rows = LL.rows, nrt = LL.nrt, nkt_r = LL.nkt_r;
+    const int N = GEN ? LL.N : SH::NW;
+    const int nrt = GEN ? LL.nrt : SH::NRT;
+    const int nkt_r = GEN ? LL.nkt_r : SH::NKR;
+    const int rows = 16 * nrt;
     const int xs_sh = LL.xs_sh, rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
     for (int idx = g * 64 + lane; idx < 16 * N; idx += 64 * RW) {
         const int st = idx / N, u = idx - st * N;
@@ -281,7 +351,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
             for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
     }
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
-    const EpRow* epl = ep + (LL.ep_off - r.ep_lo);
+    const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
     v4i gxv[RPW];
     auto load_gx = [&](int jj) {
         const bool ok = valid && b + 2 * jj + phase < e;
@@ -293,10 +363,10 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
         }
     };
     if (!tail) load_gx(0);
-    long long* clk = (r.dbg_clk && blockIdx.x == 0 && tl == 0 && (g == 0 || tail)) ? r.dbg_clk + (tail ? 4 : 0)
+    long long* clk = (r.dbg_clk && blockIdx.x == 0 && tl == 0 && (g == 0 || tail)) ? r.dbg_clk + (tail ? 8 : 0)
                                                                                      : nullptr;
 #define PROBE(k) \
-    if (clk && j < 64) clk[j * 8 + (k)] = (long long)__builtin_amdgcn_s_memtime()
+    if (clk && j < 64) clk[j * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime()
     int cur = 0;
     for (int j = 0; j <= nsteps; ++j) {
         PROBE(0);
@@ -321,22 +391,22 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                             }
                         const int u = 4 * rt + q;
                         if (u < N) {
+                            const EpRow* er = epl + 16 * rt;
                             int16_t gt[4];
 #pragma unroll
                             for (int i = 0; i < 4; ++i) {
-                                const EpRow& er = epl[16 * rt + 4 * q + i];
                                 const int32_t sx = gxv[k][i];
-                                const int32_t sh = (hh[i] << 8) + hl[i] + er.wsum_r;
-                                int64_t pre;
+                                const int32_t hx = (hh[i] << 8) + hl[i];
+                                int32_t v;
                                 if (ACC32) {
                                     const int32_t x = __builtin_expect(xs_sh != 0, 0) ? shift32(sx, xs_sh) : sx;
-                                    pre = wadd(wadd(x, sh), (int32_t)er.bterm);
+                                    v = ep_out<true>(wadd(x, hx), er[i].cst, rsh, lsh);
                                 } else {
                                     const int64_t x = __builtin_expect(xs_sh != 0, 0) ? shift64((int64_t)sx, xs_sh)
                                                                                       : (int64_t)sx;
-                                    pre = x + sh + er.bterm;
+                                    const int64_t pre = x + hx + er[i].cst;
+                                    v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                                 }
-                                const int32_t v = ep_shift<ACC32>(pre, rsh, lsh);
                                 gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
                             }
                             const int32_t c_old = R.c[sc][u];
@@ -355,56 +425,59 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
             const int t = b + 2 * jj + phase;
             const bool active = valid && t < e;
             const int16_t* in = &R.h[cur][0][0];
-            int ab = 0;
-            for (int i = r.li + 1; i < img.nl; ++i) {
-                const NnLayer& Ly = img.L[i];
-                const uint8_t* A = W + (Ly.a_off - r.a_off);
-                const EpRow* epi = ep + (Ly.ep_off - r.ep_lo);
-                const int nkt = Ly.nkt, lrt = Ly.nrt, lrows = Ly.rows, act = Ly.act;
-                const int ors = Ly.out_sh < 0 ? -Ly.out_sh : 0, ols = Ly.out_sh > 0 ? Ly.out_sh : 0;
-                int16_t* out = &R.act[ab][0][0];
-                v4i fh[2], fl[2];
-                load_b<2>(in, R_STRIDE, nkt, lane, fh, fl);
-                for (int rt = 0; rt < lrt; ++rt) {
-                    v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
-#pragma unroll
-                    for (int kt = 0; kt < 2; ++kt)
-                        if (kt < nkt) {
-                            const v4i w = *reinterpret_cast<const v4i*>(A + (size_t)(rt * nkt + kt) * 1024 + 16 * lane);
-                            ah = mfma8(w, fh[kt], ah);
-                            al = mfma8(w, fl[kt], al);
-                        }
-#pragma unroll
-                    for (int x = 0; x < 4; ++x) {
-                        const int row = 16 * rt + 4 * q + x;
-                        if (row >= lrows) continue;
-                        const EpRow& er = epi[row];
-                        const int32_t sum = (ah[x] << 8) + al[x] + er.wsum;
-                        const int64_t pre = ACC32 ? (int64_t)wadd(sum, (int32_t)er.bterm) : (int64_t)sum + er.bterm;
-                        const int32_t v = ep_shift<ACC32>(pre, ors, ols);
-                        if (act == ACT_LINEAR)
-                            reinterpret_cast<int32_t*>(out + sc * R_STRIDE)[row] = v;
-                        else
-                            out[sc * R_STRIDE + row] = act16(act, v, tt);
-                    }
-                }
+            if (!GEN) {   // relu6 (N), relu6 (N), linear (NOUT) -- def_nn*.c layers 2..4
+                const NnLayer& L2 = img.L[r.li + 1];
+                const NnLayer& L3 = img.L[r.li + 2];
+                const NnLayer& L4 = img.L[r.li + 3];
+                fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, 2>(
+                    L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), in, R_STRIDE, &R.act[0][0][0],
+                    R_STRIDE, tt, lane);
                 wave_lds_sync();
-                in = out;
-                ab ^= 1;
+                PROBE(3);
+                fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, 2>(
+                    L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.act[0][0][0], R_STRIDE,
+                    &R.act[1][0][0], R_STRIDE, tt, lane);
+                wave_lds_sync();
+                PROBE(4);
+                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, 2>(
+                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.act[1][0][0], R_STRIDE,
+                    &R.act[0][0][0], R_STRIDE, tt, lane);
+                wave_lds_sync();
+                PROBE(5);
+                in = &R.act[0][0][0];
+            } else {
+                int ab = 0;
+                for (int i = r.li + 1; i < img.nl; ++i) {
+                    const NnLayer& Ly = img.L[i];
+                    int16_t* out = &R.act[ab][0][0];
+                    fc_layer<ACC32, 0, 0, -1, 0, 2>(Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in,
+                                                    R_STRIDE, out, R_STRIDE, tt, lane);
+                    wave_lds_sync();
+                    in = out;
+                    ab ^= 1;
+                }
             }
             // outputs and post-processing (nn_speech.c:92-124)
             const int16_t* fin = in + sc * R_STRIDE;
             const NnLayer& LO = img.L[img.nl - 1];
-            const int nout = LO.N;
-            const bool lin = LO.act == ACT_LINEAR;
+            const int nout = GEN ? LO.N : SH::NOUT;
+            const bool lin = GEN ? LO.act == ACT_LINEAR : true;
             if (active && r.logits) {
                 int32_t* dst = r.logits + ((size_t)s * T + t) * nout;
                 for (int o = q; o < nout; o += 4)
                     dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
             }
             if (lane < 16 && active) {
-                const LogitRow lg = {fin, lin};
-                post_proc(ps, img, lg);
+                if (GEN) {
+                    const LogitRow lg = {fin, lin};
+                    post_proc(ps, img, lg);
+                } else {
+                    RegLogits<SH::NOUT> lg;
+                    const int32_t* f32 = reinterpret_cast<const int32_t*>(fin);
+#pragma unroll
+                    for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
+                    post_proc(ps, img, lg);
+                }
                 if (r.trig) {
                     r.trig[(size_t)s * T + t] = ps.trigger;
                     if (t + 1 < e) r.trig[(size_t)s * T + t + 1] = ps.trigger;
@@ -436,6 +509,52 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     }
 }
 
+// ---------------------------------------------------------------------------
+// launch layer
+// ---------------------------------------------------------------------------
+namespace {
+
+template <class SH>
+const void* proj_fn(bool acc32) {
+    return acc32 ? (const void*)proj_kernel<SH, true> : (const void*)proj_kernel<SH, false>;
+}
+
+template <class SH, int RPW>
+const void* recur_fn(bool acc32) {
+    return acc32 ? (const void*)recur_kernel<SH, RPW, true> : (const void*)recur_kernel<SH, RPW, false>;
+}
+
+const void* pick_proj(int shape, bool acc32) {
+    switch (shape) {
+        case NN_SHAPE_VAD: return proj_fn<ShapeVad>(acc32);
+        case NN_SHAPE_KWS: return proj_fn<ShapeKws>(acc32);
+        case NN_SHAPE_S2I: return proj_fn<ShapeS2i>(acc32);
+        default: return proj_fn<ShapeGen>(acc32);
+    }
+}
+
+const void* pick_recur(int shape, int nrt, bool acc32) {
+    switch (shape) {
+        case NN_SHAPE_VAD: return recur_fn<ShapeVad, ShapeVad::RPW>(acc32);
+        case NN_SHAPE_KWS: return recur_fn<ShapeKws, ShapeKws::RPW>(acc32);
+        case NN_SHAPE_S2I: return recur_fn<ShapeS2i, ShapeS2i::RPW>(acc32);
+        default: break;
+    }
+    const int rpw = (nrt + RG - 1) / RG;
+    if (rpw <= 2) return recur_fn<ShapeGen, 2>(acc32);
+    if (rpw <= 4) return recur_fn<ShapeGen, 4>(acc32);
+    if (rpw <= 5) return recur_fn<ShapeGen, 5>(acc32);
+    return recur_fn<ShapeGen, 8>(acc32);
+}
+
+int launch(const void* fn, dim3 grid, dim3 blk, size_t lds, void* stream, const NnImage* img, const FastRun* r) {
+    void* args[2] = {(void*)img, (void*)r};
+    hipError_t e = hipLaunchKernel(fn, grid, blk, args, lds, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
 extern "C" {
 
 size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows) {
@@ -447,9 +566,7 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows) {
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n);
-    hipLaunchKernelGGL(proj_kernel, dim3(blocks), dim3(256), lds, (hipStream_t)stream, *img, *r);
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
+    return launch(pick_proj(r->shape, img->acc32), dim3(blocks), dim3(256), lds, stream, img, r);
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
@@ -458,41 +575,23 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stre
     if (nrow <= 0) return 0;
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
-    const int rpw = (img->L[r->li].nrt + RG - 1) / RG;
-    const dim3 grid(blocks), blk(64 * RW * tpw);
-    const hipStream_t st = (hipStream_t)stream;
-#define LAUNCH(R_)                                                                        \
-    do {                                                                                  \
-        if (img->acc32)                                                                   \
-            hipLaunchKernelGGL((recur_kernel<R_, true>), grid, blk, lds, st, *img, *r);  \
-        else                                                                              \
-            hipLaunchKernelGGL((recur_kernel<R_, false>), grid, blk, lds, st, *img, *r); \
-    } while (0)
-    if (rpw <= 2)
-        LAUNCH(2);
-    else if (rpw <= 4)
-        LAUNCH(4);
-    else if (rpw <= 5)
-        LAUNCH(5);
-    else
-        LAUNCH(8);
-#undef LAUNCH
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
+    return launch(pick_recur(r->shape, img->L[r->li].nrt, img->acc32), dim3(blocks), dim3(64 * RW * tpw), lds,
+                  stream, img, r);
 }
 
 int nnspk_set_lds_limit(void) {
-    // allow up to 160 KiB of dynamic LDS for the split kernels
-    hipError_t e = hipFuncSetAttribute((const void*)proj_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return (int)e;
-    const void* ks[8] = {(const void*)recur_kernel<2, false>, (const void*)recur_kernel<4, false>,
-                         (const void*)recur_kernel<5, false>, (const void*)recur_kernel<8, false>,
-                         (const void*)recur_kernel<2, true>,  (const void*)recur_kernel<4, true>,
-                         (const void*)recur_kernel<5, true>,  (const void*)recur_kernel<8, true>};
-    for (int i = 0; i < 8; ++i) {
-        e = hipFuncSetAttribute(ks[i], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        if (e != hipSuccess) return (int)e;
-    }
+    // allow up to 160 KiB of dynamic LDS for every split-path instantiation
+    const int shapes[4] = {NN_SHAPE_GENERIC, NN_SHAPE_VAD, NN_SHAPE_KWS, NN_SHAPE_S2I};
+    const int nrts[4] = {8, 16, 20, 32};   // one generic recur instantiation each
+    for (int a = 0; a < 2; ++a)
+        for (int i = 0; i < 4; ++i) {
+            const void* fns[3] = {pick_proj(shapes[i], a), pick_recur(shapes[i], nrts[i], a),
+                                  pick_recur(NN_SHAPE_GENERIC, nrts[i], a)};
+            for (int k = 0; k < 3; ++k) {
+                hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                if (e != hipSuccess) return (int)e;
+            }
+        }
     return 0;
 }
 

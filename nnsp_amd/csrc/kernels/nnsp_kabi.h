@@ -16,6 +16,12 @@ extern "C" {
 #define NN_MAX_OUT 64   /* width of the last layer */
 #define NN_FC 0
 #define NN_LSTM 1
+/* compiled shapes of the split NN path (nnsp_fast.hip): FC(tanh, K 240) ->
+ * LSTM(N) -> FC(relu6, N) -> FC(relu6, N) -> FC(linear, NOUT) */
+#define NN_SHAPE_GENERIC 0
+#define NN_SHAPE_VAD 1 /* N 28, NOUT 2  (def_nn1_vad.c) */
+#define NN_SHAPE_KWS 2 /* N 64, NOUT 2  (def_nn2_kws_galaxy.c) */
+#define NN_SHAPE_S2I 3 /* N 72, NOUT 41 (def_nn0_s2i.c) */
 #define NN_MODE_STREAM 0 /* NNSPClass_exec over a chunk: FE features in, post-proc */
 #define NN_MODE_DIRECT 1 /* NeuralNetClass_exe: 240-wide input in, raw output */
 
@@ -93,6 +99,7 @@ typedef struct {
     int32_t n_list, seg_len;  /* seg_len as FeArgs */
     long long *dbg_clk;       /* development probe: [steps][8] s_memtime of tile 0, or NULL */
     int32_t ep_lo, ep_n;      /* epilogue rows [ep_lo, ep_lo + ep_n) staged into LDS */
+    int32_t shape, pad3;      /* NN_SHAPE_* */
 } FastRun;
 
 /* 32-byte device post-processing state, one per stream */

@@ -26,11 +26,12 @@ L.nnsp_synth_pcm(C.c_void_p(pcm.data_ptr()), S, T, C.c_uint64(1), 0, C.c_int64(0
 for _ in range(3):
     eng.exec_device(pcm.data_ptr(), T, trig.data_ptr())
 fe, nn = eng.last_timing()
-clk = np.zeros((64, 8), np.int64)
+clk = np.zeros((64, 16), np.int64)
 _lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clocks")
 st = clk[:51]
 step = np.diff(st[:, 0])
 print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; step cycles median {np.median(step[1:]):.0f}")
-for nm, k0, k1 in (("lstm work", 1, 0), ("lstm wait", 2, 1), ("tail work", 5, 4), ("tail wait", 6, 5)):
-    d = st[1:50, k1] if False else st[1:50, k0] - st[1:50, k1]
+for nm, k0, k1 in (("lstm work", 1, 0), ("lstm wait", 2, 1), ("tail fc1", 12, 8), ("tail fc2", 13, 12),
+                   ("tail fc3", 14, 13), ("tail post", 9, 14), ("tail wait", 10, 9)):
+    d = st[1:50, k0] - st[1:50, k1]
     print(f"  {nm:10s} median {np.median(d):8.0f}  mean {d.mean():8.0f}")

@@ -48,14 +48,17 @@ def _compare(name, acc32, S, chunks, seed=3):
 
 @pytest.mark.parametrize("name", NETS)
 @pytest.mark.parametrize("acc32", [False, True])
-@pytest.mark.parametrize("path", ["split", "fused"])
+@pytest.mark.parametrize("path", ["split", "generic", "fused"])
 def test_batch_matches_oracle(name, acc32, path, monkeypatch):
-    # split = proj_kernel + recur_kernel (default for one-LSTM nets);
+    # split = proj_kernel + recur_kernel compiled for the net's shape (default);
+    # generic = the same kernels reading the shape at run time;
     # fused = the general per-step nn_kernel (any fc/lstm stack)
+    monkeypatch.delenv("NNSP_FUSED_NN", raising=False)
+    monkeypatch.delenv("NNSP_GENERIC_SHAPE", raising=False)
     if path == "fused":
         monkeypatch.setenv("NNSP_FUSED_NN", "1")
-    else:
-        monkeypatch.delenv("NNSP_FUSED_NN", raising=False)
+    elif path == "generic":
+        monkeypatch.setenv("NNSP_GENERIC_SHAPE", "1")
     _compare(name, acc32, S=37, chunks=[24, 7, 1, 10])
 
 
