@@ -26,6 +26,15 @@ __device__ __forceinline__ int16_t sat16(int64_t v) {
 // (int32)(((int64)a*b) >> 32): v_mul_hi_i32
 __device__ __forceinline__ int32_t mulhi(int32_t a, int32_t b) { return __mulhi(a, b); }
 
+// acc + (int64)a*b as one v_mad_i64_i32 (the compiler otherwise hoists the
+// sign extensions of loop-invariant operands and emits a 64x64 multiply)
+__device__ __forceinline__ int64_t mad_i64_i32(int32_t a, int32_t b, int64_t acc) {
+    int64_t r;
+    uint64_t carry;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(a), "v"(b), "v"(acc));
+    return r;
+}
+
 // SMMLAR / SMMULR contribution: floor((x*c + 2^31) / 2^32)
 __device__ __forceinline__ int32_t rnd_add(int32_t x, int32_t c) {
     return (int32_t)(((int64_t)x * c + 0x80000000LL) >> 32);

@@ -22,52 +22,58 @@ using namespace nnsp;
 // ============================================================================
 // Front end
 // ============================================================================
-// LDS image of one frame: 256 complex q31, with a 32-dword pad after every
-// 64 complex so the stage-2 access pattern (i0 = 64b + j) is conflict-free.
-#define FE_SEG 160   // dwords per 64-complex segment (128 data + 32 pad)
-#define FE_FRAME_DW (4 * FE_SEG)
-__device__ __forceinline__ int cidx(int c) { return 2 * c + 32 * (c >> 6); }
+// One wave64 per frame.  The 256-point complex cFFT (arm_radix4_butterfly_q31,
+// radix-4 DIF) keeps one butterfly per lane and stage with its four complex
+// operands in registers.  Writing a position as c = 64*d3 + 16*d2 + 4*d1 + d0
+// (base-4 digits), stage s butterflies over digit d(4-s); register index m is
+// that digit and the lane index holds the other three:
+//   stage 1  lane = 16*d2 + 4*d1 + d0, m = d3  (loaded straight from the PCM)
+//   stage 2  lane = 16*d3 + 4*d1 + d0, m = d2  (T1: m <-> lane bits 4-5, permlane swaps)
+//   stage 3  lane = 16*d0 + 4*d3 + d2, m = d1  (T2: through LDS)
+//   stage 4  lane = 16*d1 + 4*d3 + d2, m = d0  (T3: permlane swaps)
+// The stage-4 outputs go to LDS at their natural bin k = rev8(c) (CMSIS's
+// bit reversal), where the split reads bins k and 256-k.  LDS slots are
+// swizzled (zslot) so that every one of these accesses is bank-conflict-free.
+#define FE_X_DW 512   // dwords of one frame's complex buffer (256 complex)
+__device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
 
 struct FeLane {
-    uint32_t win[4];      // window taps 8*lane .. 8*lane+7 as int16 pairs (0 past lane 59)
+    uint32_t win[4];      // window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
     uint32_t mc[6];       // Mel segment coefficients as int16 pairs
-    int rk[4], rn[4];     // bit-reversed slots of bins k and 256-k, k = lane + 64m
     int mj0, mfirst, mcnt;
 };
 
 // Block-shared constant tables (LDS).
 struct FeTables {
-    int32_t tw[384];      // twiddleCoef_256_q31: (cos, sin) pairs
+    int2 tw[3][3][64];    // per stage, twiddle (k, 2k, 3k) of each lane's butterfly: (cos, sin)
     int4 split[256];      // per bin k: (A_re, A_im, B_re, 0) of realCoefA/BQ31 at 16k
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
 };
 
 __device__ __forceinline__ void fe_tables_init(FeTables& T) {
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) T.tw[i] = nnsp_tbl_tw256[i];
+    for (int i = threadIdx.x; i < 576; i += blockDim.x) {
+        const int s = i / 192, j = (i / 64) % 3, l = i % 64;
+        const int k = s == 0 ? l : (s == 1 ? 4 * (l & 15) : 16 * (l >> 4));
+        T.tw[s][j][l] = make_int2(nnsp_tbl_tw256[2 * (j + 1) * k], nnsp_tbl_tw256[2 * (j + 1) * k + 1]);
+    }
     for (int k = threadIdx.x; k < 256; k += blockDim.x)
         T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
 }
 
-__device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int k) {
+__device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int s, int lane) {
     Tw3 t;
-    const int2 a = *reinterpret_cast<const int2*>(&T.tw[2 * k]);
-    const int2 b = *reinterpret_cast<const int2*>(&T.tw[4 * k]);
-    const int2 c = *reinterpret_cast<const int2*>(&T.tw[6 * k]);
+    const int2 a = T.tw[s][0][lane], b = T.tw[s][1][lane], c = T.tw[s][2][lane];
     t.c1 = a.x; t.s1 = a.y; t.c2 = b.x; t.s2 = b.y; t.c3 = c.x; t.s3 = c.y;
     return t;
 }
 
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
-    for (int j = 0; j < 4; ++j)
-        L.win[j] = lane < 60 ? ((uint32_t)(uint16_t)nnsp_tbl_window[8 * lane + 2 * j] |
-                                ((uint32_t)(uint16_t)nnsp_tbl_window[8 * lane + 2 * j + 1] << 16))
-                             : 0u;
     for (int m = 0; m < 4; ++m) {
-        const int k = lane + 64 * m;
-        L.rk[m] = rev8(k);
-        L.rn[m] = rev8((256 - k) & 255);
+        const int i = 128 * m + 2 * lane;
+        L.win[m] = i < 480 ? ((uint32_t)(uint16_t)nnsp_tbl_window[i] | ((uint32_t)(uint16_t)nnsp_tbl_window[i + 1] << 16))
+                           : 0u;
     }
     const int* sg = nnsp_tbl_melseg + 4 * lane;
     L.mj0 = sg[1];
@@ -101,86 +107,83 @@ __device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp
     return wadd(v, 0x2688 * -sh);
 }
 
-// In-place radix-4 cFFT (arm_radix4_butterfly_q31) of one frame held in LDS.
-__device__ __forceinline__ void wave_cfft256(int32_t* X, const FeTables& TB, int lane) {
-    // stage 1: butterfly i0 = lane, stride 64
-    {
-        int32_t v[8];
+// 4x4 transpose of the register index m with the lane's row (lane bits 4-5):
+// v[2m], v[2m+1] = (re, im) of register m.  permlane32_swap exchanges the
+// upper half of its first operand with the lower half of its second,
+// permlane16_swap the odd rows of the first with the even rows of the second.
+__device__ __forceinline__ void xpose_rows(int32_t (&v)[8]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+        auto a = __builtin_amdgcn_permlane32_swap((unsigned)v[0 + p], (unsigned)v[4 + p], false, false);
+        auto b = __builtin_amdgcn_permlane32_swap((unsigned)v[2 + p], (unsigned)v[6 + p], false, false);
+        auto c = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        auto d = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        v[0 + p] = (int32_t)c[0]; v[2 + p] = (int32_t)c[1];
+        v[4 + p] = (int32_t)d[0]; v[6 + p] = (int32_t)d[1];
+    }
+}
+
+// cFFT (arm_radix4_butterfly_q31) of one frame held in v in the stage-1
+// layout; leaves the output in X at natural bin order (arm_bitreversal_32).
+__device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const FeTables& TB, int lane) {
+    bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 0, lane));
+    xpose_rows(v);
+    bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 1, lane));
+    {   // T2: stage-2 layout out, stage-3 layout in
+        const int cw = 64 * (lane >> 4) + (lane & 15);
+#pragma unroll
+        for (int m = 0; m < 4; ++m)
+            *reinterpret_cast<int2*>(X + 2 * zslot(cw + 16 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
+        wave_lds_sync();
+        const int cr = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + (lane >> 4);
+#pragma unroll
         for (int m = 0; m < 4; ++m) {
-            const int2 p = *reinterpret_cast<const int2*>(X + cidx(lane + 64 * m));
+            const int2 p = *reinterpret_cast<const int2*>(X + 2 * zslot(cr + 4 * m));
             v[2 * m] = p.x; v[2 * m + 1] = p.y;
         }
-        bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, lane));
-        for (int m = 0; m < 4; ++m)
-            *reinterpret_cast<int2*>(X + cidx(lane + 64 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
     }
+    bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 2, lane));
+    xpose_rows(v);
+    bfly4_last(v);
     wave_lds_sync();
-    // stage 2: i0 = 64*(lane>>4) + (lane&15), stride 16
-    {
-        const int i0 = 64 * (lane >> 4) + (lane & 15);
-        int32_t v[8];
-        for (int m = 0; m < 4; ++m) {
-            const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 16 * m));
-            v[2 * m] = p.x; v[2 * m + 1] = p.y;
-        }
-        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 4 * (lane & 15)));
+    {   // register m is DIF position 64*d3 + 16*d2 + 4*d1 + m; its bin is rev8 of that
+        const int c = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + 4 * (lane >> 4);
+#pragma unroll
         for (int m = 0; m < 4; ++m)
-            *reinterpret_cast<int2*>(X + cidx(i0 + 16 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
-    }
-    wave_lds_sync();
-    // stage 3: i0 = 16*(lane>>2) + (lane&3), stride 4
-    {
-        const int i0 = 16 * (lane >> 2) + (lane & 3);
-        int32_t v[8];
-        for (int m = 0; m < 4; ++m) {
-            const int2 p = *reinterpret_cast<const int2*>(X + cidx(i0 + 4 * m));
-            v[2 * m] = p.x; v[2 * m + 1] = p.y;
-        }
-        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 16 * (lane & 3)));
-        for (int m = 0; m < 4; ++m)
-            *reinterpret_cast<int2*>(X + cidx(i0 + 4 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
-    }
-    wave_lds_sync();
-    // last stage: complex 4*lane .. 4*lane+3 (contiguous inside a segment)
-    {
-        int32_t* q = X + cidx(4 * lane);
-        int32_t v[8];
-        const int4 a = *reinterpret_cast<const int4*>(q);
-        const int4 b = *reinterpret_cast<const int4*>(q + 4);
-        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
-        bfly4_last(v);
-        *reinterpret_cast<int4*>(q) = make_int4(v[0], v[1], v[2], v[3]);
-        *reinterpret_cast<int4*>(q + 4) = make_int4(v[4], v[5], v[6], v[7]);
+            *reinterpret_cast<int2*>(X + 2 * zslot(rev8(c + m))) = make_int2(v[2 * m], v[2 * m + 1]);
     }
     wave_lds_sync();
 }
 
-// Split of bin k = lane + 64m from the (not yet bit-reversed) cFFT output Y.
+// Split of bin k = lane + 64m from the natural-order cFFT output in X.
 // (k = 0 yields a don't-care value; DC / Nyquist come from wave_split_dc.)
-__device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeLane& L, const FeTables& TB,
-                                               int lane, int m, int32_t& re, int32_t& im) {
-    const int4 cf = TB.split[lane + 64 * m];
-    const int2 zk = *reinterpret_cast<const int2*>(X + cidx(L.rk[m]));
-    const int2 zn = *reinterpret_cast<const int2*>(X + cidx(L.rn[m]));
+__device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeTables& TB, int lane, int m,
+                                               int32_t& re, int32_t& im) {
+    const int k = lane + 64 * m;
+    const int4 cf = TB.split[k];
+    const int2 zk = *reinterpret_cast<const int2*>(X + 2 * zslot(k));
+    const int2 zn = *reinterpret_cast<const int2*>(X + 2 * zslot((256 - k) & 255));
     split_bin(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re, im);
 }
 
 // DC and Nyquist bins: (p0 + p1) >> 1, (p0 - p1) >> 1 (arm_split_rfft_q31 tail)
 __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int32_t& nyq) {
-    const int2 z0 = *reinterpret_cast<const int2*>(X + cidx(0));
+    const int2 z0 = *reinterpret_cast<const int2*>(X);
     dc = wadd(z0.x, z0.y) >> 1;
     nyq = wsub(z0.x, z0.y) >> 1;
 }
 
-// One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.
-// 'buf' supplies the 480 samples (frames t-2, t-1, t) in 8-sample chunks.
+// One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.  Each wave
+// runs a contiguous range of frames (consecutive frames of a stream re-read
+// two thirds of their window from L1/L2) and prefetches the next frame's PCM.
 __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
-    __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_FRAME_DW];
+    __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
     __shared__ int64_t Ms[4][64];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     fe_tables_init(TB);
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = Xs[wv];
     int32_t* P = Ps[wv];
     int64_t* Mp = Ms[wv];
@@ -192,62 +195,72 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     const unsigned nrow = a.list ? (unsigned)a.n_list : (unsigned)a.S;
     const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
-    const unsigned stride = gridDim.x * 4u;
-    // frame f = (row, k): stream s, segment start b, t = b + k (valid below T);
-    // lane (< 60) loads 16-byte chunk 'lane' of the 480-sample window (input
-    // frames t-2..t; before b: the tail)
-    auto frame_of = [&](unsigned f, int& s, int& t, int& b) {
-        const unsigned i = f / W;
-        s = a.list ? a.list[i] : (int)i;
-        b = a.seg_begin ? a.seg_begin[s] : 0;
-        t = b + (int)(f - i * W);
-        if (t >= a.T) b = t + 1;   // past the chunk: skip
+    const unsigned nw = gridDim.x * 4u, wid = blockIdx.x * 4u + (unsigned)wv;
+    const unsigned per = (nfr + nw - 1) / nw;
+    const unsigned fbeg = wid * per;
+    const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
+    // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
+    // T); walked incrementally (no per-frame division)
+    struct Pos { unsigned i, k; int s, b, t; };
+    auto row_of = [&](Pos& p) {
+        p.s = a.list ? a.list[p.i] : (int)p.i;
+        p.b = a.seg_begin ? a.seg_begin[p.s] : 0;
     };
-    auto window_src = [&](int s, int t, int b) -> const int4* {
-        const int fi = t - 2 + lane / 20, off = (lane % 20) * 8;
-        if (fi < b) return reinterpret_cast<const int4*>(a.tail + (size_t)s * 320 + (fi - b + 2) * 160 + off);
+    auto advance = [&](Pos& p) {
+        if (++p.k == W) { p.k = 0; ++p.i; row_of(p); }
+        p.t = p.b + (int)p.k;
+    };
+    // samples of input frame fi (relative to the segment start b: the tail
+    // before it; input frame fi - lookback of the chunk, or of the history)
+    auto frame_ptr = [&](int s, int fi, int b) -> const int16_t* {
+        if (fi < b) return a.tail + (size_t)s * 320 + (fi - b + 2) * 160;
         const int x = fi - a.lookback;
-        return reinterpret_cast<const int4*>(x >= 0 ? a.pcm + ((size_t)s * a.T + x) * 160 + off
-                                                    : a.hist + ((size_t)s * a.hist_frames + a.hist_frames + x) * 160 + off);
+        return x >= 0 ? a.pcm + ((size_t)s * a.T + x) * 160
+                      : a.hist + ((size_t)s * a.hist_frames + a.hist_frames + x) * 160;
     };
-    unsigned f = blockIdx.x * 4u + wv;
-    int4 nxt = make_int4(0, 0, 0, 0);
-    if (f < nfr && lane < 60) {
-        int s0, t0, b0;
-        frame_of(f, s0, t0, b0);
-        if (t0 >= b0) nxt = *window_src(s0, t0, b0);
-    }
-    for (; f < nfr; f += stride) {
-        int s, t, b;
-        frame_of(f, s, t, b);
-        const int4 raw = nxt;
-        if (f + stride < nfr && lane < 60) {   // prefetch the next frame's window
-            int s1, t1, b1;
-            frame_of(f + stride, s1, t1, b1);
-            if (t1 >= b1) nxt = *window_src(s1, t1, b1);
+    // lane's window samples 128*m + 2*lane, +1 of frames t-2, t-1, t
+    auto load_frame = [&](const Pos& p, uint32_t (&r)[4]) {
+        const int16_t* p0 = frame_ptr(p.s, p.t - 2, p.b);
+        const int16_t* p1 = frame_ptr(p.s, p.t - 1, p.b);
+        const int16_t* p2 = frame_ptr(p.s, p.t, p.b);
+        const int o = 2 * lane;
+        r[0] = *reinterpret_cast<const uint32_t*>(p0 + o);
+        r[1] = *reinterpret_cast<const uint32_t*>(lane < 16 ? p0 + 128 + o : p1 + o - 32);
+        r[2] = *reinterpret_cast<const uint32_t*>(lane < 32 ? p1 + 96 + o : p2 + o - 64);
+        r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(p2 + 64 + o) : 0u;
+    };
+    if (fbeg >= fend) return;
+    Pos nx;
+    nx.i = fbeg / W;
+    nx.k = fbeg - nx.i * W;
+    row_of(nx);
+    nx.t = nx.b + (int)nx.k;
+    uint32_t nxt[4] = {0u, 0u, 0u, 0u};
+    if (nx.t < a.T) load_frame(nx, nxt);
+    for (unsigned f = fbeg; f < fend; ++f) {
+        const Pos cur = nx;
+        const uint32_t raw[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
+        if (f + 1 < fend) {   // prefetch the next frame's window
+            advance(nx);
+            if (nx.t < a.T) load_frame(nx, nxt);
         }
-        if (t < b) continue;   // before this stream's segment (wave-uniform)
+        if (cur.t >= a.T) continue;   // past the chunk (wave-uniform)
+        const int s = cur.s, t = cur.t;
         const unsigned fo = (unsigned)s * (unsigned)a.T + (unsigned)t;   // output frame index
-        // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30
-        {
-            const uint32_t rw[4] = {(uint32_t)raw.x, (uint32_t)raw.y, (uint32_t)raw.z, (uint32_t)raw.w};
-            int32_t xv[8];
+        // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30;
+        // complex c = (x[2c], x[2c+1]), c = 64*m + lane
+        int32_t v[8];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {   // win = 0 past lane 59
-                xv[2 * j] = (int32_t)(int16_t)(L.win[j] & 0xffff) * (int32_t)(int16_t)(rw[j] & 0xffff);
-                xv[2 * j + 1] = (int32_t)(int16_t)(L.win[j] >> 16) * (int32_t)(int16_t)(rw[j] >> 16);
-            }
-            int32_t* q = X + cidx(4 * lane);
-            *reinterpret_cast<int4*>(q) = make_int4(xv[0], xv[1], xv[2], xv[3]);
-            *reinterpret_cast<int4*>(q + 4) = make_int4(xv[4], xv[5], xv[6], xv[7]);
+        for (int m = 0; m < 4; ++m) {
+            v[2 * m] = (int32_t)(int16_t)(L.win[m] & 0xffff) * (int32_t)(int16_t)(raw[m] & 0xffff);
+            v[2 * m + 1] = (int32_t)(int16_t)(L.win[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
         }
-        wave_lds_sync();
-        wave_cfft256(X, TB, lane);
+        wave_cfft256(v, X, TB, lane);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             int32_t re, im;
-            wave_split_bin(X, L, TB, lane, m, re, im);
+            wave_split_bin(X, TB, lane, m, re, im);
             P[lane + 64 * m] = pspec_of(re, im);
             if (a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
@@ -275,8 +288,8 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
 #pragma unroll
             for (int i = 0; i < 6; ++i) {
                 const int2 pv = make_int2(P[L.mj0 + 2 * i], P[L.mj0 + 2 * i + 1]);
-                mac += (int64_t)(int16_t)(L.mc[i] & 0xffff) * pv.x;
-                mac += (int64_t)(int16_t)(L.mc[i] >> 16) * pv.y;
+                mac = mad_i64_i32((int32_t)(int16_t)(L.mc[i] & 0xffff), pv.x, mac);
+                mac = mad_i64_i32((int32_t)L.mc[i] >> 16, pv.y, mac);
             }
             Mp[lane] = mac;
         }
@@ -293,7 +306,6 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
         wave_lds_sync();
     }
 }
-
 // ============================================================================
 // NN: generic fc / lstm stack on int8 MFMA
 // ============================================================================
@@ -565,25 +577,23 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
 // Stage kernels (legacy scalar API + per-stage parity tests)
 // ============================================================================
 __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
-    __shared__ __attribute__((aligned(16))) int32_t X[FE_FRAME_DW];
+    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     fe_tables_init(TB);
     const int lane = threadIdx.x;
-    FeLane L;
-    fe_lane_init(L, lane);
     __syncthreads();
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
         int32_t* xb = x + (size_t)b * 512;
-        for (int c = lane; c < 256; c += 64) {
-            X[cidx(c)] = xb[2 * c];
-            X[cidx(c) + 1] = xb[2 * c + 1];
+        int32_t v[8];
+        for (int m = 0; m < 4; ++m) {   // stage-1 layout: complex 64*m + lane
+            v[2 * m] = xb[2 * (64 * m + lane)];
+            v[2 * m + 1] = xb[2 * (64 * m + lane) + 1];
         }
-        wave_lds_sync();
-        wave_cfft256(X, TB, lane);
+        wave_cfft256(v, X, TB, lane);
         int32_t* yb = y + (size_t)b * 1024;
         for (int m = 0; m < 4; ++m) {
             int32_t re, im;
-            wave_split_bin(X, L, TB, lane, m, re, im);
+            wave_split_bin(X, TB, lane, m, re, im);
             const int k = lane + 64 * m;
             if (k) {
                 yb[2 * k] = re; yb[2 * k + 1] = im;
@@ -597,8 +607,8 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
         }
         // pSrc holds the bit-reversed cFFT output afterwards (in-place CMSIS)
         for (int c = lane; c < 256; c += 64) {
-            xb[2 * c] = X[cidx(rev8(c))];
-            xb[2 * c + 1] = X[cidx(rev8(c)) + 1];
+            xb[2 * c] = X[2 * zslot(c)];
+            xb[2 * c + 1] = X[2 * zslot(c) + 1];
         }
         wave_lds_sync();
     }
