@@ -160,11 +160,14 @@ def main() -> None:
         if cascade:
             r, _, _ = eng.last_stats()
             rounds += r
+            kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + eng.fe_stats()   # shared log-Mel, one launch
+            kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
+            klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + 1
             for n in ("vad", "kws", "s2i"):
                 f, fe, nn, nl = eng.net_stats(n)
-                kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + fe
-                kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + f
-                klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + nl
+                kt[f"feat_{n}"] = kt.get(f"feat_{n}", 0.0) + fe   # seg_norm + cold-frame front end
+                kframes[f"feat_{n}"] = kframes.get(f"feat_{n}", 0) + f
+                klaunch[f"feat_{n}"] = klaunch.get(f"feat_{n}", 0) + nl
                 kt[f"nn_{n}"] = kt.get(f"nn_{n}", 0.0) + nn
                 kframes[f"nn_{n}"] = kframes.get(f"nn_{n}", 0) + f
                 klaunch[f"nn_{n}"] = klaunch.get(f"nn_{n}", 0) + nl
@@ -192,7 +195,7 @@ def main() -> None:
         cu, clk = info["compute_units"], info["clock_khz"] * 1e3
         valu_peak = cu * 128 * clk / 1e12          # int32 VALU lane-ops/s (4 SIMD32 per CU)
         mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
-        dom = max(kt, key=kt.get)                  # dominant kernel by device time
+        dom = max((k for k in kt if not k.startswith("feat_")), key=kt.get)   # dominant kernel by device time
         launches = klaunch[dom]
         avg_launch_s = kt[dom] / 1e3 / launches    # HIP-event time on the engine's stream
         units = kframes[dom] / launches            # frames per launch

@@ -74,11 +74,16 @@ void *nnsp_cascade_stream(nnsp_cascade *c);
 int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run, float *ms);
 
 /* Last chunk, one net (NNSP_ID): frames scheduled on it, the device time of
- * its front-end kernel and of its NN kernels (proj + recur) summed over the
- * rounds, and the number of rounds it ran in (one launch of each kernel per
- * round). */
+ * its segment features (normalisation of the shared log-Mel + the front end
+ * of the frames right after its resets) and of its NN kernels (proj + recur +
+ * context roll) summed over the rounds, and the number of rounds it ran in
+ * (one launch of each kernel per round). */
 int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms,
                                 float *nn_ms, int *launches);
+
+/* Last chunk: device time in ms of the shared front end (the log-Mel of every
+ * frame of every stream, one launch). */
+int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms);
 
 /* current_pos_seq of every stream -> host int8 [S]. */
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);

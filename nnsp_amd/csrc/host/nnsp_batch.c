@@ -220,6 +220,19 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     if (timed) TRY(nnspk_event_record(b->ev[0], stream));
     TRY(nnspk_launch_fe(&fa, stream));
     if (timed) TRY(nnspk_event_record(b->ev[1], stream));
+    TRY(nnsp_batch_run_nn(b, T, trig, logits, seg, stream));
+    if (timed) TRY(nnspk_event_record(b->ev[2], stream));
+    /* carry the PCM tail (last 320 samples) */
+    TRY(nnspk_launch_tail_roll(b->d_tail, pcm, b->S, T, seg->list, seg->n_list, seg->seg_begin, seg->seg_len,
+                               seg->lookback, seg->hist, seg->hist_frames, stream));
+    return 0;
+}
+
+int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, const nnsp_segment *seg,
+                      void *stream)
+{
+    static const nnsp_segment whole = {0};
+    if (!seg) seg = &whole;
     if (b->fast) {
         FastRun f;
         memset(&f, 0, sizeof f);
@@ -247,8 +260,9 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
         f.a_lds_bytes = (int)LL->ar_off;
         f.ep_lo = 0;
         f.ep_n = b->ep_proj;
+        f.n_list_dev = seg->n_list_dev;
         int blocks = b->proj_blocks;
-        if (seg->list) {   /* size the grid to the listed streams */
+        if (seg->list && !seg->n_list_dev) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
             const long long pt = (long long)seg->n_list * ((W / 2 + 1 + 15) / 16);
             const long long need = (pt + 3) / 4;
@@ -275,13 +289,10 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
         r.trig = trig;
         r.logits = logits;
         TRY(nnspk_launch_nn(&b->im.img, &r, stream));
+        /* carry the feature context (slots 1..5); recur_kernel does it on the split path */
+        TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, seg->list, seg->n_list, seg->seg_begin,
+                                  seg->seg_len, stream));
     }
-    if (timed) TRY(nnspk_event_record(b->ev[2], stream));
-    /* carry the context (slots 1..5) and the PCM tail (last 320 samples) */
-    TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, seg->list, seg->n_list, seg->seg_begin,
-                              seg->seg_len, stream));
-    TRY(nnspk_launch_tail_roll(b->d_tail, pcm, b->S, T, seg->list, seg->n_list, seg->seg_begin, seg->seg_len,
-                               seg->lookback, seg->hist, seg->hist_frames, stream));
     return 0;
 }
 

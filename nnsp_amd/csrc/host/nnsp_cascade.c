@@ -1,14 +1,25 @@
 /*
  * nnsp_cascade.c -- batched nnCntrlClass (include/nnsp_cascade.h).
  *
- * Per chunk: casc_begin lists every stream under the net at its position;
- * then rounds of { for each net with listed streams: one segment run of the
- * batch engine (fe -> proj -> recur -> context/tail roll) from each stream's
- * segment start to the end of the chunk; casc_control replays the
- * controller over the round's triggers, cuts each stream's segment at its
- * first net switch, requests the departing net's reset and lists the stream
- * for the next round; the resets run } until no stream is listed; finally
- * the PCM history (the voice buffer the look-back reads) rolls forward.
+ * Per chunk:
+ *   1. one front-end launch computes the log-Mel of every PCM frame of every
+ *      stream (FE_MODE_SHARED) into a ring that also keeps the look-back
+ *      frames of earlier chunks.  The log-Mel of a frame does not depend on
+ *      the net: all three nets run the same FeatureClass up to log10_vec, and
+ *      a net whose STFT buffer holds the real previous frames sees exactly the
+ *      shared value of the frame it reads (the current one for VAD, the one
+ *      frs_vbufBk frames back for KWS / S2I);
+ *   2. casc_begin lists every stream under the net at its position;
+ *   3. rounds of { for each net with listed streams: its features for the
+ *      segment (seg_norm normalises the shared log-Mel with the net's
+ *      mean / stdR; the 0-2 frames right after the net's reset, whose STFT
+ *      buffer still holds zeros, run the full front end in FE_MODE_COLD), then
+ *      the NN half (proj -> recur -> context roll); casc_control replays the
+ *      controller over the round's triggers, cuts each stream's segment at its
+ *      first net switch, requests the departing net's reset and lists the
+ *      stream for the next round; the resets run } until no stream is listed;
+ *   4. the PCM history (what the look-back and the cold frames read) and the
+ *      shared front end's PCM tail roll forward.
  * The host reads back three list lengths per round and nothing else.
  */
 #include <stdlib.h>
@@ -24,6 +35,7 @@
     } while (0)
 
 #define HIST_MAX 99   /* PcmBufClass keeps 100 frames: look-back 0..99 */
+#define MAX_TIMED 32  /* rounds per chunk with per-net device timing */
 
 struct nnsp_cascade {
     nnsp_batch *net[3];
@@ -38,14 +50,26 @@ struct nnsp_cascade {
     int32_t *d_list[3];
     int16_t *d_hist[2];
     int hist_cur;
+    int32_t *d_lmel;                /* [S][ring][40] shared log-Mel */
+    int ring, abs0;                 /* ring slots (>= H + Tmax); slot of chunk frame 0 */
+    int16_t *d_stail;               /* [S][320] PCM tail of the shared front end */
+    int8_t *d_fresh;                /* [S] frames the current net ran since its reset */
     int16_t *d_pcm, *d_det, *d_o3;
     int8_t *d_ran;
-    void *stream;
+    int16_t *d_pdef;                /* [3][40] FeatureClass_setDefault context value per net */
+    int32_t *d_rcount;              /* [MAX_TIMED][3] list lengths each round ran with */
+    int32_t *d_last_round;          /* last round a stream was listed for (+1) */
+    void *stream;                   /* front end, control; the nets' work forks off it */
+    void *ns[3];                    /* per net id: segment features + NN of a round */
     void *ev[2];
-    int last_rounds;
+    void *ev_fe[2];                 /* shared front end */
+    void *ev_fork, *ev_join[3];
+    void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
+    int last_rounds, launched;
     int window;                     /* frames per stream and round (0: to the chunk end) */
-    float fe_ms[3], nn_ms[3];       /* last chunk, per net id: device time of fe / proj+recur */
-    int runs[3];                    /* last chunk, per net id: segment runs (fe launches) */
+    float sfe_ms;                   /* last chunk: shared front end */
+    float fe_ms[3], nn_ms[3];       /* last chunk, per net id: features / proj+recur+roll */
+    int runs[3];                    /* last chunk, per net id: segment runs */
 };
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
@@ -89,16 +113,31 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->lookback[0] = p->frs_vbufBk_s2i;
     c->lookback[1] = 0; /* VAD reads the current frame (nnCntrlClass.c:243-247) */
     c->lookback[2] = p->frs_vbufBk_kws;
-    c->H = c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2];
-    if (c->H < 1) c->H = 1;
+    /* PCM history: the look-back frame and, for the second frame after a
+     * net's reset, the one before it (FE_MODE_COLD re-reads it) */
+    c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
+    c->ring = c->H + c->Tmax;
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
     for (int i = 0; i < 2; ++i)
-        if ((e = nnspk_event_create(&c->ev[i]))) goto fail;
+        if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
+    if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
+    for (int n = 0; n < 3; ++n) {
+        if ((e = nnspk_stream_create(&c->ns[n])) || (e = nnspk_event_create(&c->ev_join[n]))) goto fail;
+        for (int r = 0; r < MAX_TIMED; ++r)
+            for (int i = 0; i < 3; ++i)
+                if ((e = nnspk_event_create(&c->ev_t[r][n][i]))) goto fail;
+    }
     if ((e = nnspk_malloc((void **)&c->d_st, S * sizeof(CascState)))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_counts, 3 * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_counts, 9 * 4))) goto fail;   /* 3 rounds in flight x 3 nets */
+    if ((e = nnspk_malloc((void **)&c->d_rcount, MAX_TIMED * 3 * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_last_round, 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_frames, 3 * 8))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_lmel, S * (size_t)c->ring * 40 * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_fresh, S))) goto fail;
     for (int i = 0; i < 3; ++i) {
         if ((e = nnspk_malloc((void **)&c->d_trig[i], S * T * 2))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_out3[i], S * T * 6))) goto fail;
@@ -121,14 +160,35 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         a->seg_begin = c->d_seg_begin;
         a->counts = c->d_counts;
         a->frames = c->d_frames;
+        a->fresh = c->d_fresh;
+        a->last_round = c->d_last_round;
         for (int i = 0; i < 3; ++i) {
             a->trig[i] = c->d_trig[i];
             a->out3[i] = c->d_out3[i];
             a->feats[i] = nets[i]->d_feats;
             a->prev5[i] = nets[i]->d_prev5;
-            a->reset_mask[i] = c->d_mask[i];
+            a->h[i] = nets[i]->d_h;
+            a->c[i] = nets[i]->d_c;
+            a->post[i] = nets[i]->d_post;
+            a->prev_default[i] = c->d_pdef + 40 * i;
             a->list[i] = c->d_list[i];
         }
+    }
+    {   /* the reset context value of each net: FeatureClass_setDefault on a scratch stream */
+        int16_t *p5 = NULL, *tl = NULL;
+        if ((e = nnspk_malloc((void **)&p5, 400)) || (e = nnspk_malloc((void **)&tl, 640))) {
+            nnspk_free(p5);
+            goto fail;
+        }
+        for (int i = 0; i < 3 && !e; ++i) {
+            nnsp_batch *b = nets[i];
+            e = nnspk_launch_fe_default(p5, tl, b->d_mean, b->d_stdR, b->norm_shift, NULL, 1, c->stream);
+            if (!e) e = nnspk_d2d(c->d_pdef + 40 * i, p5, 80, c->stream);
+        }
+        if (!e) e = nnspk_sync(c->stream);
+        nnspk_free(p5);
+        nnspk_free(tl);
+        if (e) goto fail;
     }
     c->window = 12;
     {
@@ -150,9 +210,20 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_counts,  c->d_frames,  c->d_trig[0], c->d_trig[1],
                     c->d_trig[2], c->d_out3[0],   c->d_out3[1], c->d_out3[2], c->d_mask[0], c->d_mask[1],
                     c->d_mask[2], c->d_list[0],   c->d_list[1], c->d_list[2], c->d_hist[0], c->d_hist[1],
-                    c->d_pcm,     c->d_det,       c->d_o3,      c->d_ran};
+                    c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
+                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
-    for (int i = 0; i < 2; ++i) nnspk_event_destroy(c->ev[i]);
+    for (int i = 0; i < 2; ++i) {
+        nnspk_event_destroy(c->ev[i]);
+        nnspk_event_destroy(c->ev_fe[i]);
+    }
+    nnspk_event_destroy(c->ev_fork);
+    for (int n = 0; n < 3; ++n) {
+        nnspk_event_destroy(c->ev_join[n]);
+        for (int r = 0; r < MAX_TIMED; ++r)
+            for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
+        nnspk_stream_destroy(c->ns[n]);
+    }
     nnspk_stream_destroy(c->stream);
     free(c);
 }
@@ -167,9 +238,79 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
         TRY(nnspk_h2d(c->d_mask[0], mask, (size_t)c->S, c->stream));
         dm = c->d_mask[0];
     }
-    TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->hist_cur], c->H, dm, c->S, c->stream));
+    TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->hist_cur], c->H, c->d_stail, c->d_fresh, dm, c->S,
+                                c->stream));
+    /* PcmBufClass_reset: every look-back frame is silence */
+    TRY(nnspk_launch_lmel_fill(c->d_lmel, c->ring, dm, c->S, c->stream));
     if (mask) TRY(nnspk_memset(c->d_mask[0], 0, (size_t)c->S, c->stream));
     return nnspk_sync(c->stream);
+}
+
+/* features of net n for this round's segments: normalised shared log-Mel,
+ * and the full front end for the frames right after the net's reset */
+static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *n_list_dev,
+                            int32_t *n_list_rec, const int16_t *hist, void *stream)
+{
+    nnsp_batch *b = c->net[n];
+    FeArgs fa;
+    memset(&fa, 0, sizeof fa);
+    fa.pcm = pcm;
+    fa.S = c->S;
+    fa.T = T;
+    fa.mean = b->d_mean;
+    fa.stdR = b->d_stdR;
+    fa.norm_shift = b->norm_shift;
+    fa.feats = b->d_feats;
+    fa.list = c->d_list[n];
+    fa.n_list_dev = n_list_dev;
+    fa.n_list_rec = n_list_rec;
+    fa.seg_begin = c->d_seg_begin;
+    fa.lookback = c->lookback[n];
+    fa.hist = hist;
+    fa.hist_frames = c->H;
+    fa.seg_len = c->window;
+    fa.ring = c->ring;
+    fa.abs0 = c->abs0;
+    fa.lmel = c->d_lmel;
+    fa.fresh = c->d_fresh;
+    TRY(nnspk_launch_seg_norm(&fa, stream));
+    fa.mode = FE_MODE_COLD;
+    fa.n_list_rec = NULL;
+    return nnspk_launch_fe(&fa, stream);
+}
+
+/* One round, asynchronous: the three nets' segments on their own streams
+ * (empty lists exit on the device), then casc_control on the main stream. */
+static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm, int T, const int16_t *hist)
+{
+    int32_t *cur = c->d_counts + 3 * (r % 3);
+    TRY(nnspk_event_record(c->ev_fork, c->stream));
+    for (int n = 0; n < 3; ++n) {
+        void *st = c->ns[n];
+        const int timed = r < MAX_TIMED;
+        TRY(nnspk_stream_wait(st, c->ev_fork));
+        if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
+        TRY(segment_features(c, n, pcm, T, cur + n, timed ? c->d_rcount + 3 * r + n : NULL, hist, st));
+        if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
+        nnsp_segment seg;
+        memset(&seg, 0, sizeof seg);
+        seg.list = c->d_list[n];
+        seg.n_list_dev = cur + n;
+        seg.seg_begin = c->d_seg_begin;
+        seg.lookback = c->lookback[n];
+        seg.hist = hist;
+        seg.hist_frames = c->H;
+        seg.out3 = c->d_out3[n];
+        seg.seg_len = c->window;
+        TRY(nnsp_batch_run_nn(c->net[n], T, c->d_trig[n], NULL, &seg, st));
+        if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
+        TRY(nnspk_event_record(c->ev_join[n], st));
+        TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
+    }
+    a->counts = c->d_counts + 3 * ((r + 1) % 3);
+    a->counts_clear = c->d_counts + 3 * ((r + 2) % 3);
+    a->round = r;
+    return nnspk_launch_casc_control(a, c->stream);
 }
 
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran, int16_t *detected,
@@ -185,66 +326,70 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     a.net_ran = net_ran;
     a.detected = detected;
     a.outputs3 = outputs3;
-    int32_t cnt[3];
     TRY(nnspk_event_record(c->ev[0], c->stream));
-    TRY(nnspk_memset(c->d_counts, 0, 12, c->stream));
+    TRY(nnspk_memset(c->d_counts, 0, 9 * 4, c->stream));
     TRY(nnspk_memset(c->d_frames, 0, 3 * 8, c->stream));
+    TRY(nnspk_memset(c->d_last_round, 0, 4, c->stream));
+    TRY(nnspk_memset(c->d_rcount, 0, MAX_TIMED * 3 * 4, c->stream));
+    {   /* 1. log-Mel of every frame (net-independent) */
+        FeArgs fa;
+        memset(&fa, 0, sizeof fa);
+        fa.pcm = pcm;
+        fa.tail = c->d_stail;
+        fa.S = c->S;
+        fa.T = T;
+        fa.mean = c->net[0]->d_mean; /* unused in FE_MODE_SHARED */
+        fa.stdR = c->net[0]->d_stdR;
+        fa.mode = FE_MODE_SHARED;
+        fa.ring = c->ring;
+        fa.abs0 = c->abs0;
+        fa.lmel = c->d_lmel;
+        TRY(nnspk_event_record(c->ev_fe[0], c->stream));
+        TRY(nnspk_launch_fe(&fa, c->stream));
+        TRY(nnspk_event_record(c->ev_fe[1], c->stream));
+    }
+    a.counts = c->d_counts; /* round 0's lists */
+    TRY(nnspk_launch_casc_begin(&a, c->stream));
+    /* rounds run without host round trips: launch as many as the last chunk
+     * needed, then check the next round's list lengths (one read-back) */
+    const int16_t *hist = c->d_hist[c->hist_cur];
+    int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
+    for (;;) {
+        for (; r < R; ++r) TRY(launch_round(c, &a, r, pcm, T, hist));
+        int32_t cnt[3];
+        TRY(nnspk_d2h(cnt, c->d_counts + 3 * (r % 3), 12, c->stream));
+        TRY(nnspk_sync(c->stream));
+        if (cnt[0] + cnt[1] + cnt[2] == 0) break;
+        R = r + 2;
+    }
+    c->launched = r;
+    /* voice buffer: keep the last H frames for the next chunk's look-back;
+     * the shared front end's STFT buffer keeps the last 2 frames */
+    TRY(nnspk_launch_hist_roll(c->d_hist[c->hist_cur ^ 1], hist, pcm, c->S, T, c->H, c->stream));
+    c->hist_cur ^= 1;
+    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
+    c->abs0 = (c->abs0 + T) % c->ring;
+    TRY(nnspk_event_record(c->ev[1], c->stream));
+    /* bookkeeping: rounds that had work, per-net device time of those rounds */
+    int32_t last = 0, rc[MAX_TIMED][3];
+    TRY(nnspk_d2h(&last, c->d_last_round, 4, c->stream));
+    TRY(nnspk_d2h(rc, c->d_rcount, sizeof rc, c->stream));
+    TRY(nnspk_sync(c->stream));
+    c->last_rounds = last + 1;
+    TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
     for (int n = 0; n < 3; ++n) {
         c->fe_ms[n] = c->nn_ms[n] = 0.f;
         c->runs[n] = 0;
-    }
-    TRY(nnspk_launch_casc_begin(&a, c->stream));
-    TRY(nnspk_d2h(cnt, c->d_counts, 12, c->stream));
-    TRY(nnspk_sync(c->stream));
-    int rounds = 0;
-    const int16_t *hist = c->d_hist[c->hist_cur];
-    while (cnt[0] + cnt[1] + cnt[2] > 0) {
-        int ran[3];
-        for (int n = 0; n < 3; ++n) {
-            ran[n] = cnt[n] > 0;
-            if (!cnt[n]) continue;
-            c->runs[n]++;
-            nnsp_batch *b = c->net[n];
-            nnsp_segment seg;
-            memset(&seg, 0, sizeof seg);
-            seg.list = c->d_list[n];
-            seg.n_list = cnt[n];
-            seg.seg_begin = c->d_seg_begin;
-            seg.lookback = c->lookback[n];
-            seg.hist = hist;
-            seg.hist_frames = c->H;
-            seg.out3 = c->d_out3[n];
-            seg.seg_len = c->window;
-            TRY(nnsp_batch_run(b, pcm, T, c->d_trig[n], NULL, &seg, c->stream, 1));
-        }
-        TRY(nnspk_memset(c->d_counts, 0, 12, c->stream));
-        TRY(nnspk_launch_casc_control(&a, c->stream));
-        for (int n = 0; n < 3; ++n) {
-            nnsp_batch *b = c->net[n];
-            /* NNSPClass_reset of the departing streams (slot 5 already set) */
-            TRY(nnspk_launch_fe_default(b->d_prev5, b->d_tail, b->d_mean, b->d_stdR, b->norm_shift,
-                                        c->d_mask[n], c->S, c->stream));
-            TRY(nnspk_launch_nn_default(b->d_h, b->d_c, b->d_post, b->im.img.n_lstm ? b->im.img.n_lstm : 1,
-                                        c->d_mask[n], c->S, c->stream));
-            TRY(nnspk_memset(c->d_mask[n], 0, (size_t)c->S, c->stream));
-        }
-        TRY(nnspk_d2h(cnt, c->d_counts, 12, c->stream));
-        TRY(nnspk_sync(c->stream));
-        for (int n = 0; n < 3; ++n) {   /* kernel times of this round's segment runs */
-            if (!ran[n]) continue;
+        for (int k = 0; k < r && k < MAX_TIMED; ++k) {
+            if (!rc[k][n]) continue;
             float fe = 0.f, nn = 0.f;
-            TRY(nnspk_event_elapsed(&fe, c->net[n]->ev[0], c->net[n]->ev[1]));
-            TRY(nnspk_event_elapsed(&nn, c->net[n]->ev[1], c->net[n]->ev[2]));
+            TRY(nnspk_event_elapsed(&fe, c->ev_t[k][n][0], c->ev_t[k][n][1]));
+            TRY(nnspk_event_elapsed(&nn, c->ev_t[k][n][1], c->ev_t[k][n][2]));
             c->fe_ms[n] += fe;
             c->nn_ms[n] += nn;
+            c->runs[n]++;
         }
-        ++rounds;
     }
-    /* voice buffer: keep the last H frames for the next chunk's look-back */
-    TRY(nnspk_launch_hist_roll(c->d_hist[c->hist_cur ^ 1], hist, pcm, c->S, T, c->H, c->stream));
-    c->hist_cur ^= 1;
-    TRY(nnspk_event_record(c->ev[1], c->stream));
-    c->last_rounds = rounds;
     return 0;
 }
 
@@ -294,6 +439,14 @@ int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run,
         *frames_run = (long long)(f[0] + f[1] + f[2]);
     }
     if (ms) TRY(nnspk_event_elapsed(ms, c->ev[0], c->ev[1]));
+    return 0;
+}
+
+int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms)
+{
+    if (!c) return NNSP_EINVAL;
+    TRY(nnspk_sync(c->stream));
+    if (ms) *ms = c->sfe_ms;
     return 0;
 }
 

@@ -75,10 +75,15 @@ typedef struct {
     int16_t *out3;
     int n_list, lookback, hist_frames;
     int seg_len;              /* > 0: segments end at min(T, seg_begin + seg_len) */
+    const int32_t *n_list_dev; /* non-NULL: list length on the device (overrides n_list) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
                    const nnsp_segment *seg, void *stream, int timed);
+/* the NN half of a segment run (features already in d_feats): proj + recur
+ * (or the fused kernel) and the feature-context roll */
+int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, const nnsp_segment *seg,
+                      void *stream);
 
 void nnsp_set_error(const char *fmt, ...);
 const char *nnsp_last_error(void);

@@ -61,6 +61,7 @@ __global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
 
 __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < 3 && a.counts_clear) a.counts_clear[s] = 0;
     const int T = a.T;
     bool want = false;
     int n_next = 0, b_next = T;
@@ -116,13 +117,38 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
                 break;
             }
         }
+        // frames since the reset of the net the stream runs next round (the
+        // front end's STFT buffer is zero right after NNSPClass_reset)
+        a.fresh[s] = (int8_t)(cut >= 0 ? 0 : min(2, (int)a.fresh[s] + (e - b)));
         if (cut >= 0) {
-            // NNSPClass_reset of the departing net; slot 5 = this frame's feature (T4)
-            a.reset_mask[n][s] = 1;
+            // NNSPClass_reset of the departing net (nn_speech.c:57-72):
+            // FeatureClass_setDefault -- context slots 0..4 := the default,
+            // slot 5 keeps this frame's feature (T4); the STFT buffer's zeros
+            // are fresh = 0 of the next net to run -- then the LSTM state
+            // (NeuralNetClass_setDefault) and the post-processing state
             const int4* src = reinterpret_cast<const int4*>(a.feats[n] + ((size_t)s * T + cut) * 40);
-            int4* dst = reinterpret_cast<int4*>(a.prev5[n] + ((size_t)s * 5 + 4) * 40);
+            const int4* def = reinterpret_cast<const int4*>(a.prev_default[n]);
+            int4* p5 = reinterpret_cast<int4*>(a.prev5[n] + (size_t)s * 200);
 #pragma unroll
-            for (int k = 0; k < 5; ++k) dst[k] = src[k];
+            for (int k = 0; k < 5; ++k) {
+                const int4 d = def[k];
+                p5[k] = d;
+                p5[5 + k] = d;
+                p5[10 + k] = d;
+                p5[15 + k] = d;
+                p5[20 + k] = src[k];
+            }
+            const int4 z = make_int4(0, 0, 0, 0);
+            int4* hs = reinterpret_cast<int4*>(a.h[n] + (size_t)s * NN_MAX_W);
+            int4* cs = reinterpret_cast<int4*>(a.c[n] + (size_t)s * NN_MAX_W);
+            for (int k = 0; k < NN_MAX_W / 8; ++k) hs[k] = z;
+            for (int k = 0; k < NN_MAX_W / 4; ++k) cs[k] = z;
+            NnPost* ps = reinterpret_cast<NnPost*>(a.post[n]) + s;
+            ps->slides = 1;
+            ps->trigger = 0;
+            ps->argmax_last = 0;
+            for (int k = 0; k < 7; ++k) ps->counts[k] = 0;
+            ps->outputs[0] = ps->outputs[1] = ps->outputs[2] = 0;
             b_next = cut + 1;
         }
         a.st[s] = st;
@@ -133,23 +159,28 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
         }
     }
     list_push(a, n_next, s, want);
+    if (a.last_round && __ballot(want) && (threadIdx.x & 63) == 0) atomicMax(a.last_round, a.round + 1);
     add_frames(a, n_next,
                want ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, T - b_next) : T - b_next) : 0ull);
 }
 
 // nnCntrlClass_reset's controller part + PcmBufClass_reset (nnCntrlClass.c:132-150,
-// PcmBufClass.c:19-28): timeout counters and the PCM history; the sequence
-// position is kept, as the reference does.
-__global__ __launch_bounds__(256) void casc_reset_kernel(CascState* st, int16_t* hist, int H, const uint8_t* mask,
-                                                        int S) {
+// PcmBufClass.c:19-28): timeout counters, the PCM history and the shared
+// front end's PCM tail; every net restarts from its reset (fresh 0).  The
+// sequence position is kept, as the reference does.
+__global__ __launch_bounds__(256) void casc_reset_kernel(CascState* st, int16_t* hist, int H, int16_t* stail,
+                                                        int8_t* fresh, const uint8_t* mask, int S) {
     const int s = blockIdx.x;
     if (s >= S || (mask && !mask[s])) return;
     if (threadIdx.x == 0) {
         st[s].cnt_kws = 0;
         st[s].cnt_s2i = 0;
+        fresh[s] = 0;
     }
     int4* h = reinterpret_cast<int4*>(hist + (size_t)s * H * 160);
     for (int i = threadIdx.x; i < H * 20; i += blockDim.x) h[i] = make_int4(0, 0, 0, 0);
+    int4* tl = reinterpret_cast<int4*>(stail + (size_t)s * 320);
+    for (int i = threadIdx.x; i < 40; i += blockDim.x) tl[i] = make_int4(0, 0, 0, 0);
 }
 
 // dst := last H frames of (src ++ pcm chunk), per stream (int4 = 8 samples).
@@ -184,11 +215,11 @@ int nnspk_launch_casc_control(const CascArgs* a, void* stream) {
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_casc_reset(CascState* st, int16_t* hist, int hist_frames, const uint8_t* mask, int S,
-                            void* stream) {
+int nnspk_launch_casc_reset(CascState* st, int16_t* hist, int hist_frames, int16_t* stail, int8_t* fresh,
+                            const uint8_t* mask, int S, void* stream) {
     if (S <= 0) return 0;
-    hipLaunchKernelGGL(casc_reset_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, st, hist, hist_frames, mask,
-                       S);
+    hipLaunchKernelGGL(casc_reset_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, st, hist, hist_frames, stail,
+                       fresh, mask, S);
     return ok(hipGetLastError());
 }
 

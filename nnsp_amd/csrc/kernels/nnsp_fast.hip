@@ -177,7 +177,7 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     const int rows = 16 * nrt;   // LSTM rows are padded to whole tiles (4 units per group)
     const int wsteps = r.seg_len > 0 ? min(r.nstep_max, (r.seg_len + 1) / 2) : r.nstep_max;
     const int ntps = (wsteps + 15) / 16;
-    const int nrow = r.list ? r.n_list : r.S;
+    const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
     const long long ntiles = (long long)nrow * ntps;
     for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
          tile += (long long)gridDim.x * (blockDim.x >> 6)) {
@@ -294,6 +294,9 @@ template <class SH, int RPW, bool ACC32>   // RPW: LSTM row tiles per wave = cei
 __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     constexpr bool GEN = SH::generic;
+    // tile = 16 consecutive entries of the stream list (identity when list == NULL)
+    const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
+    if ((int)(blockIdx.x * (blockDim.x / (64 * RW))) * 16 >= nrow) return;   // whole workgroup past the list
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
@@ -307,8 +310,6 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     const bool tail = g == RG;
     RecTile& R = tiles[tl];
     const int sc = lane & 15, q = lane >> 4;
-    // tile = 16 consecutive entries of the stream list (identity when list == NULL)
-    const int nrow = r.list ? r.n_list : r.S;
     const int i0 = (blockIdx.x * tpw + tl) * 16;
     auto sid = [&](int i) { return r.list ? r.list[i] : i; };
     const bool valid = i0 + sc < nrow;
@@ -507,6 +508,30 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
         ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
+    // ---- feature context (normFeatContext slots 1..5) := last 5 of prev5 ++ feats[b..e):
+    // all of the tile's reads before any write (a stream's old slots feed its new ones)
+    int4 cv[2];
+    int ci[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int idx = g * 64 + lane + 64 * RW * k;   // (stream in tile, 16-byte chunk of 5x40)
+        ci[k] = -1;
+        if (idx < 16 * 25 && i0 + idx / 25 < nrow) {
+            const int st = idx / 25, c = idx - st * 25, m = c / 5, part = c - 5 * m;
+            const int L = R.end[st] - R.beg[st];
+            if (L > 0) {
+                const int gs = sid(i0 + st), j = L + m;
+                cv[k] = j < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + j) * 40 + 8 * part)
+                              : *reinterpret_cast<const int4*>(r.feats + ((size_t)gs * T + R.beg[st] + j - 5) * 40 +
+                                                               8 * part);
+                ci[k] = gs * 25 + c;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (ci[k] >= 0) reinterpret_cast<int4*>(r.prev5)[ci[k]] = cv[k];
 }
 
 // ---------------------------------------------------------------------------
@@ -571,7 +596,7 @@ int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* st
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n);
-    const int nrow = r->list ? r->n_list : r->S;
+    const int nrow = r->n_list_dev ? r->S : (r->list ? r->n_list : r->S);
     if (nrow <= 0) return 0;
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;

@@ -43,7 +43,23 @@ typedef struct {
     const int16_t *hist;
     int32_t n_list, lookback, hist_frames;
     int32_t seg_len;          /* > 0: a segment ends at min(T, seg_begin + seg_len) */
+    /* cascade modes (FE_MODE_*): SHARED writes the log-Mel of every frame of
+     * every stream (no normalisation) into the ring lmel [S][ring][40], chunk
+     * frame t at slot (abs0 + t) % ring; COLD runs only the frames of a listed
+     * segment that come less than 2 frames after the net's reset (fresh[s] =
+     * frames the net ran since its reset, 0..2): input frames before the reset
+     * point are zero (stftModule_setDefault), the rest come from pcm/hist */
+    int32_t mode;
+    int32_t ring, abs0;
+    int32_t *lmel;
+    const int8_t *fresh;
+    const int32_t *n_list_dev; /* non-NULL: the list length, read on the device */
+    int32_t *n_list_rec;      /* seg_norm: non-NULL, block 0 records *n_list_dev there */
 } FeArgs;
+
+#define FE_MODE_BATCH 0
+#define FE_MODE_SHARED 1
+#define FE_MODE_COLD 2
 
 typedef struct {
     int32_t type, K, N, act;
@@ -86,7 +102,7 @@ typedef struct {
     int32_t a_lds_bytes, pad;
     int64_t a_off;            /* byte offset in NnImage.A of the LDS-staged region */
     const int16_t *feats;     /* [S][T][40] */
-    const int16_t *prev5;     /* [S][5][40] */
+    int16_t *prev5;           /* [S][5][40]; recur rolls it forward over the segment */
     void *post;               /* [S] NnPost */
     int32_t *gx;              /* [S][nstep_max][LSTM rows] exact Wx.x sums */
     int16_t *h;               /* [S][NN_MAX_W] */
@@ -100,6 +116,7 @@ typedef struct {
     long long *dbg_clk;       /* development probe: [steps][8] s_memtime of tile 0, or NULL */
     int32_t ep_lo, ep_n;      /* epilogue rows [ep_lo, ep_lo + ep_n) staged into LDS */
     int32_t shape, pad3;      /* NN_SHAPE_* */
+    const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
 
 /* 32-byte device post-processing state, one per stream */
@@ -111,6 +128,11 @@ typedef struct {
 
 /* launch layer (nnsp_kernels.hip) */
 int nnspk_launch_fe(const FeArgs *a, void *stream);
+/* cascade: normalised features of a segment's frames from the shared log-Mel
+ * ring (frames >= 2 after the net's reset; FeArgs fields as FE_MODE_COLD) */
+int nnspk_launch_seg_norm(const FeArgs *a, void *stream);
+/* cascade reset: ring slots of the masked streams := log-Mel of silence */
+int nnspk_launch_lmel_fill(int32_t *lmel, int ring, const uint8_t *mask, int S, void *stream);
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
 int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
                           int n_list, const int32_t *seg_begin, int seg_len, void *stream);
@@ -153,6 +175,7 @@ int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);
 int nnspk_event_record(void *e, void *stream);
 int nnspk_event_elapsed(float *ms, void *a, void *b);
+int nnspk_stream_wait(void *stream, void *event);
 int nnspk_device_info(int *cus, int *clock_khz, char *name, int name_len);
 
 
@@ -174,19 +197,26 @@ typedef struct {
     const int16_t *out3[3];   /* per net id: [S][T][3] NNSPClass.outputs after each frame */
     const int16_t *feats[3];  /* per net id: [S][T][40] */
     int16_t *prev5[3];        /* per net id: [S][5][40] */
-    uint8_t *reset_mask[3];   /* per net id: [S] NNSPClass_reset requests */
+    int16_t *h[3];            /* per net id: [S][NN_MAX_W] LSTM state (one LSTM layer) */
+    int32_t *c[3];
+    void *post[3];            /* per net id: [S] NnPost */
+    const int16_t *prev_default[3]; /* per net id: [40] FeatureClass_setDefault context value */
     int32_t *list[3];         /* per net id: next round's streams */
-    int32_t *counts;          /* [3] next round's list lengths */
+    int32_t *counts;          /* [3] next round's list lengths (appended to) */
+    int32_t *counts_clear;    /* [3] zeroed by casc_control: the round after next appends there */
+    int32_t *last_round;      /* atomicMax'ed with round + 1 when a stream is listed for it */
+    int32_t round;            /* index of the round casc_control closes */
     unsigned long long *frames; /* [3] frames scheduled per net id (speculation included) */
     int8_t *net_ran;          /* [S][T] or NULL */
     int16_t *detected;        /* [S][T] or NULL */
     int16_t *outputs3;        /* [S][T][3] or NULL */
+    int8_t *fresh;            /* [S] frames the current net ran since its reset (0..2) */
 } CascArgs;
 
 int nnspk_launch_casc_begin(const CascArgs *a, void *stream);
 int nnspk_launch_casc_control(const CascArgs *a, void *stream);
-int nnspk_launch_casc_reset(CascState *st, int16_t *hist, int hist_frames, const uint8_t *mask, int S,
-                            void *stream);
+int nnspk_launch_casc_reset(CascState *st, int16_t *hist, int hist_frames, int16_t *stail, int8_t *fresh,
+                            const uint8_t *mask, int S, void *stream);
 int nnspk_launch_hist_roll(int16_t *dst, const int16_t *src, const int16_t *pcm, int S, int T,
                            int hist_frames, void *stream);
 

@@ -35,6 +35,7 @@ using namespace nnsp;
 // bit reversal), where the split reads bins k and 256-k.  LDS slots are
 // swizzled (zslot) so that every one of these accesses is bank-conflict-free.
 #define FE_X_DW 512   // dwords of one frame's complex buffer (256 complex)
+__device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (FE_MODE_COLD)
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
 
 struct FeLane {
@@ -192,8 +193,10 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
-    const unsigned nrow = a.list ? (unsigned)a.n_list : (unsigned)a.S;
-    const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
+    const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    const bool cold = a.mode == FE_MODE_COLD;
+    const unsigned W = cold ? (segW < 2u ? segW : 2u) : segW;
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
     const unsigned nw = gridDim.x * 4u, wid = blockIdx.x * 4u + (unsigned)wv;
     const unsigned per = (nfr + nw - 1) / nw;
@@ -201,10 +204,19 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
     // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
     // T); walked incrementally (no per-frame division)
-    struct Pos { unsigned i, k; int s, b, t; };
+    // t >= lim: nothing to do (past the chunk; COLD: past the segment or not
+    // within 2 frames of the reset); z: COLD, input frames before z are zero
+    struct Pos { unsigned i, k; int s, b, t, lim, z; };
     auto row_of = [&](Pos& p) {
         p.s = a.list ? a.list[p.i] : (int)p.i;
         p.b = a.seg_begin ? a.seg_begin[p.s] : 0;
+        p.lim = a.T;
+        p.z = 0;
+        if (cold) {
+            const int fr = a.fresh[p.s];
+            p.z = p.b - fr;
+            p.lim = min(min(a.T, p.b + (int)segW), p.b + 2 - fr);
+        }
     };
     auto advance = [&](Pos& p) {
         if (++p.k == W) { p.k = 0; ++p.i; row_of(p); }
@@ -212,17 +224,21 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     };
     // samples of input frame fi (relative to the segment start b: the tail
     // before it; input frame fi - lookback of the chunk, or of the history)
-    auto frame_ptr = [&](int s, int fi, int b) -> const int16_t* {
-        if (fi < b) return a.tail + (size_t)s * 320 + (fi - b + 2) * 160;
+    auto frame_ptr = [&](const Pos& p, int fi) -> const int16_t* {
+        if (cold) {
+            if (fi < p.z) return nnsp_zero_pcm;
+        } else if (fi < p.b) {
+            return a.tail + (size_t)p.s * 320 + (fi - p.b + 2) * 160;
+        }
         const int x = fi - a.lookback;
-        return x >= 0 ? a.pcm + ((size_t)s * a.T + x) * 160
-                      : a.hist + ((size_t)s * a.hist_frames + a.hist_frames + x) * 160;
+        return x >= 0 ? a.pcm + ((size_t)p.s * a.T + x) * 160
+                      : a.hist + ((size_t)p.s * a.hist_frames + a.hist_frames + x) * 160;
     };
     // lane's window samples 128*m + 2*lane, +1 of frames t-2, t-1, t
     auto load_frame = [&](const Pos& p, uint32_t (&r)[4]) {
-        const int16_t* p0 = frame_ptr(p.s, p.t - 2, p.b);
-        const int16_t* p1 = frame_ptr(p.s, p.t - 1, p.b);
-        const int16_t* p2 = frame_ptr(p.s, p.t, p.b);
+        const int16_t* p0 = frame_ptr(p, p.t - 2);
+        const int16_t* p1 = frame_ptr(p, p.t - 1);
+        const int16_t* p2 = frame_ptr(p, p.t);
         const int o = 2 * lane;
         r[0] = *reinterpret_cast<const uint32_t*>(p0 + o);
         r[1] = *reinterpret_cast<const uint32_t*>(lane < 16 ? p0 + 128 + o : p1 + o - 32);
@@ -236,15 +252,15 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     row_of(nx);
     nx.t = nx.b + (int)nx.k;
     uint32_t nxt[4] = {0u, 0u, 0u, 0u};
-    if (nx.t < a.T) load_frame(nx, nxt);
+    if (nx.t < nx.lim) load_frame(nx, nxt);
     for (unsigned f = fbeg; f < fend; ++f) {
         const Pos cur = nx;
         const uint32_t raw[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
         if (f + 1 < fend) {   // prefetch the next frame's window
             advance(nx);
-            if (nx.t < a.T) load_frame(nx, nxt);
+            if (nx.t < nx.lim) load_frame(nx, nxt);
         }
-        if (cur.t >= a.T) continue;   // past the chunk (wave-uniform)
+        if (cur.t >= cur.lim) continue;   // wave-uniform
         const int s = cur.s, t = cur.t;
         const unsigned fo = (unsigned)s * (unsigned)a.T + (unsigned)t;   // output frame index
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30;
@@ -300,8 +316,12 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
             for (int k = 0; k < L.mcnt; ++k) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
             if (a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
-            const int64_t d = (int64_t)lg - mean;
-            a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
+            if (a.mode == FE_MODE_SHARED) {
+                a.lmel[((size_t)s * a.ring + (unsigned)(a.abs0 + t) % (unsigned)a.ring) * 40 + lane] = lg;
+            } else {
+                const int64_t d = (int64_t)lg - mean;
+                a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
+            }
         }
         wave_lds_sync();
     }
@@ -573,6 +593,48 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
     for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
 }
 
+// Cascade: normalised features (feature_module.c:67-73) of the listed
+// segments' frames that come 2 or more frames after the net's reset, from the
+// shared log-Mel ring; one thread per 8 features.
+__global__ __launch_bounds__(256) void seg_norm_kernel(FeArgs a) {
+    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (unsigned)a.n_list;
+    if (a.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *a.n_list_rec = (int32_t)nrow;
+    const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    const unsigned long long n = (unsigned long long)nrow * W * 5;
+    for (unsigned long long x = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; x < n;
+         x += (unsigned long long)gridDim.x * blockDim.x) {
+        const unsigned part = (unsigned)(x % 5), rk = (unsigned)(x / 5);
+        const unsigned i = rk / W, k = rk - i * W;
+        const int s = a.list[i];
+        const int b = a.seg_begin[s], t = b + (int)k;
+        if (t >= a.T || (int)k + a.fresh[s] < 2) continue;
+        const unsigned slot = (unsigned)(a.abs0 + t - a.lookback + a.ring) % (unsigned)a.ring;
+        const int4* src = reinterpret_cast<const int4*>(a.lmel + ((size_t)s * a.ring + slot) * 40 + 8 * part);
+        const int4 l0 = src[0], l1 = src[1];
+        const int32_t lg[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+        int16_t o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t d = (int64_t)lg[j] - a.mean[8 * part + j];
+            o[j] = sat16((d * a.stdR[8 * part + j]) >> a.norm_shift);
+        }
+        int4 w;
+        w.x = (int32_t)((uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16));
+        w.y = (int32_t)((uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16));
+        w.z = (int32_t)((uint32_t)(uint16_t)o[4] | ((uint32_t)(uint16_t)o[5] << 16));
+        w.w = (int32_t)((uint32_t)(uint16_t)o[6] | ((uint32_t)(uint16_t)o[7] << 16));
+        *reinterpret_cast<int4*>(a.feats + ((size_t)s * a.T + t) * 40 + 8 * part) = w;
+    }
+}
+
+// log-Mel of silence: mel 0 -> log10_vec's x == 0 -> 1 (fixlog10.c:56)
+__global__ __launch_bounds__(256) void lmel_fill_kernel(int32_t* lmel, int ring, const uint8_t* mask, int S) {
+    const int s = blockIdx.x;
+    if (s >= S || (mask && !mask[s])) return;
+    const int32_t v = log10_q15(0);
+    for (int i = threadIdx.x; i < ring * 40; i += blockDim.x) lmel[(size_t)s * ring * 40 + i] = v;
+}
+
 // ============================================================================
 // Stage kernels (legacy scalar API + per-stage parity tests)
 // ============================================================================
@@ -746,13 +808,31 @@ static int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 extern "C" {
 
 int nnspk_launch_fe(const FeArgs* a, void* stream) {
-    const int nrow = a->list ? a->n_list : a->S;
+    const int nrow = a->n_list_dev ? a->S : (a->list ? a->n_list : a->S);
     if (nrow <= 0 || a->T <= 0) return 0;
-    const int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
+    int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
+    if (a->mode == FE_MODE_COLD && W > 2) W = 2;
     const long long nfr = (long long)nrow * W;
     long long blocks = (nfr + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
+    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 1024) blocks = 1024;   // a few frames per switch
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_seg_norm(const FeArgs* a, void* stream) {
+    const int nrow = a->n_list_dev ? a->S : a->n_list;   // device count: size for the maximum
+    if (nrow <= 0 || a->T <= 0) return 0;
+    const int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
+    long long blocks = ((long long)nrow * W * 5 + 255) / 256;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    hipLaunchKernelGGL(seg_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_lmel_fill(int32_t* lmel, int ring, const uint8_t* mask, int S, void* stream) {
+    if (S <= 0) return 0;
+    hipLaunchKernelGGL(lmel_fill_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, lmel, ring, mask, S);
     return ok(hipGetLastError());
 }
 
@@ -866,6 +946,9 @@ int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }
 int nnspk_event_record(void* e, void* stream) { return ok(hipEventRecord((hipEvent_t)e, (hipStream_t)stream)); }
+int nnspk_stream_wait(void* stream, void* event) {
+    return ok(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+}
 int nnspk_event_elapsed(float* ms, void* a, void* b) {
     return ok(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b));
 }

@@ -168,6 +168,12 @@ class NNSPCascade:
                                                           C.byref(nn), C.byref(n)), "net_stats")
         return f.value, fe.value, nn.value, n.value
 
+    def fe_stats(self) -> float:
+        """Device ms of the shared front end (log-Mel of every frame) in the last chunk."""
+        ms = C.c_float()
+        _lib.check(_lib.lib().nnsp_cascade_last_fe_stats(self.h, C.byref(ms)), "fe_stats")
+        return ms.value
+
     def positions(self) -> np.ndarray:
         pos = np.zeros(self.S, np.int8)
         _lib.check(_lib.lib().nnsp_cascade_positions(self.h, _lib.ptr(pos)), "positions")
