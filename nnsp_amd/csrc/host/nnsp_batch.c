@@ -57,17 +57,28 @@ static void plan_fast(nnsp_batch *b)
     b->ep_proj = g->L[li].ep_off + 16 * g->L[li].nrt;
     b->ep_rec_lo = g->L[li].ep_off;
     b->ep_rec_n = b->im.rows_total - g->L[li].ep_off;
-    if (nnspk_fast_lds_bytes(0, a_proj, 4, b->ep_proj) > LDS_MAX) return;
-    if (nnspk_fast_lds_bytes(1, a_rec, 1, b->ep_rec_n) > LDS_MAX) return;
+    const int shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
+    const size_t proj_lds = nnspk_fast_lds_bytes(0, a_proj, 4, b->ep_proj, shape);
+    if (proj_lds > LDS_MAX) return;
+    if (nnspk_fast_lds_bytes(1, a_rec, 1, b->ep_rec_n, shape) > LDS_MAX) return;
     /* tiles per 4-wave group in one workgroup: 2 once there are >= 2 tiles per CU */
     const int tiles = (b->S + 15) / 16;
-    b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2, b->ep_rec_n) <= LDS_MAX) ? 2 : 1;
+    b->rec_waves = (tiles >= 512 && nnspk_fast_lds_bytes(1, a_rec, 2, b->ep_rec_n, shape) <= LDS_MAX) ? 2 : 1;
     b->li = li;
-    b->shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
+    b->shape = shape;
     b->nstep_max = (b->Tmax + 1) / 2;
+    /* proj: a persistent grid of as many 4-wave workgroups as fit on the
+     * device at once (LDS-bound, at most 8 per CU) */
+    int cus = 256, clk = 0;
+    char arch[64];
+    if (nnspk_device_info(&cus, &clk, arch, (int)sizeof arch) || cus <= 0) cus = 256;
+    int per_cu = (int)(LDS_MAX / proj_lds);
+    if (per_cu > 8) per_cu = 8;
+    if (per_cu < 1) per_cu = 1;
     const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);
     long long blocks = (ptiles + 3) / 4;
-    b->proj_blocks = (int)(blocks < 256 ? blocks : 256);
+    const long long cap = (long long)cus * per_cu;
+    b->proj_blocks = (int)(blocks < cap ? blocks : cap);
     b->fast = 1;
 }
 

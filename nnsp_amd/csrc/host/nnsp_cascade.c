@@ -47,7 +47,7 @@ struct nnsp_cascade {
     unsigned long long *d_frames;
     int16_t *d_trig[3], *d_out3[3];
     uint8_t *d_mask[3];
-    int32_t *d_list[3];
+    int32_t *d_list[3], *d_cold_list[3];
     int16_t *d_hist[2];
     int hist_cur;
     int32_t *d_lmel;                /* [S][ring][40] shared log-Mel */
@@ -130,7 +130,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     }
     if ((e = nnspk_malloc((void **)&c->d_st, S * sizeof(CascState)))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_counts, 9 * 4))) goto fail;   /* 3 rounds in flight x 3 nets */
+    /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
+    if ((e = nnspk_malloc((void **)&c->d_counts, 18 * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_rcount, MAX_TIMED * 3 * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_last_round, 4))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
@@ -143,6 +144,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         if ((e = nnspk_malloc((void **)&c->d_out3[i], S * T * 6))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_mask[i], S))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_list[i], S * 4))) goto fail;
+        if ((e = nnspk_malloc((void **)&c->d_cold_list[i], S * 4))) goto fail;
         if ((e = nnspk_memset(c->d_mask[i], 0, S, c->stream))) goto fail;
     }
     for (int i = 0; i < 2; ++i)
@@ -172,6 +174,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             a->post[i] = nets[i]->d_post;
             a->prev_default[i] = c->d_pdef + 40 * i;
             a->list[i] = c->d_list[i];
+            a->cold_list[i] = c->d_cold_list[i];
         }
     }
     {   /* the reset context value of each net: FeatureClass_setDefault on a scratch stream */
@@ -211,7 +214,8 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
                     c->d_trig[2], c->d_out3[0],   c->d_out3[1], c->d_out3[2], c->d_mask[0], c->d_mask[1],
                     c->d_mask[2], c->d_list[0],   c->d_list[1], c->d_list[2], c->d_hist[0], c->d_hist[1],
                     c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
-                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round};
+                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round, c->d_cold_list[0],
+                    c->d_cold_list[1], c->d_cold_list[2]};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 2; ++i) {
         nnspk_event_destroy(c->ev[i]);
@@ -248,7 +252,7 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 
 /* features of net n for this round's segments: normalised shared log-Mel,
  * and the full front end for the frames right after the net's reset */
-static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *n_list_dev,
+static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *cnt,
                             int32_t *n_list_rec, const int16_t *hist, void *stream)
 {
     nnsp_batch *b = c->net[n];
@@ -262,7 +266,7 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.norm_shift = b->norm_shift;
     fa.feats = b->d_feats;
     fa.list = c->d_list[n];
-    fa.n_list_dev = n_list_dev;
+    fa.n_list_dev = cnt + n;
     fa.n_list_rec = n_list_rec;
     fa.seg_begin = c->d_seg_begin;
     fa.lookback = c->lookback[n];
@@ -275,6 +279,8 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.fresh = c->d_fresh;
     TRY(nnspk_launch_seg_norm(&fa, stream));
     fa.mode = FE_MODE_COLD;
+    fa.list = c->d_cold_list[n];
+    fa.n_list_dev = cnt + 3 + n;
     fa.n_list_rec = NULL;
     return nnspk_launch_fe(&fa, stream);
 }
@@ -283,14 +289,14 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
  * (empty lists exit on the device), then casc_control on the main stream. */
 static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm, int T, const int16_t *hist)
 {
-    int32_t *cur = c->d_counts + 3 * (r % 3);
+    int32_t *cur = c->d_counts + 6 * (r % 3);
     TRY(nnspk_event_record(c->ev_fork, c->stream));
     for (int n = 0; n < 3; ++n) {
         void *st = c->ns[n];
         const int timed = r < MAX_TIMED;
         TRY(nnspk_stream_wait(st, c->ev_fork));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
-        TRY(segment_features(c, n, pcm, T, cur + n, timed ? c->d_rcount + 3 * r + n : NULL, hist, st));
+        TRY(segment_features(c, n, pcm, T, cur, timed ? c->d_rcount + 3 * r + n : NULL, hist, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
         nnsp_segment seg;
         memset(&seg, 0, sizeof seg);
@@ -307,8 +313,8 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         TRY(nnspk_event_record(c->ev_join[n], st));
         TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
     }
-    a->counts = c->d_counts + 3 * ((r + 1) % 3);
-    a->counts_clear = c->d_counts + 3 * ((r + 2) % 3);
+    a->counts = c->d_counts + 6 * ((r + 1) % 3);
+    a->counts_clear = c->d_counts + 6 * ((r + 2) % 3);
     a->round = r;
     return nnspk_launch_casc_control(a, c->stream);
 }
@@ -327,7 +333,7 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     a.detected = detected;
     a.outputs3 = outputs3;
     TRY(nnspk_event_record(c->ev[0], c->stream));
-    TRY(nnspk_memset(c->d_counts, 0, 9 * 4, c->stream));
+    TRY(nnspk_memset(c->d_counts, 0, 18 * 4, c->stream));
     TRY(nnspk_memset(c->d_frames, 0, 3 * 8, c->stream));
     TRY(nnspk_memset(c->d_last_round, 0, 4, c->stream));
     TRY(nnspk_memset(c->d_rcount, 0, MAX_TIMED * 3 * 4, c->stream));
@@ -357,7 +363,7 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     for (;;) {
         for (; r < R; ++r) TRY(launch_round(c, &a, r, pcm, T, hist));
         int32_t cnt[3];
-        TRY(nnspk_d2h(cnt, c->d_counts + 3 * (r % 3), 12, c->stream));
+        TRY(nnspk_d2h(cnt, c->d_counts + 6 * (r % 3), 12, c->stream));
         TRY(nnspk_sync(c->stream));
         if (cnt[0] + cnt[1] + cnt[2] == 0) break;
         R = r + 2;

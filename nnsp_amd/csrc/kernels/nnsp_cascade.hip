@@ -22,7 +22,7 @@ namespace {
 inline int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 // Append s to list[n] for every lane with want; one atomic per wave and net.
-__device__ __forceinline__ void list_push(const CascArgs& a, int n, int s, bool want) {
+__device__ __forceinline__ void list_push(int32_t* const* lists, int32_t* counts, int n, int s, bool want) {
     const int lane = threadIdx.x & 63;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -31,10 +31,18 @@ __device__ __forceinline__ void list_push(const CascArgs& a, int n, int s, bool 
         if (!m) continue;
         const int leader = __ffsll((long long)m) - 1;
         int base = 0;
-        if (lane == leader) base = atomicAdd(&a.counts[k], __popcll(m));
+        if (lane == leader) base = atomicAdd(&counts[k], __popcll(m));
         base = __shfl(base, leader);
-        if (mine) a.list[k][base + __popcll(m & ((1ull << lane) - 1ull))] = s;
+        if (mine) lists[k][base + __popcll(m & ((1ull << lane) - 1ull))] = s;
     }
+}
+
+// list s under net n for the next round; also on n's cold list while the
+// net's STFT buffer still holds zeros from its reset (the front end runs in
+// full for those frames)
+__device__ __forceinline__ void list_next(const CascArgs& a, int n, int s, bool want, int fresh) {
+    list_push(a.list, a.counts, n, s, want);
+    list_push(a.cold_list, a.counts + 3, n, s, want && fresh < 2);
 }
 
 __device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned long long v) {
@@ -50,21 +58,22 @@ __device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned lo
 __global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     const bool ok_s = s < a.S;
-    int n = 0;
+    int n = 0, fr = 2;
     if (ok_s) {
         a.seg_begin[s] = 0;
         n = a.seq[a.st[s].pos];
+        fr = a.fresh[s];
     }
-    list_push(a, n, s, ok_s);
+    list_next(a, n, s, ok_s, fr);
     add_frames(a, n, ok_s ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, a.T) : a.T) : 0ull);
 }
 
 __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < 3 && a.counts_clear) a.counts_clear[s] = 0;
+    if (s < 6 && a.counts_clear) a.counts_clear[s] = 0;
     const int T = a.T;
     bool want = false;
-    int n_next = 0, b_next = T;
+    int n_next = 0, b_next = T, fr_next = 2;
     if (s < a.S && a.seg_begin[s] < T) {
         const int b = a.seg_begin[s];
         const int e = a.seg_len > 0 ? min(T, b + a.seg_len) : T;   // this round's segment b..e-1
@@ -119,7 +128,8 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
         }
         // frames since the reset of the net the stream runs next round (the
         // front end's STFT buffer is zero right after NNSPClass_reset)
-        a.fresh[s] = (int8_t)(cut >= 0 ? 0 : min(2, (int)a.fresh[s] + (e - b)));
+        fr_next = cut >= 0 ? 0 : min(2, (int)a.fresh[s] + (e - b));
+        a.fresh[s] = (int8_t)fr_next;
         if (cut >= 0) {
             // NNSPClass_reset of the departing net (nn_speech.c:57-72):
             // FeatureClass_setDefault -- context slots 0..4 := the default,
@@ -158,7 +168,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
             n_next = a.seq[st.pos];
         }
     }
-    list_push(a, n_next, s, want);
+    list_next(a, n_next, s, want, fr_next);
     if (a.last_round && __ballot(want) && (threadIdx.x & 63) == 0) atomicMax(a.last_round, a.round + 1);
     add_frames(a, n_next,
                want ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, T - b_next) : T - b_next) : 0ull);

@@ -151,9 +151,15 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 // ---------------------------------------------------------------------------
 // proj_kernel
 // ---------------------------------------------------------------------------
-struct ProjWave {
+// Per-wave LDS of proj.  The compiled shapes keep one activation buffer as
+// wide as the LSTM input's K tiles (+8: rows 16 B apart modulo 256 B); the
+// generic shape ping-pongs two full-width buffers across its prefix layers.
+template <class SH>
+struct alignas(16) ProjWave {
+    static constexpr int AS = SH::generic ? P_ASTRIDE : 64 * SH::NKR + 8;
+    static constexpr int NA = SH::generic ? 2 : 1;
     int16_t uni[P_UNION + 32];
-    int16_t act[2][16][P_ASTRIDE];
+    int16_t act[NA][16][AS];
 };
 
 template <class SH, bool ACC32>
@@ -162,14 +168,15 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
-    ProjWave* pw = reinterpret_cast<ProjWave*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    using PW = ProjWave<SH>;
+    PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, false);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     __syncthreads();
     constexpr bool GEN = SH::generic;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    ProjWave& P = pw[wv];
+    PW& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
     const NnLayer& LL = img.L[r.li];
     const int nrt = GEN ? LL.nrt : SH::NRT;
@@ -205,19 +212,19 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
         if (!GEN) {   // one tanh FC layer, K = 240
             const NnLayer& L0 = img.L[0];
             fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
-                                                          in, in_stride, &P.act[0][0][0], P_ASTRIDE, tt, lane);
+                                                          in, in_stride, &P.act[0][0][0], PW::AS, tt, lane);
             wave_lds_sync();
             in = &P.act[0][0][0];
-            in_stride = P_ASTRIDE;
+            in_stride = PW::AS;
         } else {
             for (int i = 0; i < r.li; ++i) {
                 const NnLayer& Ly = img.L[i];
-                int16_t* out = &P.act[i & 1][0][0];
+                int16_t* out = &P.act[i & (PW::NA - 1)][0][0];
                 fc_layer<ACC32, 0, 0, -1, 0, 4>(Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in,
-                                                in_stride, out, P_ASTRIDE, tt, lane);
+                                                in_stride, out, PW::AS, tt, lane);
                 wave_lds_sync();
                 in = out;
-                in_stride = P_ASTRIDE;
+                in_stride = PW::AS;
             }
         }
         // ---- LSTM input half: gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
@@ -273,10 +280,15 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
 #define RG 4
 #define RW (RG + 1)
 
-struct RecTile {
-    int16_t h[2][16][R_STRIDE];     // LSTM h, ping-pong across steps
-    int16_t act[2][16][R_STRIDE];   // tail wave: FC activations, ping-pong across layers
-    int32_t c[16][R_CW];
+// Per-tile LDS of recur; compiled shapes size the rows to their K tiles and
+// the cell state to N (the generic shape to the widest net).
+template <class SH>
+struct alignas(16) RecTile {
+    static constexpr int RS = SH::generic ? R_STRIDE : 64 * SH::NKR + 8;
+    static constexpr int CW = SH::generic ? R_CW : (SH::NW + 3) / 4 * 4;
+    int16_t h[2][16][RS];     // LSTM h, ping-pong across steps
+    int16_t act[2][16][RS];   // tail wave: FC activations, ping-pong across layers
+    int32_t c[16][CW];
     int32_t phase[16];
     int32_t nst[16];    // NN steps of each stream's segment
     int32_t beg[16];    // segment start frame
@@ -300,7 +312,9 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
-    RecTile* tiles = reinterpret_cast<RecTile*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    using RT = RecTile<SH>;
+    constexpr int R_STRIDE_ = RT::RS;
+    RT* tiles = reinterpret_cast<RT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
@@ -308,7 +322,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     const int tpw = blockDim.x / (64 * RW);
     const int tl = wv / RW, g = wv - tl * RW;   // tile in workgroup, wave in tile
     const bool tail = g == RG;
-    RecTile& R = tiles[tl];
+    RT& R = tiles[tl];
     const int sc = lane & 15, q = lane >> 4;
     const int i0 = (blockIdx.x * tpw + tl) * 16;
     auto sid = [&](int i) { return r.list ? r.list[i] : i; };
@@ -377,7 +391,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                 const int t = b + 2 * j + phase;
                 const bool active = valid && t < e;
                 v4i bh[2], bl[2];
-                load_b<2>(&R.h[cur][0][0], R_STRIDE, nkt_r, lane, bh, bl);
+                load_b<2>(&R.h[cur][0][0], R_STRIDE_, nkt_r, lane, bh, bl);
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
                     const int rt = g + RG * k;
@@ -431,18 +445,18 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                 const NnLayer& L3 = img.L[r.li + 2];
                 const NnLayer& L4 = img.L[r.li + 3];
                 fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, 2>(
-                    L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), in, R_STRIDE, &R.act[0][0][0],
-                    R_STRIDE, tt, lane);
+                    L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), in, R_STRIDE_, &R.act[0][0][0],
+                    R_STRIDE_, tt, lane);
                 wave_lds_sync();
                 PROBE(3);
                 fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, 2>(
-                    L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.act[0][0][0], R_STRIDE,
-                    &R.act[1][0][0], R_STRIDE, tt, lane);
+                    L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.act[0][0][0], R_STRIDE_,
+                    &R.act[1][0][0], R_STRIDE_, tt, lane);
                 wave_lds_sync();
                 PROBE(4);
                 fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, 2>(
-                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.act[1][0][0], R_STRIDE,
-                    &R.act[0][0][0], R_STRIDE, tt, lane);
+                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.act[1][0][0], R_STRIDE_,
+                    &R.act[0][0][0], R_STRIDE_, tt, lane);
                 wave_lds_sync();
                 PROBE(5);
                 in = &R.act[0][0][0];
@@ -452,14 +466,14 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                     const NnLayer& Ly = img.L[i];
                     int16_t* out = &R.act[ab][0][0];
                     fc_layer<ACC32, 0, 0, -1, 0, 2>(Ly, W + (Ly.a_off - r.a_off), ep + (Ly.ep_off - r.ep_lo), in,
-                                                    R_STRIDE, out, R_STRIDE, tt, lane);
+                                                    R_STRIDE_, out, R_STRIDE_, tt, lane);
                     wave_lds_sync();
                     in = out;
                     ab ^= 1;
                 }
             }
             // outputs and post-processing (nn_speech.c:92-124)
-            const int16_t* fin = in + sc * R_STRIDE;
+            const int16_t* fin = in + sc * R_STRIDE_;
             const NnLayer& LO = img.L[img.nl - 1];
             const int nout = GEN ? LO.N : SH::NOUT;
             const bool lin = GEN ? LO.act == ACT_LINEAR : true;
@@ -582,20 +596,26 @@ int launch(const void* fn, dim3 grid, dim3 blk, size_t lds, void* stream, const 
 
 extern "C" {
 
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows) {
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape) {
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
     const size_t base = (size_t)a_bytes + 768 + ep_bytes(ep_rows);
-    if (which == 0) return base + (size_t)units * sizeof(ProjWave);
-    return base + (size_t)units * sizeof(RecTile);
+    size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
+    switch (shape) {
+        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(RecTile<ShapeVad>); break;
+        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(RecTile<ShapeKws>); break;
+        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(RecTile<ShapeS2i>); break;
+        default: break;
+    }
+    return base + (size_t)units * (which == 0 ? pw : rt);
 }
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n);
+    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n, r->shape);
     return launch(pick_proj(r->shape, img->acc32), dim3(blocks), dim3(256), lds, stream, img, r);
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n);
+    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n, r->shape);
     const int nrow = r->n_list_dev ? r->S : (r->list ? r->n_list : r->S);
     if (nrow <= 0) return 0;
     const int tiles = (nrow + 15) / 16;

@@ -154,7 +154,7 @@ int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
                             void *stream);
 int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
                             int n, void *stream);
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows);
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape);
 int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, void *stream);
 int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, void *stream);
 int nnspk_set_lds_limit(void);
@@ -202,8 +202,9 @@ typedef struct {
     void *post[3];            /* per net id: [S] NnPost */
     const int16_t *prev_default[3]; /* per net id: [40] FeatureClass_setDefault context value */
     int32_t *list[3];         /* per net id: next round's streams */
-    int32_t *counts;          /* [3] next round's list lengths (appended to) */
-    int32_t *counts_clear;    /* [3] zeroed by casc_control: the round after next appends there */
+    int32_t *cold_list[3];    /* per net id: those of them within 2 frames of the net's reset */
+    int32_t *counts;          /* [6] next round's list lengths (appended to): lists, cold lists */
+    int32_t *counts_clear;    /* [6] zeroed by casc_control: the round after next appends there */
     int32_t *last_round;      /* atomicMax'ed with round + 1 when a stream is listed for it */
     int32_t round;            /* index of the round casc_control closes */
     unsigned long long *frames; /* [3] frames scheduled per net id (speculation included) */

@@ -182,6 +182,14 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
     __shared__ int64_t Ms[4][64];
     __shared__ __attribute__((aligned(16))) FeTables TB;
+    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
+    const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    const bool cold = a.mode == FE_MODE_COLD;
+    const unsigned W = cold ? (segW < 2u ? segW : 2u) : segW;
+    const unsigned nfr = nrow * W;   // host guarantees < 2^31
+    const unsigned nw = gridDim.x * 4u;
+    const unsigned per = (nfr + nw - 1) / nw;
+    if (blockIdx.x * 4u * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
     fe_tables_init(TB);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -193,13 +201,7 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
-    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
-    const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
-    const bool cold = a.mode == FE_MODE_COLD;
-    const unsigned W = cold ? (segW < 2u ? segW : 2u) : segW;
-    const unsigned nfr = nrow * W;   // host guarantees < 2^31
-    const unsigned nw = gridDim.x * 4u, wid = blockIdx.x * 4u + (unsigned)wv;
-    const unsigned per = (nfr + nw - 1) / nw;
+    const unsigned wid = blockIdx.x * 4u + (unsigned)wv;
     const unsigned fbeg = wid * per;
     const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
     // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
@@ -815,7 +817,7 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     const long long nfr = (long long)nrow * W;
     long long blocks = (nfr + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
-    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 1024) blocks = 1024;   // a few frames per switch
+    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 512) blocks = 512;   // at most 2 frames per switch
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
     return ok(hipGetLastError());
 }
