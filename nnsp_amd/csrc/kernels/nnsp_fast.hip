@@ -140,7 +140,58 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
             }
         }
     };
-    if constexpr (NRT > 0) {
+    if constexpr (NRT > 0 && NKT > 0) {
+        // compiled shape: the LDS loads of a group of row tiles (A fragments,
+        // epilogue constants) are issued before the group's first output
+        // store -- the compiler cannot move loads across stores into the same
+        // LDS, so a per-tile load/compute/store order would expose the full
+        // latency per tile; groups of <= 3 tiles bound the registers
+        constexpr int CH = NRT < 3 ? NRT : 3;
+#pragma unroll
+        for (int r0 = 0; r0 < NRT; r0 += CH) {
+            v4i w[CH][NKT];
+            int64_t cst[CH][4];
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                const int rt = r0 + c;
+                if (rt < NRT) {
+#pragma unroll
+                    for (int kt = 0; kt < NKT; ++kt)
+                        w[c][kt] = *reinterpret_cast<const v4i*>(A + (size_t)(rt * NKT + kt) * 1024 + 16 * lane);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = 16 * rt + 4 * q + i;
+                        cst[c][i] = row < rows ? ep[row].cst : 0;
+                    }
+                }
+            }
+            v4i ah[CH], al[CH];
+#pragma unroll
+            for (int c = 0; c < CH; ++c) {
+                ah[c] = v4i{0, 0, 0, 0};
+                al[c] = v4i{0, 0, 0, 0};
+                if (r0 + c < NRT)
+#pragma unroll
+                    for (int kt = 0; kt < NKT; ++kt) {
+                        ah[c] = mfma8(w[c][kt], bh[kt], ah[c]);
+                        al[c] = mfma8(w[c][kt], bl[kt], al[c]);
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int row = 16 * (r0 + c) + 4 * q + i;
+                    if (r0 + c < NRT && row < rows) {
+                        const int32_t v = ep_out<ACC32>((ah[c][i] << 8) + al[c][i], cst[c][i], rsh, lsh);
+                        if (act == ACT_LINEAR)
+                            reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
+                        else
+                            out[sc * out_stride + row] = act16(act, v, tt);
+                    }
+                }
+        }
+    } else if constexpr (NRT > 0) {
 #pragma unroll
         for (int rt = 0; rt < NRT; ++rt) tile(rt);
     } else {
@@ -549,6 +600,286 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
 }
 
 // ---------------------------------------------------------------------------
+// recur_pipe_kernel (the compiled shapes): one 16-stream tile per workgroup of
+// RG LSTM waves and 3 tail waves, a 4-stage pipeline across NN steps:
+//   LSTM waves  iteration j: step j   -- Wh.h + gx, gate epilogue, cell and
+//                                        hidden update (lstm.c:48-124)
+//   tail wave 1 iteration j: step j-1 -- FC relu6  (h  -> a2)
+//   tail wave 2 iteration j: step j-2 -- FC relu6  (a2 -> a3)
+//   tail wave 3 iteration j: step j-3 -- FC linear (a3 -> logits), outputs,
+//                                        post-processing, trigger stores
+// Only the LSTM stage is recurrent; the FC stages hang off it one step apart,
+// so a step costs the slowest stage instead of their sum.  One workgroup
+// barrier per iteration; h, a2 and a3 are double-buffered by iteration
+// parity (stage k reads what stage k-1 wrote one iteration earlier, and that
+// buffer is rewritten only after the next barrier).
+// ---------------------------------------------------------------------------
+template <class SH>
+struct PipeCfg {
+    static constexpr int LW = SH::NRT <= 8 ? 4 : (SH::NRT + 1) / 2;   // LSTM waves: <= 2 row tiles each
+    static constexpr int RPW = (SH::NRT + LW - 1) / LW;      // LSTM row tiles per wave
+    static constexpr int NWV = LW + 3;                       // waves per workgroup
+};
+
+template <class SH>
+struct alignas(16) PipeTile {
+    static constexpr int RS = 64 * SH::NKR + 8;
+    static constexpr int CW = (SH::NW + 3) / 4 * 4;
+    int16_t h[2][16][RS];
+    int16_t a2[2][16][RS];
+    int16_t a3[2][16][RS];
+    int16_t a4[16][RS];       // stage 3: int32 logits
+    int32_t c[16][CW];
+    int32_t phase[16];
+    int32_t nst[16];          // NN steps of each stream's segment
+    int32_t beg[16];          // segment start frame
+    int32_t end[16];          // segment end frame (exclusive)
+};
+
+template <class SH, bool ACC32>
+__global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRun r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    using CF = PipeCfg<SH>;
+    using PT = PipeTile<SH>;
+    constexpr int RGP = CF::LW, RPW = CF::RPW, RS = PT::RS;
+    constexpr int N = SH::NW, nrt = SH::NRT, nkt_r = SH::NKR;
+    const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
+    const int i0 = blockIdx.x * 16;   // tile = 16 consecutive entries of the stream list
+    if (i0 >= nrow) return;
+    uint8_t* W = smem;
+    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
+    PT& R = *reinterpret_cast<PT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    stage_ep(ep, img, r.ep_lo, r.ep_n, true);
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    const int lane = threadIdx.x & 63;
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // < RGP: LSTM wave; then stages 1..3
+    const int sc = lane & 15, q = lane >> 4;
+    auto sid = [&](int i) { return r.list ? r.list[i] : i; };
+    const bool valid = i0 + sc < nrow;
+    const int s = valid ? sid(i0 + sc) : 0;
+    const NnLayer& LL = img.L[r.li];
+    constexpr int rows = 16 * nrt;
+    const int xs_sh = LL.xs_sh, rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
+    for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
+        const int st = idx / N, u = idx - st * N;
+        const bool ok = i0 + st < nrow;
+        const int gs = ok ? sid(i0 + st) : 0;
+        R.h[0][st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
+        R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
+    }
+    const int T = r.T;
+    const bool post_w = g == RGP + 2;
+    PostState ps = {};
+    if (post_w && lane < 16) {
+        const int b = valid && r.seg_begin ? r.seg_begin[s] : 0;
+        const int e = r.seg_len > 0 ? min(T, b + r.seg_len) : T;
+        if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
+        const int ph = valid ? 1 - ps.slides : 0;
+        R.phase[lane] = ph;
+        R.beg[lane] = b;
+        R.end[lane] = e;
+        R.nst[lane] = valid && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
+    }
+    __syncthreads();
+    const int phase = R.phase[sc];
+    const int b = R.beg[sc];
+    const int e = R.end[sc];   // segment: frames b..e-1
+    int nsteps = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
+    if (post_w && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
+        if (r.trig) r.trig[(size_t)s * T + b] = ps.trigger;
+        if (r.out3)
+            for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
+    }
+    const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
+    const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
+    v4i gxv[RPW];
+    auto load_gx = [&](int jj) {
+        const bool ok = valid && b + 2 * jj + phase < e;
+        const int32_t* gsrc = r.gx + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * rows + 4 * q;
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int rt = g + RGP * k;
+            if (rt < nrt) gxv[k] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
+        }
+    };
+    if (g < RGP) load_gx(0);
+    const NnLayer& L2 = img.L[r.li + 1];
+    const NnLayer& L3 = img.L[r.li + 2];
+    const NnLayer& L4 = img.L[r.li + 3];
+    // development probe (NNSP_RECUR_CLOCKS): s_memtime at the start and end of each
+    // iteration's work of LSTM wave 0 and the three stage waves, tile 0
+    long long* clk = (r.dbg_clk && blockIdx.x == 0 && lane == 0 && (g == 0 || g >= RGP))
+                         ? r.dbg_clk + 2 * (g == 0 ? 0 : g - RGP + 1)
+                         : nullptr;
+    for (int j = 0; j < nsteps + 3; ++j) {
+        const int cur = j & 1;
+        if (clk && j < 64) clk[j * 16] = (long long)__builtin_amdgcn_s_memtime();
+        if (g < RGP) {
+            if (j < nsteps) {
+                // ---- LSTM step j: row tile = 4 units x gates i, j, f, o
+                const int t = b + 2 * j + phase;
+                const bool active = valid && t < e;
+                v4i bh[nkt_r], bl[nkt_r];
+                load_b<nkt_r>(&R.h[cur][0][0], RS, nkt_r, lane, bh, bl);
+                // every LDS load of the step (A fragments, epilogue constants,
+                // cell state, the previous h kept for inactive streams) before
+                // the first store: loads cannot be moved across LDS stores
+                v4i w[RPW][nkt_r];
+                int64_t cst[RPW][4];
+                int32_t c_old[RPW];
+                int16_t h_old[RPW];
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) {
+                    const int rt = g + RGP * k;
+                    const int u = 4 * rt + q;
+                    if (rt < nrt) {
+#pragma unroll
+                        for (int kt = 0; kt < nkt_r; ++kt)
+                            w[k][kt] = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * nkt_r + kt) * 1024 + 16 * lane);
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) cst[k][i] = epl[16 * rt + i].cst;
+                        c_old[k] = u < N ? R.c[sc][u] : 0;
+                        h_old[k] = u < N ? R.h[cur][sc][u] : (int16_t)0;
+                    }
+                }
+                v4i hh[RPW], hl[RPW];
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) {
+                    hh[k] = v4i{0, 0, 0, 0};
+                    hl[k] = v4i{0, 0, 0, 0};
+                    if (g + RGP * k < nrt)
+#pragma unroll
+                        for (int kt = 0; kt < nkt_r; ++kt) {
+                            hh[k] = mfma8(w[k][kt], bh[kt], hh[k]);
+                            hl[k] = mfma8(w[k][kt], bl[kt], hl[k]);
+                        }
+                }
+                int32_t c_new[RPW];
+                int16_t hv[RPW];
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) {
+                    const int rt = g + RGP * k;
+                    c_new[k] = 0;
+                    hv[k] = 0;
+                    if (rt < nrt && 4 * rt + q < N) {
+                        int16_t gt[4];
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const int32_t sx = gxv[k][i];
+                            const int32_t hx = (hh[k][i] << 8) + hl[k][i];
+                            int32_t v;
+                            if (ACC32) {
+                                const int32_t x = __builtin_expect(xs_sh != 0, 0) ? shift32(sx, xs_sh) : sx;
+                                v = ep_out<true>(wadd(x, hx), cst[k][i], rsh, lsh);
+                            } else {
+                                const int64_t x = __builtin_expect(xs_sh != 0, 0) ? shift64((int64_t)sx, xs_sh)
+                                                                                  : (int64_t)sx;
+                                const int64_t pre = x + hx + cst[k][i];
+                                v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
+                            }
+                            gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                        }
+                        c_new[k] = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old[k]) >> 15);
+                        hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < RPW; ++k) {
+                    const int rt = g + RGP * k;
+                    const int u = 4 * rt + q;
+                    if (rt < nrt && u < N) {
+                        if (active) R.c[sc][u] = c_new[k];
+                        R.h[cur ^ 1][sc][u] = active ? hv[k] : h_old[k];   // h after all groups (T6)
+                    }
+                }
+                if (j + 1 < nsteps) load_gx(j + 1);
+            }
+        } else if (g == RGP) {   // stage 1: step j-1
+            if (j >= 1 && j - 1 < nsteps)
+                fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
+                    L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
+                    RS, tt, lane);
+        } else if (g == RGP + 1) {   // stage 2: step j-2
+            if (j >= 2 && j - 2 < nsteps)
+                fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
+                    L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
+                    &R.a3[cur][0][0], RS, tt, lane);
+        } else if (j >= 3 && j - 3 < nsteps) {   // stage 3: step j-3
+            const int jj = j - 3;
+            const int t = b + 2 * jj + phase;
+            const bool active = valid && t < e;
+            fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
+                L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS, &R.a4[0][0], RS,
+                tt, lane);
+            wave_lds_sync();
+            // outputs and post-processing (nn_speech.c:92-124)
+            const int32_t* f32 = reinterpret_cast<const int32_t*>(&R.a4[sc][0]);
+            if (active && r.logits) {
+                int32_t* dst = r.logits + ((size_t)s * T + t) * SH::NOUT;
+                for (int o = q; o < SH::NOUT; o += 4) dst[o] = f32[o];
+            }
+            if (lane < 16 && active) {
+                RegLogits<SH::NOUT> lg;
+#pragma unroll
+                for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
+                post_proc(ps, img, lg);
+                if (r.trig) {
+                    r.trig[(size_t)s * T + t] = ps.trigger;
+                    if (t + 1 < e) r.trig[(size_t)s * T + t + 1] = ps.trigger;
+                }
+                if (r.out3)
+                    for (int f = t; f < min(t + 2, e); ++f)
+                        for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + f) * 3 + o] = ps.outputs[o];
+            }
+        }
+        if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
+        __syncthreads();
+    }
+    // ---- state out: LSTM step nsteps-1 wrote h[nsteps & 1]
+    const int hb = nsteps & 1;
+    for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
+        const int st = idx / N, u = idx - st * N;
+        if (i0 + st < nrow) {
+            const int gs = sid(i0 + st);
+            r.h[(size_t)gs * NN_MAX_W + u] = R.h[hb][st][u];
+            r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
+        }
+    }
+    if (post_w && lane < 16 && valid && b < e) {
+        ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
+        reinterpret_cast<PostState*>(r.post)[s] = ps;
+    }
+    // ---- feature context (normFeatContext slots 1..5) := last 5 of prev5 ++ feats[b..e):
+    // all of the tile's reads before any write (a stream's old slots feed its new ones)
+    int4 cv[2];
+    int ci[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int idx = threadIdx.x + (int)blockDim.x * k;   // (stream in tile, 16-byte chunk of 5x40)
+        ci[k] = -1;
+        if (idx < 16 * 25 && i0 + idx / 25 < nrow) {
+            const int st = idx / 25, c = idx - st * 25, m = c / 5, part = c - 5 * m;
+            const int L = R.end[st] - R.beg[st];
+            if (L > 0) {
+                const int gs = sid(i0 + st), jx = L + m;
+                cv[k] = jx < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + jx) * 40 + 8 * part)
+                               : *reinterpret_cast<const int4*>(r.feats + ((size_t)gs * T + R.beg[st] + jx - 5) * 40 +
+                                                                8 * part);
+                ci[k] = gs * 25 + c;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+        if (ci[k] >= 0) reinterpret_cast<int4*>(r.prev5)[ci[k]] = cv[k];
+}
+
+// ---------------------------------------------------------------------------
 // launch layer
 // ---------------------------------------------------------------------------
 namespace {
@@ -569,6 +900,21 @@ const void* pick_proj(int shape, bool acc32) {
         case NN_SHAPE_KWS: return proj_fn<ShapeKws>(acc32);
         case NN_SHAPE_S2I: return proj_fn<ShapeS2i>(acc32);
         default: return proj_fn<ShapeGen>(acc32);
+    }
+}
+
+template <class SH>
+const void* pipe_fn(bool acc32) {
+    return acc32 ? (const void*)recur_pipe_kernel<SH, true> : (const void*)recur_pipe_kernel<SH, false>;
+}
+
+// compiled shapes: the pipelined recurrence (one tile per workgroup)
+const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes) {
+    switch (shape) {
+        case NN_SHAPE_VAD: *waves = PipeCfg<ShapeVad>::NWV; *tile_bytes = sizeof(PipeTile<ShapeVad>); return pipe_fn<ShapeVad>(acc32);
+        case NN_SHAPE_KWS: *waves = PipeCfg<ShapeKws>::NWV; *tile_bytes = sizeof(PipeTile<ShapeKws>); return pipe_fn<ShapeKws>(acc32);
+        case NN_SHAPE_S2I: *waves = PipeCfg<ShapeS2i>::NWV; *tile_bytes = sizeof(PipeTile<ShapeS2i>); return pipe_fn<ShapeS2i>(acc32);
+        default: return nullptr;
     }
 }
 
@@ -600,10 +946,10 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int 
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
     const size_t base = (size_t)a_bytes + 768 + ep_bytes(ep_rows);
     size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
-    switch (shape) {
-        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(RecTile<ShapeVad>); break;
-        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(RecTile<ShapeKws>); break;
-        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(RecTile<ShapeS2i>); break;
+    switch (shape) {   // compiled shapes: recur runs one pipelined tile per workgroup
+        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(PipeTile<ShapeVad>); units = which ? 1 : units; break;
+        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(PipeTile<ShapeKws>); units = which ? 1 : units; break;
+        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(PipeTile<ShapeS2i>); units = which ? 1 : units; break;
         default: break;
     }
     return base + (size_t)units * (which == 0 ? pw : rt);
@@ -618,6 +964,10 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stre
     const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n, r->shape);
     const int nrow = r->n_list_dev ? r->S : (r->list ? r->n_list : r->S);
     if (nrow <= 0) return 0;
+    int waves = 0;
+    size_t tb = 0;
+    if (const void* fn = pick_pipe(r->shape, img->acc32, &waves, &tb))
+        return launch(fn, dim3((nrow + 15) / 16), dim3(64 * waves), lds, stream, img, r);
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
     return launch(pick_recur(r->shape, img->L[r->li].nrt, img->acc32), dim3(blocks), dim3(64 * RW * tpw), lds,
@@ -630,9 +980,13 @@ int nnspk_set_lds_limit(void) {
     const int nrts[4] = {8, 16, 20, 32};   // one generic recur instantiation each
     for (int a = 0; a < 2; ++a)
         for (int i = 0; i < 4; ++i) {
-            const void* fns[3] = {pick_proj(shapes[i], a), pick_recur(shapes[i], nrts[i], a),
-                                  pick_recur(NN_SHAPE_GENERIC, nrts[i], a)};
-            for (int k = 0; k < 3; ++k) {
+            int wv = 0;
+            size_t tb = 0;
+            const void* pipe = pick_pipe(shapes[i], a, &wv, &tb);
+            const void* fns[4] = {pick_proj(shapes[i], a), pick_recur(shapes[i], nrts[i], a),
+                                  pick_recur(NN_SHAPE_GENERIC, nrts[i], a), pipe};
+            for (int k = 0; k < 4; ++k) {
+                if (!fns[k]) continue;
                 hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (e != hipSuccess) return (int)e;
             }

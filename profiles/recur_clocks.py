@@ -28,10 +28,10 @@ for _ in range(3):
 fe, nn = eng.last_timing()
 clk = np.zeros((64, 16), np.int64)
 _lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clocks")
-st = clk[:51]
+st = clk[:53]
 step = np.diff(st[:, 0])
-print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; step cycles median {np.median(step[1:]):.0f}")
-for nm, k0, k1 in (("lstm work", 1, 0), ("lstm wait", 2, 1), ("tail fc1", 12, 8), ("tail fc2", 13, 12),
-                   ("tail fc3", 14, 13), ("tail post", 9, 14), ("tail wait", 10, 9)):
-    d = st[1:50, k0] - st[1:50, k1]
-    print(f"  {nm:10s} median {np.median(d):8.0f}  mean {d.mean():8.0f}")
+print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; iteration cycles median {np.median(step[3:48]):.0f}")
+for k, nm in enumerate(("lstm wave 0", "stage 1 fc", "stage 2 fc", "stage 3 fc+post")):
+    d = st[3:50, 2 * k + 1] - st[3:50, 2 * k]
+    lag = st[3:50, 2 * k] - st[3:50, 0]
+    print(f"  {nm:16s} work median {np.median(d):7.0f}  start lag {np.median(lag):6.0f}")
