@@ -38,6 +38,43 @@ static int net_shape(const NnImage *g)
     return NN_SHAPE_GENERIC;
 }
 
+/* An acc64 net runs on the int32-accumulator kernels when every accumulator
+ * provably stays inside int32: |sum_k W x| <= K * max|W| * 2^15 per half
+ * (activations are int16) plus the aligned bias.  Without overflow the two
+ * builds compute the same values -- shift_64b's clamp to int32
+ * (affine.c:242-249) never binds and shift_32b (affine_acc32b.c:243-250)
+ * never wraps -- provided no left (saturating) shift is involved. */
+static int fits_int32(const nnsp_batch *b, const nnsp_layer_desc *L, int nl)
+{
+    const NnImage *g = &b->im.img;
+    const long long LIM = 2147483647LL;
+    for (int i = 0; i < nl; ++i) {
+        const NnLayer *Ly = &g->L[i];
+        if (Ly->out_sh > 0 || Ly->xs_sh != 0) return 0;
+        const int lstm = L[i].type == NN_LSTM;
+        const int rows = lstm ? 4 * L[i].N : L[i].N;
+        long long wmax = 0, rmax = 0, bmax = 0;
+        for (size_t k = 0; k < (size_t)rows * (size_t)L[i].K; ++k) {
+            const long long v = L[i].W[k] < 0 ? -(long long)L[i].W[k] : L[i].W[k];
+            if (v > wmax) wmax = v;
+        }
+        if (lstm && L[i].Wr)
+            for (size_t k = 0; k < (size_t)rows * (size_t)L[i].N; ++k) {
+                const long long v = L[i].Wr[k] < 0 ? -(long long)L[i].Wr[k] : L[i].Wr[k];
+                if (v > rmax) rmax = v;
+            }
+        if (L[i].B)
+            for (int r = 0; r < rows; ++r) {
+                const long long v = L[i].B[r] < 0 ? -(long long)L[i].B[r] : L[i].B[r];
+                if (v > bmax) bmax = v;
+            }
+        long long bound = (long long)L[i].K * wmax * 32768 + (lstm ? (long long)L[i].N * rmax * 32768 : 0);
+        if (Ly->has_bias) bound += Ly->bias_sh >= 0 ? (Ly->bias_sh < 32 ? bmax << Ly->bias_sh : LIM) : bmax;
+        if (bound >= LIM) return 0;
+    }
+    return 1;
+}
+
 /* Use the split proj/recur kernels when the net has exactly one LSTM layer,
  * every other layer is FC and the staged weights fit in LDS. */
 static void plan_fast(nnsp_batch *b)
@@ -145,6 +182,7 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     if ((e = nnspk_malloc((void **)&b->d_feats, S * T * 40 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_mask, S))) goto fail;
     plan_fast(b);
+    b->ep32 = !b->im.img.acc32 && !getenv("NNSP_NO_EP32") && fits_int32(b, L, nl);
     if (b->fast) {
         if ((e = nnspk_set_lds_limit())) goto fail;
         const size_t rows = (size_t)b->im.img.L[b->li].rows;
@@ -266,6 +304,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.seg_len = seg->seg_len;
         f.dbg_clk = b->d_clk;
         f.shape = b->shape;
+        f.ep32 = b->ep32;
         const NnLayer *LL = &b->im.img.L[b->li];
         f.a_off = 0;
         f.a_lds_bytes = (int)LL->ar_off;

@@ -61,6 +61,7 @@ struct nnsp_batch {
     int fast, li, nstep_max, rec_waves, proj_blocks;
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int shape;                        /* NN_SHAPE_* compiled split-path shape */
+    int ep32;                         /* acc64 net that provably fits int32 accumulators */
     int32_t *d_gx;
     long long *d_clk; /* NNSP_RECUR_CLOCKS development probe */
 };

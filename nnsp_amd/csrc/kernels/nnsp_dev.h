@@ -155,8 +155,9 @@ __device__ __forceinline__ int16_t tanh_q15(int32_t x, const int16_t* tbl) {   /
     kx = kx < 0 ? 0 : (kx > 191 ? 191 : kx);
     const int32_t dx = wsub(wsub(a, 512), kx << 10);
     const uint32_t pr = reinterpret_cast<const uint32_t*>(tbl)[kx];
-    const int32_t v = (int32_t)(int16_t)(pr & 0xffff) +
-                      ((int32_t)((uint32_t)dx * (uint32_t)(int32_t)(int16_t)(pr >> 16)) >> 15);
+    // dx is in [-512, 1023] whenever the result is used (|x| < 5*2^15 below),
+    // so the 24-bit multiply (full rate) gives the exact 32-bit product
+    const int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (__mul24(dx, (int32_t)(int16_t)(pr >> 16)) >> 15);
     const int16_t y = a >= (5 << 15) ? (int16_t)0x7fff : (int16_t)(v > 0 ? v : 0);
     return neg ? (int16_t)-y : y;
 }

@@ -957,7 +957,7 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int 
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n, r->shape);
-    return launch(pick_proj(r->shape, img->acc32), dim3(blocks), dim3(256), lds, stream, img, r);
+    return launch(pick_proj(r->shape, img->acc32 || r->ep32), dim3(blocks), dim3(256), lds, stream, img, r);
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
@@ -966,11 +966,11 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stre
     if (nrow <= 0) return 0;
     int waves = 0;
     size_t tb = 0;
-    if (const void* fn = pick_pipe(r->shape, img->acc32, &waves, &tb))
+    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb))
         return launch(fn, dim3((nrow + 15) / 16), dim3(64 * waves), lds, stream, img, r);
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
-    return launch(pick_recur(r->shape, img->L[r->li].nrt, img->acc32), dim3(blocks), dim3(64 * RW * tpw), lds,
+    return launch(pick_recur(r->shape, img->L[r->li].nrt, img->acc32 || r->ep32), dim3(blocks), dim3(64 * RW * tpw), lds,
                   stream, img, r);
 }
 

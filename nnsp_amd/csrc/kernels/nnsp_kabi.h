@@ -115,7 +115,8 @@ typedef struct {
     int32_t n_list, seg_len;  /* seg_len as FeArgs */
     long long *dbg_clk;       /* development probe: [steps][8] s_memtime of tile 0, or NULL */
     int32_t ep_lo, ep_n;      /* epilogue rows [ep_lo, ep_lo + ep_n) staged into LDS */
-    int32_t shape, pad3;      /* NN_SHAPE_* */
+    int32_t shape;            /* NN_SHAPE_* */
+    int32_t ep32;             /* acc64 net whose accumulators provably fit int32: run the int32 kernels */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
 
