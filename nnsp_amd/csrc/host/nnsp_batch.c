@@ -298,6 +298,10 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.trig = trig;
         f.logits = logits;
         f.out3 = seg->out3;
+        f.net_ran = seg->net_ran;
+        f.detected = seg->detected;
+        f.outputs3 = seg->outputs3;
+        f.net_id = seg->net_id;
         f.list = seg->list;
         f.n_list = seg->n_list;
         f.seg_begin = seg->seg_begin;

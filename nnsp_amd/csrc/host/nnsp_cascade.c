@@ -306,8 +306,11 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         seg.lookback = c->lookback[n];
         seg.hist = hist;
         seg.hist_frames = c->H;
-        seg.out3 = c->d_out3[n];
         seg.seg_len = c->window;
+        seg.net_ran = a->net_ran;
+        seg.detected = a->detected;
+        seg.outputs3 = a->outputs3;
+        seg.net_id = n;
         TRY(nnsp_batch_run_nn(c->net[n], T, c->d_trig[n], NULL, &seg, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
         TRY(nnspk_event_record(c->ev_join[n], st));

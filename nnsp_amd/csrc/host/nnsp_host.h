@@ -77,6 +77,9 @@ typedef struct {
     int n_list, lookback, hist_frames;
     int seg_len;              /* > 0: segments end at min(T, seg_begin + seg_len) */
     const int32_t *n_list_dev; /* non-NULL: list length on the device (overrides n_list) */
+    int8_t *net_ran;           /* cascade: the caller's per-frame outputs (NULL skips) */
+    int16_t *detected, *outputs3;
+    int net_id;
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

@@ -82,17 +82,15 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
         const int16_t* tr = a.trig[n] + (size_t)s * T;
         int cut = -1;
         b_next = e;   // no switch: carry on in the same net next round (if e < T)
+        // the caller's per-frame outputs were written by the net's recur kernel;
+        // here only the controller runs, 16 prefetched triggers at a time
+        int16_t dq[16];
         for (int t = b; t < e; ++t) {
-            const int16_t det = tr[t];
-            const size_t f = (size_t)s * T + t;
-            if (a.net_ran) a.net_ran[f] = (int8_t)n;
-            if (a.detected) a.detected[f] = det;
-            if (a.outputs3) {
-                const int16_t* o = a.out3[n] + f * 3;
-                a.outputs3[f * 3 + 0] = o[0];
-                a.outputs3[f * 3 + 1] = o[1];
-                a.outputs3[f * 3 + 2] = o[2];
+            if (((t - b) & 15) == 0) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) dq[k] = t + k < e ? tr[t + k] : (int16_t)0;
             }
+            const int16_t det = dq[(t - b) & 15];
             bool move = false, rst = false;
             int np = st.pos;
             if (n == 0) {   // s2i (nnCntrlClass.c:173-200)

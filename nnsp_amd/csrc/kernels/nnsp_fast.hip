@@ -199,6 +199,20 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
     }
 }
 
+
+// per-frame results of stream s at frame f (NNSPClass_exec's return value and
+// NNSPClass.outputs after the frame): per-net buffers for the controller and,
+// in a cascade, the caller's outputs
+__device__ __forceinline__ void put_frame(const FastRun& r, int s, int T, int f, const PostState& ps) {
+    const size_t i = (size_t)s * T + f;
+    if (r.trig) r.trig[i] = ps.trigger;
+    if (r.out3)
+        for (int o = 0; o < 3; ++o) r.out3[i * 3 + o] = ps.outputs[o];
+    if (r.detected) r.detected[i] = ps.trigger;
+    if (r.net_ran) r.net_ran[i] = (int8_t)r.net_id;
+    if (r.outputs3)
+        for (int o = 0; o < 3; ++o) r.outputs3[i * 3 + o] = ps.outputs[o];
+}
 // ---------------------------------------------------------------------------
 // proj_kernel
 // ---------------------------------------------------------------------------
@@ -411,11 +425,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     int nsteps = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
-    if (tail && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
-        if (r.trig) r.trig[(size_t)s * T + b] = ps.trigger;
-        if (r.out3)
-            for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
-    }
+    if (tail && lane < 16 && valid && phase == 1 && b < e) put_frame(r, s, T, b, ps);   // frame b: no NN, trigger carried
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
     const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
     v4i gxv[RPW];
@@ -544,13 +554,8 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                     for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
                     post_proc(ps, img, lg);
                 }
-                if (r.trig) {
-                    r.trig[(size_t)s * T + t] = ps.trigger;
-                    if (t + 1 < e) r.trig[(size_t)s * T + t + 1] = ps.trigger;
-                }
-                if (r.out3)
-                    for (int f = t; f < min(t + 2, e); ++f)
-                        for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + f) * 3 + o] = ps.outputs[o];
+                put_frame(r, s, T, t, ps);
+                if (t + 1 < e) put_frame(r, s, T, t + 1, ps);
             }
         }
         PROBE(1);
@@ -689,11 +694,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     int nsteps = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
-    if (post_w && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
-        if (r.trig) r.trig[(size_t)s * T + b] = ps.trigger;
-        if (r.out3)
-            for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + b) * 3 + o] = ps.outputs[o];
-    }
+    if (post_w && lane < 16 && valid && phase == 1 && b < e) put_frame(r, s, T, b, ps);   // frame b: no NN, trigger carried
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
     const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
     v4i gxv[RPW];
@@ -827,13 +828,8 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
 #pragma unroll
                 for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
                 post_proc(ps, img, lg);
-                if (r.trig) {
-                    r.trig[(size_t)s * T + t] = ps.trigger;
-                    if (t + 1 < e) r.trig[(size_t)s * T + t + 1] = ps.trigger;
-                }
-                if (r.out3)
-                    for (int f = t; f < min(t + 2, e); ++f)
-                        for (int o = 0; o < 3; ++o) r.out3[((size_t)s * T + f) * 3 + o] = ps.outputs[o];
+                put_frame(r, s, T, t, ps);
+                if (t + 1 < e) put_frame(r, s, T, t + 1, ps);
             }
         }
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();

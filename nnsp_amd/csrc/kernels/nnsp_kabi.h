@@ -117,6 +117,13 @@ typedef struct {
     int32_t ep_lo, ep_n;      /* epilogue rows [ep_lo, ep_lo + ep_n) staged into LDS */
     int32_t shape;            /* NN_SHAPE_* */
     int32_t ep32;             /* acc64 net whose accumulators provably fit int32: run the int32 kernels */
+    /* cascade: the caller's per-frame outputs, written for every frame of the
+     * segment (frames past a net switch are rewritten by the next net's
+     * segment in the next round); NULL skips */
+    int8_t *net_ran;          /* [S][T] NNSP_ID of this net */
+    int16_t *detected;        /* [S][T] NNSPClass_exec return */
+    int16_t *outputs3;        /* [S][T][3] NNSPClass.outputs */
+    int32_t net_id, pad4;
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
 
