@@ -302,6 +302,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.detected = seg->detected;
         f.outputs3 = seg->outputs3;
         f.net_id = seg->net_id;
+        f.fs = seg->fs;
         f.list = seg->list;
         f.n_list = seg->n_list;
         f.seg_begin = seg->seg_begin;

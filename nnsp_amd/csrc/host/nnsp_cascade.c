@@ -175,6 +175,14 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             a->prev_default[i] = c->d_pdef + 40 * i;
             a->list[i] = c->d_list[i];
             a->cold_list[i] = c->d_cold_list[i];
+            FeatSrc *fs = &a->fs[i];
+            fs->lmel = c->d_lmel;
+            fs->fresh = c->d_fresh;
+            fs->mean = nets[i]->d_mean;
+            fs->stdR = nets[i]->d_stdR;
+            fs->ring = c->ring;
+            fs->lookback = c->lookback[i];
+            fs->norm_shift = nets[i]->norm_shift;
         }
     }
     {   /* the reset context value of each net: FeatureClass_setDefault on a scratch stream */
@@ -250,8 +258,9 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
     return nnspk_sync(c->stream);
 }
 
-/* features of net n for this round's segments: normalised shared log-Mel,
- * and the full front end for the frames right after the net's reset */
+/* features of net n for this round's segments: the full front end for the
+ * frames right after the net's reset (the others are normalised from the
+ * shared log-Mel by the kernels that read them, FeatSrc) */
 static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *cnt,
                             int32_t *n_list_rec, const int16_t *hist, void *stream)
 {
@@ -277,7 +286,6 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.abs0 = c->abs0;
     fa.lmel = c->d_lmel;
     fa.fresh = c->d_fresh;
-    TRY(nnspk_launch_seg_norm(&fa, stream));
     fa.mode = FE_MODE_COLD;
     fa.list = c->d_cold_list[n];
     fa.n_list_dev = cnt + 3 + n;
@@ -311,6 +319,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         seg.detected = a->detected;
         seg.outputs3 = a->outputs3;
         seg.net_id = n;
+        seg.fs = a->fs[n];
         TRY(nnsp_batch_run_nn(c->net[n], T, c->d_trig[n], NULL, &seg, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
         TRY(nnspk_event_record(c->ev_join[n], st));
@@ -335,6 +344,7 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     a.net_ran = net_ran;
     a.detected = detected;
     a.outputs3 = outputs3;
+    for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
     TRY(nnspk_event_record(c->ev[0], c->stream));
     TRY(nnspk_memset(c->d_counts, 0, 18 * 4, c->stream));
     TRY(nnspk_memset(c->d_frames, 0, 3 * 8, c->stream));

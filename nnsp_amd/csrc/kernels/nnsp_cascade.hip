@@ -16,6 +16,9 @@
 #include <stdint.h>
 
 #include "nnsp_kabi.h"
+#include "nnsp_nn.h"
+
+using nnsp::feat8;
 
 namespace {
 
@@ -127,6 +130,10 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
         // frames since the reset of the net the stream runs next round (the
         // front end's STFT buffer is zero right after NNSPClass_reset)
         fr_next = cut >= 0 ? 0 : min(2, (int)a.fresh[s] + (e - b));
+        int4 slot5[5];   // the cut frame's feature, read while fresh[s] is still the segment's
+        if (cut >= 0)
+#pragma unroll
+            for (int k = 0; k < 5; ++k) slot5[k] = feat8(a.fs[n], a.feats[n], s, T, b, cut, k);
         a.fresh[s] = (int8_t)fr_next;
         if (cut >= 0) {
             // NNSPClass_reset of the departing net (nn_speech.c:57-72):
@@ -134,7 +141,6 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
             // slot 5 keeps this frame's feature (T4); the STFT buffer's zeros
             // are fresh = 0 of the next net to run -- then the LSTM state
             // (NeuralNetClass_setDefault) and the post-processing state
-            const int4* src = reinterpret_cast<const int4*>(a.feats[n] + ((size_t)s * T + cut) * 40);
             const int4* def = reinterpret_cast<const int4*>(a.prev_default[n]);
             int4* p5 = reinterpret_cast<int4*>(a.prev5[n] + (size_t)s * 200);
 #pragma unroll
@@ -144,7 +150,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
                 p5[5 + k] = d;
                 p5[10 + k] = d;
                 p5[15 + k] = d;
-                p5[20 + k] = src[k];
+                p5[20 + k] = slot5[k];
             }
             const int4 z = make_int4(0, 0, 0, 0);
             int4* hs = reinterpret_cast<int4*>(a.h[n] + (size_t)s * NN_MAX_W);

@@ -267,7 +267,7 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
             if (idx < 5)
                 v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part);
             else if (idx - 5 < L)
-                v = *reinterpret_cast<const int4*>(r.feats + ((size_t)s * r.T + b + idx - 5) * 40 + 8 * part);
+                v = feat8(r.fs, r.feats, s, r.T, b, b + idx - 5, part);
             *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
         }
         wave_lds_sync();
@@ -592,8 +592,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
             if (L > 0) {
                 const int gs = sid(i0 + st), j = L + m;
                 cv[k] = j < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + j) * 40 + 8 * part)
-                              : *reinterpret_cast<const int4*>(r.feats + ((size_t)gs * T + R.beg[st] + j - 5) * 40 +
-                                                               8 * part);
+                              : feat8(r.fs, r.feats, gs, T, R.beg[st], R.beg[st] + j - 5, part);
                 ci[k] = gs * 25 + c;
             }
         }
@@ -863,8 +862,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
             if (L > 0) {
                 const int gs = sid(i0 + st), jx = L + m;
                 cv[k] = jx < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + jx) * 40 + 8 * part)
-                               : *reinterpret_cast<const int4*>(r.feats + ((size_t)gs * T + R.beg[st] + jx - 5) * 40 +
-                                                                8 * part);
+                               : feat8(r.fs, r.feats, gs, T, R.beg[st], R.beg[st] + jx - 5, part);
                 ci[k] = gs * 25 + c;
             }
         }

@@ -57,6 +57,17 @@ typedef struct {
     int32_t *n_list_rec;      /* seg_norm: non-NULL, block 0 records *n_list_dev there */
 } FeArgs;
 
+/* Cascade: where a net's segment features come from -- the shared log-Mel
+ * ring normalised on the fly with the net's mean / stdR (feature_module.c:
+ * 67-73), except the frames within 2 frames of the net's reset, which the
+ * cold front end (FE_MODE_COLD) wrote to the net's feats buffer. */
+typedef struct {
+    const int32_t *lmel;      /* [S][ring][40]; NULL: every frame from feats */
+    const int8_t *fresh;      /* [S] frames the net ran since its reset, at the segment start */
+    const int32_t *mean, *stdR;
+    int32_t ring, abs0, lookback, norm_shift;
+} FeatSrc;
+
 #define FE_MODE_BATCH 0
 #define FE_MODE_SHARED 1
 #define FE_MODE_COLD 2
@@ -124,6 +135,7 @@ typedef struct {
     int16_t *detected;        /* [S][T] NNSPClass_exec return */
     int16_t *outputs3;        /* [S][T][3] NNSPClass.outputs */
     int32_t net_id, pad4;
+    FeatSrc fs;               /* cascade feature source (fs.lmel NULL: feats) */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
 
@@ -136,9 +148,6 @@ typedef struct {
 
 /* launch layer (nnsp_kernels.hip) */
 int nnspk_launch_fe(const FeArgs *a, void *stream);
-/* cascade: normalised features of a segment's frames from the shared log-Mel
- * ring (frames >= 2 after the net's reset; FeArgs fields as FE_MODE_COLD) */
-int nnspk_launch_seg_norm(const FeArgs *a, void *stream);
 /* cascade reset: ring slots of the masked streams := log-Mel of silence */
 int nnspk_launch_lmel_fill(int32_t *lmel, int ring, const uint8_t *mask, int S, void *stream);
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
@@ -220,6 +229,7 @@ typedef struct {
     int16_t *detected;        /* [S][T] or NULL */
     int16_t *outputs3;        /* [S][T][3] or NULL */
     int8_t *fresh;            /* [S] frames the current net ran since its reset (0..2) */
+    FeatSrc fs[3];            /* per net id: segment feature source (slot 5 kept at a reset) */
 } CascArgs;
 
 int nnspk_launch_casc_begin(const CascArgs *a, void *stream);

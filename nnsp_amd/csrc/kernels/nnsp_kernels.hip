@@ -595,40 +595,6 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
     for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
 }
 
-// Cascade: normalised features (feature_module.c:67-73) of the listed
-// segments' frames that come 2 or more frames after the net's reset, from the
-// shared log-Mel ring; one thread per 8 features.
-__global__ __launch_bounds__(256) void seg_norm_kernel(FeArgs a) {
-    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (unsigned)a.n_list;
-    if (a.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *a.n_list_rec = (int32_t)nrow;
-    const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
-    const unsigned long long n = (unsigned long long)nrow * W * 5;
-    for (unsigned long long x = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; x < n;
-         x += (unsigned long long)gridDim.x * blockDim.x) {
-        const unsigned part = (unsigned)(x % 5), rk = (unsigned)(x / 5);
-        const unsigned i = rk / W, k = rk - i * W;
-        const int s = a.list[i];
-        const int b = a.seg_begin[s], t = b + (int)k;
-        if (t >= a.T || (int)k + a.fresh[s] < 2) continue;
-        const unsigned slot = (unsigned)(a.abs0 + t - a.lookback + a.ring) % (unsigned)a.ring;
-        const int4* src = reinterpret_cast<const int4*>(a.lmel + ((size_t)s * a.ring + slot) * 40 + 8 * part);
-        const int4 l0 = src[0], l1 = src[1];
-        const int32_t lg[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-        int16_t o[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int64_t d = (int64_t)lg[j] - a.mean[8 * part + j];
-            o[j] = sat16((d * a.stdR[8 * part + j]) >> a.norm_shift);
-        }
-        int4 w;
-        w.x = (int32_t)((uint32_t)(uint16_t)o[0] | ((uint32_t)(uint16_t)o[1] << 16));
-        w.y = (int32_t)((uint32_t)(uint16_t)o[2] | ((uint32_t)(uint16_t)o[3] << 16));
-        w.z = (int32_t)((uint32_t)(uint16_t)o[4] | ((uint32_t)(uint16_t)o[5] << 16));
-        w.w = (int32_t)((uint32_t)(uint16_t)o[6] | ((uint32_t)(uint16_t)o[7] << 16));
-        *reinterpret_cast<int4*>(a.feats + ((size_t)s * a.T + t) * 40 + 8 * part) = w;
-    }
-}
-
 // log-Mel of silence: mel 0 -> log10_vec's x == 0 -> 1 (fixlog10.c:56)
 __global__ __launch_bounds__(256) void lmel_fill_kernel(int32_t* lmel, int ring, const uint8_t* mask, int S) {
     const int s = blockIdx.x;
@@ -819,16 +785,6 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (blocks > 256 * 16) blocks = 256 * 16;
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 512) blocks = 512;   // at most 2 frames per switch
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
-    return ok(hipGetLastError());
-}
-
-int nnspk_launch_seg_norm(const FeArgs* a, void* stream) {
-    const int nrow = a->n_list_dev ? a->S : a->n_list;   // device count: size for the maximum
-    if (nrow <= 0 || a->T <= 0) return 0;
-    const int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
-    long long blocks = ((long long)nrow * W * 5 + 255) / 256;
-    if (blocks > 256 * 16) blocks = 256 * 16;
-    hipLaunchKernelGGL(seg_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
     return ok(hipGetLastError());
 }
 

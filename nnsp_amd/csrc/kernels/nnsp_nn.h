@@ -49,6 +49,27 @@ __device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) 
     return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15(v, tt) : sigmoid_q15(v, tt));
 }
 
+// 8 features [8*part, 8*part + 8) of stream s at chunk frame t of a segment
+// starting at b: from the net's feats buffer, or the shared log-Mel ring
+// normalised on the fly (cascade; the 2 frames after a reset come from feats)
+__device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
+                                      int part) {
+    if (!fs.lmel || t - b + fs.fresh[s] < 2)
+        return *reinterpret_cast<const int4*>(feats + ((size_t)s * T + t) * 40 + 8 * part);
+    const unsigned slot = (unsigned)(fs.abs0 + t - fs.lookback + fs.ring) % (unsigned)fs.ring;
+    const int4* src = reinterpret_cast<const int4*>(fs.lmel + ((size_t)s * fs.ring + slot) * 40 + 8 * part);
+    const int4 l0 = src[0], l1 = src[1];
+    const int32_t lg[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
+    uint32_t o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int64_t d = (int64_t)lg[j] - fs.mean[8 * part + j];
+        o[j] = (uint16_t)sat16((d * fs.stdR[8 * part + j]) >> fs.norm_shift);
+    }
+    return make_int4((int)(o[0] | o[1] << 16), (int)(o[2] | o[3] << 16), (int)(o[4] | o[5] << 16),
+                     (int)(o[6] | o[7] << 16));
+}
+
 // Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
 template <int MAXKT>
 __device__ __forceinline__ void load_b(const int16_t* buf, int stride, int nkt, int lane,
