@@ -316,6 +316,12 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.ep_lo = 0;
         f.ep_n = b->ep_proj;
         f.n_list_dev = seg->n_list_dev;
+        f.n_list_rec = seg->n_list_rec;
+        {   /* proj tiles: pack 2 or 4 streams per 16-row tile when a segment has <= 8 / 4 NN steps */
+            const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
+            const int steps = (W + 1) / 2;
+            f.gpt = b->shape == NN_SHAPE_GENERIC ? 1 : (steps <= 4 ? 4 : (steps <= 8 ? 2 : 1));
+        }
         int blocks = b->proj_blocks;
         if (seg->list && !seg->n_list_dev) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;

@@ -262,7 +262,7 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
  * frames right after the net's reset (the others are normalised from the
  * shared log-Mel by the kernels that read them, FeatSrc) */
 static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *cnt,
-                            int32_t *n_list_rec, const int16_t *hist, void *stream)
+                            const int16_t *hist, void *stream)
 {
     nnsp_batch *b = c->net[n];
     FeArgs fa;
@@ -276,7 +276,6 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.feats = b->d_feats;
     fa.list = c->d_list[n];
     fa.n_list_dev = cnt + n;
-    fa.n_list_rec = n_list_rec;
     fa.seg_begin = c->d_seg_begin;
     fa.lookback = c->lookback[n];
     fa.hist = hist;
@@ -304,7 +303,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         const int timed = r < MAX_TIMED;
         TRY(nnspk_stream_wait(st, c->ev_fork));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
-        TRY(segment_features(c, n, pcm, T, cur, timed ? c->d_rcount + 3 * r + n : NULL, hist, st));
+        TRY(segment_features(c, n, pcm, T, cur, hist, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
         nnsp_segment seg;
         memset(&seg, 0, sizeof seg);
@@ -320,6 +319,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         seg.outputs3 = a->outputs3;
         seg.net_id = n;
         seg.fs = a->fs[n];
+        seg.n_list_rec = timed ? c->d_rcount + 3 * r + n : NULL;
         TRY(nnsp_batch_run_nn(c->net[n], T, c->d_trig[n], NULL, &seg, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
         TRY(nnspk_event_record(c->ev_join[n], st));

@@ -29,7 +29,7 @@
 using namespace nnsp;
 
 #define P_ASTRIDE 264   // int16 per row of a proj activation buffer
-#define P_UNION 1440    // 36 frames x 40 features (int16)
+#define P_UNION 1920    // context frames of a tile: G streams x (32/G + 4) frames x 40 features (int16)
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
 #define R_CW 128        // int32 per row of the c buffer
 
@@ -248,31 +248,68 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
     const int nkt = GEN ? LL.nkt : SH::NKR;
     const int rows = 16 * nrt;   // LSTM rows are padded to whole tiles (4 units per group)
     const int wsteps = r.seg_len > 0 ? min(r.nstep_max, (r.seg_len + 1) / 2) : r.nstep_max;
-    const int ntps = (wsteps + 15) / 16;
+    // a 16-row MFMA tile is G streams x SPT consecutive NN steps: G = 1 tiles
+    // a stream's steps 16 at a time; short segments (cascade rounds, host:
+    // SPT >= the segment's steps) pack G = 2 or 4 streams into one tile
+    const int G = GEN ? 1 : r.gpt;
+    const int SPT = 16 / G;
+    const int FR = 2 * SPT + 4;                       // context frames of one stream's rows
+    const int ntps = G > 1 ? 1 : (wsteps + 15) / 16;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
-    const long long ntiles = (long long)nrow * ntps;
+    if (r.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *r.n_list_rec = nrow;
+    const long long ngrp = (nrow + G - 1) / G;
+    const long long ntiles = ngrp * ntps;
+    // stream k of a tile: list entry, segment start b, length L, NN phase
+    struct Seg { int s, b, L, ph; bool ok; };
+    auto seg_of = [&](long long grp, int k) {
+        Seg g;
+        const long long i = grp * G + k;
+        g.ok = i < nrow;
+        g.s = g.ok ? (r.list ? r.list[i] : (int)i) : 0;
+        g.b = g.ok && r.seg_begin ? r.seg_begin[g.s] : 0;
+        g.L = g.ok ? (r.seg_len > 0 ? min(r.T, g.b + r.seg_len) : r.T) - g.b : 0;
+        g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
+        return g;
+    };
     for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
          tile += (long long)gridDim.x * (blockDim.x >> 6)) {
-        const int i_row = (int)(tile / ntps), j0 = 16 * (int)(tile - (long long)i_row * ntps);
-        const int s = r.list ? r.list[i_row] : i_row;
-        const int b = r.seg_begin ? r.seg_begin[s] : 0;   // segment: frames b..e-1
-        const int L = (r.seg_len > 0 ? min(r.T, b + r.seg_len) : r.T) - b;
-        const int phase = 1 - reinterpret_cast<const NnPost*>(r.post)[s].slides;
-        const int t0 = 2 * j0 + phase;            // segment-relative NN frame of row 0
-        if (t0 >= L) continue;                    // wave-uniform
-        // ---- union of the 16 context windows: V[t0 .. t0+35], V = prev5 ++ feats[b..T)
-        for (int c = lane; c < 180; c += 64) {
-            const int fr = c / 5, part = c - 5 * fr, idx = t0 + fr;
+        const long long grp = tile / ntps;
+        const int j0 = 16 * (int)(tile - grp * ntps);
+        // lanes 0..G-1 load the tile's stream descriptors; the others read them by shuffle
+        const Seg mine = seg_of(grp, lane < G ? lane : 0);
+        auto seg_k = [&](int k) {
+            Seg g;
+            g.s = __shfl(mine.s, k);
+            g.b = __shfl(mine.b, k);
+            g.L = __shfl(mine.L, k);
+            g.ph = __shfl(mine.ph, k);
+            g.ok = __shfl((int)mine.ok, k) != 0;
+            return g;
+        };
+        // wave-uniform: skip a tile none of whose rows has a frame
+        if (!__any(lane < G && mine.ok && 2 * j0 + mine.ph < mine.L)) continue;
+        // ---- union of the context windows: stream k's rows read
+        //      V_k[t0 .. t0 + FR - 1], V = prev5 ++ features[b..b+L), t0 = 2*j0 + phase
+        for (int c = lane; c < G * FR * 5; c += 64) {
+            const int k = c / (FR * 5), rem = c - k * FR * 5, fr = rem / 5, part = rem - 5 * fr;
+            const Seg g = seg_k(k);
+            const int idx = 2 * j0 + g.ph + fr;
             int4 v = make_int4(0, 0, 0, 0);
-            if (idx < 5)
-                v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)s * 5 + idx) * 40 + 8 * part);
-            else if (idx - 5 < L)
-                v = feat8(r.fs, r.feats, s, r.T, b, b + idx - 5, part);
+            if (g.ok) {
+                if (idx < 5)
+                    v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part);
+                else if (idx - 5 < g.L)
+                    v = feat8(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+            }
             *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
         }
         wave_lds_sync();
-        // ---- prefix FC layers (row p's context = uni[80p .. 80p+239])
-        const int16_t* in = P.uni;
+        // this lane's row sc: stream kr of the tile, its step j0 + jr
+        const int kr = sc / SPT, jr = sc - kr * SPT;
+        const Seg me = seg_k(kr);
+        // ---- prefix FC layers (row (k, j)'s context = uni[k*FR*40 + 80j .. +239];
+        //      the per-lane base makes in + sc * in_stride that row)
+        const int16_t* in = P.uni + kr * FR * 40 + 80 * jr - 80 * sc;
         int in_stride = 80;
         if (!GEN) {   // one tanh FC layer, K = 240
             const NnLayer& L0 = img.L[0];
@@ -298,9 +335,9 @@ __global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
             load_b<2>(in, in_stride, nkt, lane, bh, bl);
             const uint8_t* A = W + (LL.a_off - r.a_off);
             const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
-            const int j = j0 + sc;
-            const bool act = j < r.nstep_max && 2 * j + phase < L;
-            int32_t* dst = r.gx + ((size_t)s * r.nstep_max + j) * rows + 4 * q;
+            const int j = j0 + jr;
+            const bool act = me.ok && j < r.nstep_max && 2 * j + me.ph < me.L;
+            int32_t* dst = r.gx + ((size_t)me.s * r.nstep_max + j) * rows + 4 * q;
             auto tile = [&](int rt) {
                 v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll

@@ -134,7 +134,9 @@ typedef struct {
     int8_t *net_ran;          /* [S][T] NNSP_ID of this net */
     int16_t *detected;        /* [S][T] NNSPClass_exec return */
     int16_t *outputs3;        /* [S][T][3] NNSPClass.outputs */
-    int32_t net_id, pad4;
+    int32_t net_id;
+    int32_t gpt;              /* proj: streams per 16-row tile (1, 2 or 4; compiled shapes) */
+    int32_t *n_list_rec;      /* non-NULL: proj records the list length it ran with (stats) */
     FeatSrc fs;               /* cascade feature source (fs.lmel NULL: feats) */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
