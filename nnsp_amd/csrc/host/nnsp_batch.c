@@ -95,8 +95,20 @@ static void plan_fast(nnsp_batch *b)
     b->ep_rec_lo = g->L[li].ep_off;
     b->ep_rec_n = b->im.rows_total - g->L[li].ep_off;
     const int shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
-    const size_t proj_lds = nnspk_fast_lds_bytes(0, a_proj, 4, b->ep_proj, shape);
-    if (proj_lds > LDS_MAX) return;
+    /* proj workgroups of 4 or 8 waves (they share the staged weights), whichever
+     * keeps more waves per CU resident (LDS-bound) */
+    int wpb = 4, per_cu = 0;
+    for (int w = 4; w <= 8; w += 4) {
+        const size_t lds = nnspk_fast_lds_bytes(0, a_proj, w, b->ep_proj, shape);
+        int fit = lds <= LDS_MAX ? (int)(LDS_MAX / lds) : 0;
+        if (fit * w > 32) fit = 32 / w;
+        if (fit * w > per_cu * wpb) {
+            per_cu = fit;
+            wpb = w;
+        }
+    }
+    if (per_cu < 1) return;
+    b->proj_waves = wpb;
     if (nnspk_fast_lds_bytes(1, a_rec, 1, b->ep_rec_n, shape) > LDS_MAX) return;
     /* tiles per 4-wave group in one workgroup: 2 once there are >= 2 tiles per CU */
     const int tiles = (b->S + 15) / 16;
@@ -109,11 +121,8 @@ static void plan_fast(nnsp_batch *b)
     int cus = 256, clk = 0;
     char arch[64];
     if (nnspk_device_info(&cus, &clk, arch, (int)sizeof arch) || cus <= 0) cus = 256;
-    int per_cu = (int)(LDS_MAX / proj_lds);
-    if (per_cu > 8) per_cu = 8;
-    if (per_cu < 1) per_cu = 1;
     const long long ptiles = (long long)b->S * ((b->nstep_max + 15) / 16);
-    long long blocks = (ptiles + 3) / 4;
+    long long blocks = (ptiles + wpb - 1) / wpb;
     const long long cap = (long long)cus * per_cu;
     b->proj_blocks = (int)(blocks < cap ? blocks : cap);
     b->fast = 1;
@@ -326,10 +335,10 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         if (seg->list && !seg->n_list_dev) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
             const long long pt = (long long)seg->n_list * ((W / 2 + 1 + 15) / 16);
-            const long long need = (pt + 3) / 4;
+            const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
             if (need < blocks) blocks = (int)need;
         }
-        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, stream));
+        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
         f.a_off = LL->ar_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
         f.ep_lo = b->ep_rec_lo;

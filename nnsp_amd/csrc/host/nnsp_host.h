@@ -58,7 +58,7 @@ struct nnsp_batch {
     uint8_t *d_mask;
     int last_T;
     /* split NN path (one LSTM layer) */
-    int fast, li, nstep_max, rec_waves, proj_blocks;
+    int fast, li, nstep_max, rec_waves, proj_blocks, proj_waves;
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int shape;                        /* NN_SHAPE_* compiled split-path shape */
     int ep32;                         /* acc64 net that provably fits int32 accumulators */

@@ -228,7 +228,7 @@ struct alignas(16) ProjWave {
 };
 
 template <class SH, bool ACC32>
-__global__ __launch_bounds__(256) void proj_kernel(NnImage img, FastRun r) {
+__global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
@@ -986,9 +986,9 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int 
     return base + (size_t)units * (which == 0 ? pw : rt);
 }
 
-int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, 4, r->ep_n, r->shape);
-    return launch(pick_proj(r->shape, img->acc32 || r->ep32), dim3(blocks), dim3(256), lds, stream, img, r);
+int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, int waves, void* stream) {
+    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, waves, r->ep_n, r->shape);
+    return launch(pick_proj(r->shape, img->acc32 || r->ep32), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {

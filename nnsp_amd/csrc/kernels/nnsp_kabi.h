@@ -174,7 +174,7 @@ int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
 int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
                             int n, void *stream);
 size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape);
-int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, void *stream);
+int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, int waves, void *stream);
 int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, void *stream);
 int nnspk_set_lds_limit(void);
 int nnspk_malloc(void **p, size_t n);
