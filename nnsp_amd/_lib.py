@@ -144,6 +144,21 @@ def _declare(L: C.CDLL) -> None:
         "sigmoid_fix": (P, [P, P, I]),
         "relu6_fix": (P, [P, P, I]),
         "linear_fix": (P, [P, P, I]),
+        "affine_Krows_8x16": (I, [C.c_int16, C.POINTER(P), C.POINTER(P), C.POINTER(P), P, C.c_int16, C.c_int16,
+                                  C.c_int16, C.c_int16, P, C.c_int8, P]),
+        "affine_Krows_8x16_acc32b": (I, [C.c_int16, C.POINTER(P), C.POINTER(P), C.POINTER(P), P, C.c_int16,
+                                         C.c_int16, C.c_int16, C.c_int16, P, C.c_int8, P]),
+        "rc_Krows_8x16": (I, [C.c_int16, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P, C.c_int16,
+                              C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16, P]),
+        "rc_Krows_8x16_acc32b": (I, [C.c_int16, C.POINTER(P), C.POINTER(P), C.POINTER(P), C.POINTER(P), P, P,
+                                     C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16, P]),
+        "rc_8x16": (I, [P, P, P, P, P, P, C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16,
+                        C.c_int16, I, P]),
+        "rc_8x16_acc32b": (I, [P, P, P, P, P, P, C.c_int16, C.c_int16, C.c_int16, C.c_int16, C.c_int16,
+                               C.c_int16, C.c_int16, I, P]),
+        "shift_64b": (None, [P, C.c_int8, I]),
+        "shift_32b": (None, [P, C.c_int8, I]),
+        "arm_fft_init": (None, []),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -114,15 +114,34 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
     return n;
 }
 
+/* A NeuralNetClass's device image is cached by everything that defines the
+ * net -- its address, and a hash of its shape, qbits, layer / activation
+ * functions and weight / bias / state table pointers (the weight tables are
+ * const data in def_nn*.c) -- so a struct rebuilt at a reused address with
+ * other tables gets its own image. */
 static img_node *net_image(const NeuralNetClass *net)
 {
-    static const int zk[8];
-    img_node *n = img_find(net, NULL, NULL, NULL, zk);
+    uint64_t h = 1469598103934665603ULL;
+#define MIX(v)                                   \
+    do {                                         \
+        h ^= (uint64_t)(uintptr_t)(v);           \
+        h *= 1099511628211ULL;                   \
+    } while (0)
+    MIX(net->numlayers);
+    for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i) {
+        MIX(net->size_layer[i]); MIX(net->size_layer[i + 1]); MIX(net->net_layer_type[i]);
+        MIX(net->qbit_kernel[i]); MIX(net->qbit_input[i]); MIX(net->qbit_bias[i]); MIX(net->activation_type[i]);
+        MIX(net->act_func[i]); MIX(net->layer_func[i]); MIX(net->pt_kernel[i]); MIX(net->pt_bias[i]);
+        MIX(net->pt_kernel_rec[i]);
+    }
+#undef MIX
+    const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
+    img_node *n = img_find(net, NULL, NULL, NULL, ik);
     if (n) return n;
     nnsp_layer_desc L[NN_MAX_LAYERS];
     int nl = 0, lin = 0;
     CK(nnsp_describe_net(net, L, &nl, &lin));
-    return img_add(net, NULL, NULL, NULL, zk, L, nl, lin);
+    return img_add(net, NULL, NULL, NULL, ik, L, nl, lin);
 }
 
 /* LSTM h/c of a NeuralNetClass <-> device rows [l][NN_MAX_W] */
@@ -627,62 +646,173 @@ void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) 
 }
 
 /* ---------------------------------------------------------------------------
- * row-block primitives (affine.c:12-407, affine_acc32b.c) -- not yet on GPU
+ * row-block primitives (affine.c:12-407, :492-591; affine_acc32b.c) on the GPU
+ * (k_rows: one thread per output row).  Pointer arguments advance exactly as
+ * the reference's: the kernel stream by rows * dim_input bytes, the bias by
+ * rows (when present), the output by the activation's width (when is_out).
  * ------------------------------------------------------------------------- */
-static int unsupported(const char *fn)
+static int row_act(void *(*act)(void *, int32_t *, int), int is_out)
 {
-    fprintf(stderr, "libnnsp_mi355x: %s is not provided by this build (use fc_8x16 / lstm_8x16)\n", fn);
-    return -1;
+    if (!is_out) return 0;
+    const int a = nnsp_act_of(act);
+    if (a < 0) fprintf(stderr, "libnnsp_mi355x: unsupported activation function pointer\n");
+    return a;
 }
-int affine_Krows_8x16(int16_t a, int16_t **b, int8_t **c, int16_t **d, int16_t *e, int16_t f,
-                      int16_t g, int16_t h, int16_t i, int64_t *j, int8_t k,
-                      void *(*l)(void *, int32_t *, int))
+
+/* affine_Krows_8x16 (+_acc32b): acc64 accumulators, or int32 ones widened */
+static int affine_rows_call(int16_t R, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+                            int16_t *input, int16_t K, int16_t qk, int16_t qb, int16_t qi, int64_t *acc64,
+                            int32_t *acc32, int8_t is_out, void *(*act)(void *, int32_t *, int))
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l;
-    return unsupported("affine_Krows_8x16");
+    if (R < 1 || R > 4 || K < 0) return -1;
+    const int a_t = row_act(act, is_out);
+    if (a_t < 0) return -1;
+    begin();
+    RowArgs a;
+    memset(&a, 0, sizeof a);
+    a.mode = ROWS_AFFINE;
+    a.rows = R;
+    a.K = K;
+    a.qk = qk; a.qb = qb; a.qi = qi;
+    a.acc32 = acc32 != NULL;
+    a.is_out = is_out;
+    a.act = a_t;
+    int64_t acc[4];
+    for (int i = 0; i < R; ++i) acc[i] = acc32 ? (int64_t)acc32[i] : acc64[i];
+    a.w = (const int8_t *)up(*pp_kernel, (size_t)R * K);
+    a.b = *pp_bias ? (const int16_t *)up(*pp_bias, (size_t)R * 2) : NULL;
+    a.x = (const int16_t *)up(input, (size_t)K * 2);
+    a.acc = (int64_t *)up(acc, (size_t)R * 8);
+    const size_t ob = (size_t)R * (a_t == 3 ? 4 : 2);
+    if (is_out) a.out = up(NULL, ob);
+    CK(nnspk_launch_rows(&a, G.stream));
+    down(acc, a.acc, (size_t)R * 8);
+    if (is_out) down(*pp_output, a.out, ob);
+    fin();
+    for (int i = 0; i < R; ++i) {
+        if (acc32) acc32[i] = (int32_t)acc[i];
+        else acc64[i] = acc[i];
+    }
+    *pp_kernel += (size_t)R * K;
+    if (*pp_bias) *pp_bias += R;
+    if (is_out) *pp_output = (int16_t *)((char *)*pp_output + ob);
+    return 0;
 }
-int affine_Krows_8x16_acc32b(int16_t a, int16_t **b, int8_t **c, int16_t **d, int16_t *e, int16_t f,
-                             int16_t g, int16_t h, int16_t i, int32_t *j, int8_t k,
-                             void *(*l)(void *, int32_t *, int))
+
+int affine_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+                      int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
+                      int16_t qbit_input, int64_t *pt_accum, int8_t is_out,
+                      void *(*act)(void *, int32_t *, int)) /* affine.c:12-259 */
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l;
-    return unsupported("affine_Krows_8x16_acc32b");
+    return affine_rows_call(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias,
+                            qbit_input, pt_accum, NULL, is_out, act);
 }
-int rc_Krows_8x16(int16_t a, int16_t **b, int8_t **c, int8_t **d, int16_t **e, int16_t *f, int16_t *g,
-                  int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m,
-                  void *(*n)(void *, int32_t *, int))
+
+int affine_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+                             int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
+                             int16_t qbit_input, int32_t *pt_accum, int8_t is_out,
+                             void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:12-260 */
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n;
-    return unsupported("rc_Krows_8x16");
+    return affine_rows_call(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias,
+                            qbit_input, NULL, pt_accum, is_out, act);
 }
-int rc_Krows_8x16_acc32b(int16_t a, int16_t **b, int8_t **c, int8_t **d, int16_t **e, int16_t *f,
-                         int16_t *g, int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m,
-                         void *(*n)(void *, int32_t *, int))
+
+/* rc_Krows_8x16 (one group of <= 4 rows) and rc_8x16 (a whole layer) */
+static int rc_rows_call(int rows, int16_t *p_output, const int8_t *w, const int8_t *wr, const int16_t *bias,
+                        int16_t *input, int16_t *input_rec, int K, int Kr, int qk, int qb, int qi, int qir,
+                        int acc32, void *(*act)(void *, int32_t *, int), size_t *out_bytes)
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n;
-    return unsupported("rc_Krows_8x16_acc32b");
+    const int a_t = row_act(act, 1);
+    if (a_t < 0 || rows < 1 || K < 0 || Kr < 0) return -1;
+    begin();
+    RowArgs a;
+    memset(&a, 0, sizeof a);
+    a.mode = ROWS_RC;
+    a.rows = rows;
+    a.K = K;
+    a.Kr = Kr;
+    a.qk = qk; a.qb = qb; a.qi = qi; a.qir = qir;
+    a.acc32 = acc32;
+    a.is_out = 1;
+    a.act = a_t;
+    a.w = (const int8_t *)up(w, (size_t)rows * K);
+    a.wr = (const int8_t *)up(wr, (size_t)rows * Kr);
+    a.b = bias ? (const int16_t *)up(bias, (size_t)rows * 2) : NULL;
+    a.x = (const int16_t *)up(input, (size_t)K * 2);
+    a.xr = (const int16_t *)up(input_rec, (size_t)Kr * 2);
+    *out_bytes = (size_t)rows * (a_t == 3 ? 4 : 2);
+    a.out = up(NULL, *out_bytes);
+    CK(nnspk_launch_rows(&a, G.stream));
+    down(p_output, a.out, *out_bytes);
+    fin();
+    return 0;
 }
-int rc_8x16(int16_t *a, int8_t *b, int8_t *c, int16_t *d, int16_t *e, int16_t *f, int16_t g, int16_t h,
-            int16_t i, int16_t j, int16_t k, int16_t l, int16_t m, ACTIVATION_TYPE n,
-            void *(*o)(void *, int32_t *, int))
+
+static int rc_krows(int16_t R, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec, int16_t **pp_bias,
+                    int16_t *input, int16_t *input_rec, int16_t K, int16_t Kr, int16_t qk, int16_t qb, int16_t qi,
+                    int16_t qir, int acc32, void *(*act)(void *, int32_t *, int))
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n; (void)o;
-    return unsupported("rc_8x16");
+    if (R < 1 || R > 4) return -1;
+    size_t ob = 0;
+    if (rc_rows_call(R, *pp_output, *pp_kernel, *pp_kernel_rec, *pp_bias, input, input_rec, K, Kr, qk, qb, qi, qir,
+                     acc32, act, &ob))
+        return -1;
+    *pp_output = (int16_t *)((char *)*pp_output + ob);
+    *pp_kernel += (size_t)R * K;
+    *pp_kernel_rec += (size_t)R * Kr;
+    if (*pp_bias) *pp_bias += R;
+    return 0;
 }
-int rc_8x16_acc32b(int16_t *a, int8_t *b, int8_t *c, int16_t *d, int16_t *e, int16_t *f, int16_t g,
-                   int16_t h, int16_t i, int16_t j, int16_t k, int16_t l, int16_t m, ACTIVATION_TYPE n,
-                   void *(*o)(void *, int32_t *, int))
+
+int rc_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+                  int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec,
+                  int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                  void *(*act)(void *, int32_t *, int)) /* affine.c:348-407 */
 {
-    (void)a; (void)b; (void)c; (void)d; (void)e; (void)f; (void)g; (void)h; (void)i; (void)j; (void)k; (void)l; (void)m; (void)n; (void)o;
-    return unsupported("rc_8x16_acc32b");
+    return rc_krows(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input,
+                    dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 0, act);
 }
-void shift_64b(int64_t *x, int8_t shift, int len)
+
+int rc_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+                         int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input,
+                         int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input,
+                         int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:349-408 */
 {
-    (void)x; (void)shift; (void)len;
-    unsupported("shift_64b");
+    return rc_krows(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input,
+                    dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 1, act);
 }
-void shift_32b(int32_t *x, int8_t shift, int len)
+
+int rc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+            int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+            int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+            void *(*act)(void *, int32_t *, int)) /* affine.c:492-563 */
 {
-    (void)x; (void)shift; (void)len;
-    unsupported("shift_32b");
+    (void)act_type;
+    size_t ob = 0;
+    return rc_rows_call(dim_output, p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_input,
+                        dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 0, act, &ob);
 }
+
+int rc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+                   int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec,
+                   int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:493-564 */
+{
+    (void)act_type;
+    size_t ob = 0;
+    return rc_rows_call(dim_output, p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_input,
+                        dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 1, act, &ob);
+}
+
+static void shift_call(void *x, int shift, int len, int acc32)
+{
+    if (len <= 0 || shift == 0) return;
+    begin();
+    const size_t nb = (size_t)len * (acc32 ? 4 : 8);
+    void *d = up(x, nb);
+    CK(nnspk_launch_shift(d, shift, len, acc32, G.stream));
+    down(x, d, nb);
+    fin();
+}
+void shift_64b(int64_t *x, int8_t shift, int len) { shift_call(x, shift, len, 0); } /* affine.c:565-591 */
+void shift_32b(int32_t *x, int8_t shift, int len) { shift_call(x, shift, len, 1); } /* affine_acc32b.c:566-592 */

@@ -141,6 +141,25 @@ typedef struct {
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
 } FastRun;
 
+/* Legacy row-block primitives (affine_Krows_8x16*, rc_Krows_8x16*, rc_8x16*):
+ * one thread per output row; rows come in the reference's 4-row groups
+ * (remainder group last), weights interleaved as def_nn*.c store them. */
+#define ROWS_AFFINE 0   /* affine_Krows: acc[] in/out, one group of <= 4 rows */
+#define ROWS_RC 1       /* rc_Krows / rc_8x16: input half, shift, recurrent half + bias */
+typedef struct {
+    const int8_t *w, *wr;     /* input / recurrent weights */
+    const int16_t *b;         /* NULL: no bias */
+    const int16_t *x, *xr;    /* input / recurrent input */
+    void *out;                /* activation output (int16; int32 for linear) or NULL */
+    int64_t *acc;             /* ROWS_AFFINE: [rows] accumulators in/out (int32 values for acc32) */
+    int32_t mode, rows, K, Kr;
+    int32_t qk, qb, qi, qir;
+    int32_t acc32, is_out, act, pad;
+} RowArgs;
+int nnspk_launch_rows(const RowArgs *a, void *stream);
+/* shift_64b / shift_32b (affine.c:565-591, affine_acc32b.c:566-592) over n values */
+int nnspk_launch_shift(void *x, int shift, int n, int acc32, void *stream);
+
 /* 32-byte device post-processing state, one per stream */
 typedef struct {
     int16_t slides, trigger, argmax_last, pad0;

@@ -753,6 +753,81 @@ __global__ void k_nn_default(int16_t* h, int32_t* c, void* post, int n_lstm, con
     }
 }
 
+// Legacy row-block primitives (RowArgs, nnsp_kabi.h): one thread per output
+// row of a layer stored as 4-row groups, remainder group last (fc_8x16 /
+// rc_8x16, affine.c:409-563).  Byte of (row r, column c of a pair) inside a
+// group's column pair of R rows (Appendix B of SURVEY; affine.c:80-149):
+__device__ __forceinline__ int rows_wofs(int R, int r, int c) {
+    return R == 4 ? (r >> 1) * 4 + 2 * c + (r & 1) : (R == 3 ? (r < 2 ? 2 * c + r : 4 + c) : (R == 2 ? 2 * c + r : c));
+}
+// sum_k W[i][k] x[k] of row i (the SMLALD pairs, then the odd-column tail)
+__device__ int64_t rows_dot(const int8_t* w, const int16_t* x, int K, int rows, int i) {
+    const int g = i >> 2, r = i & 3, R = min(4, rows - 4 * g);
+    const int8_t* wg = w + (size_t)g * 4 * K;
+    const int o0 = rows_wofs(R, r, 0), o1 = rows_wofs(R, r, 1);
+    int64_t s = 0;
+    for (int p = 0; p < (K >> 1); ++p)
+        s += (int64_t)wg[2 * R * p + o0] * x[2 * p] + (int64_t)wg[2 * R * p + o1] * x[2 * p + 1];
+    if (K & 1) s += (int64_t)wg[(K >> 1) * 2 * R + r] * x[K - 1];
+    return s;
+}
+__device__ __forceinline__ int64_t wrap32(int64_t v) { return (int64_t)(int32_t)(uint32_t)(uint64_t)v; }
+
+// affine_Krows_8x16 (affine.c:12-259; _acc32b affine_acc32b.c:12-260) and
+// rc_Krows_8x16 (affine.c:348-407): accumulate, (rc: shift by qir - qi and add
+// the recurrent half), bias aligned to qbit_s, then if is_out the output
+// shift, clamp (acc64) and activation.  The "align acc" shift_64b on
+// pt_accum (affine.c:186-187) acts on values the sums then overwrite (T1).
+__global__ void k_rows(RowArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.rows) return;
+    int64_t s;
+    int qs;
+    if (a.mode == ROWS_RC) {
+        int64_t s1 = rows_dot(a.w, a.x, a.K, a.rows, i);   // no bias: qbit_s = qi + qk
+        if (a.acc32) s1 = shift32((int32_t)wrap32(s1), a.qir - a.qi);
+        else s1 = shift64(s1, a.qir - a.qi);
+        s = s1 + rows_dot(a.wr, a.xr, a.Kr, a.rows, i);
+        qs = a.b ? max(15, a.qir + a.qk) : a.qir + a.qk;
+    } else {
+        s = a.acc[i] + rows_dot(a.w, a.x, a.K, a.rows, i);
+        qs = a.b ? max(15, a.qi + a.qk) : a.qi + a.qk;
+    }
+    if (a.acc32) s = wrap32(s);
+    if (a.b) {
+        const int sh = qs - a.qb;
+        const int16_t bv = a.b[i];
+        if (a.acc32)
+            s = wadd((int32_t)s, sh >= 0 ? wshl(bv, sh) : ((int32_t)bv >> -sh));
+        else
+            s += sh >= 0 ? (int64_t)((uint64_t)(int64_t)bv << sh) : ((int64_t)bv >> -sh);
+    }
+    // is_out: shift_64b/32b(pt_accum, 15 - qbit_s) in place, then clamp (acc64) and act (affine.c:242-253)
+    if (a.is_out) s = a.acc32 ? (int64_t)shift32((int32_t)s, 15 - qs) : shift64(s, 15 - qs);
+    if (a.mode == ROWS_AFFINE) a.acc[i] = s;
+    if (a.is_out && a.out) {
+        const int32_t v = a.acc32 ? (int32_t)s : sat32(s);
+        if (a.act == ACT_LINEAR)
+            reinterpret_cast<int32_t*>(a.out)[i] = v;
+        else
+            reinterpret_cast<int16_t*>(a.out)[i] = a.act == ACT_RELU6 ? relu6_q12(v)
+                                                 : (a.act == ACT_TANH ? tanh_q15(v, nnsp_tbl_tanh)
+                                                                      : sigmoid_q15(v, nnsp_tbl_tanh));
+    }
+}
+
+__global__ void k_shift(void* x, int sh, int n, int acc32) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (acc32) {
+        int32_t* p = reinterpret_cast<int32_t*>(x);
+        p[i] = shift32(p[i], sh);
+    } else {
+        int64_t* p = reinterpret_cast<int64_t*>(x);
+        p[i] = shift64(p[i], sh);
+    }
+}
+
 // Synthetic PCM (bench / tests): SplitMix64(seed, stream, sample) -> int16 in
 // [-amp, amp-1]; identical to oracle.synthetic_pcm.
 __global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp) {
@@ -785,6 +860,18 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (blocks > 256 * 16) blocks = 256 * 16;
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 512) blocks = 512;   // at most 2 frames per switch
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_rows(const RowArgs* a, void* stream) {
+    if (a->rows <= 0) return 0;
+    hipLaunchKernelGGL(k_rows, dim3((a->rows + 63) / 64), dim3(64), 0, (hipStream_t)stream, *a);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_shift(void* x, int shift, int n, int acc32, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_shift, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, x, shift, n, acc32);
     return ok(hipGetLastError());
 }
 

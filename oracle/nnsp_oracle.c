@@ -380,6 +380,28 @@ static void rc_rows(int R, char **po, const int8_t **pw, const int8_t **pwr, con
     affine_rows(R, pwr, pb, h, Kr, qk, qb, qir, acc, acc32, 1, act, po);
 }
 
+void or_affine_krows(int32_t R, const int8_t *w, const int16_t *b, const int16_t *x, int32_t K, int32_t qk,
+                     int32_t qb, int32_t qi, int64_t *acc, int32_t acc32, int32_t is_out, int32_t act, void *out)
+{ /* affine.c:12-259 / affine_acc32b.c:12-260 */
+    const int8_t *pw = w;
+    const int16_t *pb = b;
+    char *po = (char *)out;
+    affine_rows(R, &pw, b ? &pb : NULL, x, K, qk, qb, qi, acc, acc32, is_out, act, &po);
+}
+
+void or_rc_layer(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b, const int16_t *x,
+                 const int16_t *h, int32_t K, int32_t Kr, int32_t qk, int32_t qb, int32_t qi, int32_t qir,
+                 int32_t act, int32_t acc32, void *out)
+{ /* rc_8x16, affine.c:492-563: 4-row groups, remainder last */
+    char *po = (char *)out;
+    const int8_t *pw = w, *pwr = wr;
+    const int16_t *pb = b;
+    for (int r0 = 0; r0 < N; r0 += 4)
+        rc_rows(N - r0 >= 4 ? 4 : N - r0, &po, &pw, &pwr, b ? &pb : NULL, x, h, K, Kr, qk, qb, qi, qir, act, acc32);
+}
+
+void or_shift(int64_t *a, int32_t sh, int32_t n, int32_t acc32) { shift_acc(a, sh, n, acc32); }
+
 static void fc_layer(char *out, const int8_t *w, const int16_t *b, const int16_t *x, int N, int K,
                      int qk, int qb, int qi, int act, int acc32) /* affine.c:409-490 */
 {

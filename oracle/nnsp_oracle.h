@@ -81,6 +81,16 @@ void or_fe_exec(or_stream *st, const or_cfg *cfg, const int16_t *pcm160);
 
 /* activations (type = OR_*); y is int16 except OR_LINEAR (int32) */
 void or_act(int32_t type, const int32_t *x, void *y, int32_t n);
+/* row-block primitives as the legacy API exposes them (test entry points):
+ * affine_Krows_8x16(_acc32b) on R <= 4 rows with accumulators in/out (int32
+ * values for acc32; b NULL: no bias); rc_8x16(_acc32b) on a whole layer of N
+ * rows in 4-row groups; shift_64b / shift_32b */
+void or_affine_krows(int32_t R, const int8_t *w, const int16_t *b, const int16_t *x, int32_t K, int32_t qk,
+                     int32_t qb, int32_t qi, int64_t *acc, int32_t acc32, int32_t is_out, int32_t act, void *out);
+void or_rc_layer(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b, const int16_t *x,
+                 const int16_t *h, int32_t K, int32_t Kr, int32_t qk, int32_t qb, int32_t qi, int32_t qir,
+                 int32_t act, int32_t acc32, void *out);
+void or_shift(int64_t *a, int32_t sh, int32_t n, int32_t acc32);
 
 /* NN */
 void or_nn_reset(const or_net *net, or_stream *st);

@@ -75,7 +75,7 @@ def _check(oc, gc, pcm, chunks, reset_at=None, reset_mask=None):
 
 @pytest.mark.parametrize("th", ["lively", "slow"])
 @pytest.mark.parametrize("acc32", [False, True])
-@pytest.mark.parametrize("window", [32, 0])
+@pytest.mark.parametrize("window", [32, 12, 0])
 def test_cascade_matches_oracle(th, acc32, window):
     S, chunks = 150, [100, 37, 1, 63]
     oc, gc, _ = _build(TH[th], S, max(chunks), acc32, (1, 2, 0), 80, 60, 80, 50)

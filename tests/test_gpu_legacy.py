@@ -1,0 +1,197 @@
+"""GPU parity of the single-stream drop-in API (include/nnsp_api.h, the
+reference's ns-nnsp C API) against the CPU oracle, bit for bit.
+
+Every legacy entry point runs the gfx950 kernels on a batch of one
+(nnsp_amd/csrc/host/nnsp_legacy.c): the front-end stages (arm_fft_exec,
+spec2pspec_arm, melSpecProc, log10_vec), the activations, the row-block
+primitives (affine_Krows_8x16*, rc_Krows_8x16*, rc_8x16*, shift_64b/32b),
+NeuralNetClass_exe, FeatureClass_execute and NNSPClass_exec per frame.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle as O
+from oracle import OracleNet, synthetic_pcm
+
+from nnsp_amd import _lib
+from nnsp_amd.nets import synth_net
+
+pytestmark = pytest.mark.gpu
+
+ACT_FN = {0: "relu6_fix", 1: "tanh_fix", 2: "sigmoid_fix", 3: "linear_fix"}
+_KEEP = []   # nets stay alive for the session: their tables' addresses are never reused
+
+
+def L():
+    return _lib.lib()
+
+
+def vp(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+def fn(name):
+    return C.c_void_p(_lib.fn_addr(name))
+
+
+def test_front_end_stages():
+    rng = np.random.default_rng(1)
+    L().arm_fft_init()
+    for amp in (1 << 12, 1 << 20, 1 << 29):
+        x = np.zeros(514, np.int32)
+        x[:480] = rng.integers(-amp, amp, 480)
+        oy, ox = O.rfft512(x[:512])
+        y = np.zeros(1024, np.int32)
+        L().arm_fft_exec(vp(y), vp(x))
+        np.testing.assert_array_equal(y, oy)
+        np.testing.assert_array_equal(x[:512], ox)   # pSrc is transformed in place (CMSIS)
+        p = np.zeros(1024, np.int32)
+        L().spec2pspec_arm(vp(p), vp(y), 257)
+        np.testing.assert_array_equal(p[:257], O.spec2pspec(y))
+        m = np.zeros(40, np.int32)
+        L().melSpecProc(vp(p), vp(m))
+        np.testing.assert_array_equal(m, O.mel(p[:257]))
+        lg = np.zeros(40, np.int32)
+        L().log10_vec(vp(lg), vp(m), 40, 15)
+        np.testing.assert_array_equal(lg, O.log10(m))
+
+
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+def test_activations(kind):
+    x = np.concatenate([np.arange(-200000, 200000, 97), [0, 1, -1, 2 ** 31 - 1, -2 ** 31 + 1]]).astype(np.int32)
+    y = np.zeros(len(x), np.int32 if kind == 3 else np.int16)
+    getattr(L(), ACT_FN[kind])(vp(y), vp(x), len(x))
+    np.testing.assert_array_equal(y, O.act(kind, x))
+
+
+QBITS = [(7, 14, 8), (5, 13, 15), (6, 13, 8), (4, 14, 12), (7, 15, 12)]
+
+
+@pytest.mark.parametrize("acc32", [False, True])
+@pytest.mark.parametrize("R", [1, 2, 3, 4])
+def test_affine_krows(R, acc32):
+    rng = np.random.default_rng(R + 10 * acc32)
+    f = L().affine_Krows_8x16_acc32b if acc32 else L().affine_Krows_8x16
+    for K in (240, 27, 2):
+        for qk, qb, qi in QBITS:
+            for act in (0, 1, 2, 3):
+                for bias in (True, False):
+                    for is_out in (1, 0):
+                        w = rng.integers(-128, 128, R * K).astype(np.int8)
+                        b = rng.integers(-9000, 9000, R).astype(np.int16)
+                        x = rng.integers(-32768, 32768, K).astype(np.int16)
+                        acc = rng.integers(-2 ** 22, 2 ** 22, 4).astype(np.int64)
+                        oacc = acc.copy()
+                        oout = np.zeros(R, np.int32 if act == 3 else np.int16)
+                        O.lib().or_affine_krows(R, vp(w), vp(b) if bias else None, vp(x), K, qk, qb, qi, vp(oacc),
+                                                int(acc32), is_out, act, vp(oout))
+                        gacc = acc.astype(np.int32) if acc32 else acc.copy()
+                        gout = np.zeros(R, oout.dtype)
+                        po, pw = C.c_void_p(gout.ctypes.data), C.c_void_p(w.ctypes.data)
+                        pb = C.c_void_p(b.ctypes.data if bias else None)
+                        assert f(R, C.byref(po), C.byref(pw), C.byref(pb), vp(x), K, qk, qb, qi, vp(gacc),
+                                 is_out, fn(ACT_FN[act])) == 0
+                        np.testing.assert_array_equal(gacc[:R].astype(np.int64), oacc[:R])
+                        if is_out:
+                            np.testing.assert_array_equal(gout, oout)
+                        assert pw.value == w.ctypes.data + R * K
+                        assert (pb.value or 0) == (b.ctypes.data + 2 * R if bias else 0)
+                        assert po.value == gout.ctypes.data + (gout.nbytes if is_out else 0)
+
+
+@pytest.mark.parametrize("acc32", [False, True])
+@pytest.mark.parametrize("N", [4, 7, 28, 41, 72])
+def test_rc_layer_and_krows(N, acc32):
+    rng = np.random.default_rng(N + 100 * acc32)
+    for K, Kr in ((28, 28), (240, 72), (9, 5)):
+        for qk, qb, qi in QBITS:
+            qir = 15
+            for act in (1, 2, 3):
+                w = rng.integers(-128, 128, N * K).astype(np.int8)
+                wr = rng.integers(-128, 128, N * Kr).astype(np.int8)
+                b = rng.integers(-9000, 9000, N).astype(np.int16)
+                x = rng.integers(-32768, 32768, K).astype(np.int16)
+                h = rng.integers(-32768, 32768, Kr).astype(np.int16)
+                dt = np.int32 if act == 3 else np.int16
+                oout = np.zeros(N, dt)
+                O.lib().or_rc_layer(N, vp(w), vp(wr), vp(b), vp(x), vp(h), K, Kr, qk, qb, qi, qir, act, int(acc32),
+                                    vp(oout))
+                gout = np.zeros(N, dt)
+                f = L().rc_8x16_acc32b if acc32 else L().rc_8x16
+                assert f(vp(gout), vp(w), vp(wr), vp(b), vp(x), vp(h), N, K, Kr, qk, qb, qi, qir, act,
+                         fn(ACT_FN[act])) == 0
+                np.testing.assert_array_equal(gout, oout)
+                # the same layer through rc_Krows_8x16 one 4-row group at a time
+                g2 = np.zeros(N, dt)
+                po, pw, pwr, pb = (C.c_void_p(a.ctypes.data) for a in (g2, w, wr, b))
+                fk = L().rc_Krows_8x16_acc32b if acc32 else L().rc_Krows_8x16
+                for r0 in range(0, N, 4):
+                    assert fk(min(4, N - r0), C.byref(po), C.byref(pw), C.byref(pwr), C.byref(pb), vp(x), vp(h), K,
+                              Kr, qk, qb, qi, qir, fn(ACT_FN[act])) == 0
+                np.testing.assert_array_equal(g2, oout)
+                assert pw.value == w.ctypes.data + N * K and pwr.value == wr.ctypes.data + N * Kr
+                assert pb.value == b.ctypes.data + 2 * N and po.value == g2.ctypes.data + g2.nbytes
+
+
+@pytest.mark.parametrize("acc32", [False, True])
+def test_shift(acc32):
+    rng = np.random.default_rng(5)
+    for sh in (-31, -7, -1, 0, 1, 5, 20):
+        v = rng.integers(-2 ** 62, 2 ** 62, 300, dtype=np.int64)
+        if acc32:
+            v = rng.integers(-2 ** 31, 2 ** 31, 300).astype(np.int64)
+            if sh < -30:
+                continue
+        o = v.copy()
+        O.lib().or_shift(vp(o), sh, len(o), int(acc32))
+        if acc32:
+            g = v.astype(np.int32)
+            L().shift_32b(vp(g), sh, len(g))
+        else:
+            g = v.copy()
+            L().shift_64b(vp(g), sh, len(g))
+        np.testing.assert_array_equal(g.astype(np.int64), o)
+
+
+@pytest.mark.parametrize("name", ["vad", "kws", "s2i"])
+def test_neural_net_exe(name):
+    data = synth_net(name, 21)
+    orc = OracleNet(data)
+    h = _lib.NetHandle(data)
+    _KEEP.append(h)
+    L().NeuralNetClass_setDefault(C.c_void_p(h.addr))
+    st = orc.new_states(1)[0]
+    rng = np.random.default_rng(3)
+    for _ in range(4):   # the LSTM state carries across calls
+        x = rng.integers(-20000, 20000, 240).astype(np.int16)
+        out = np.zeros(64, np.int32)
+        L().NeuralNetClass_exe(C.c_void_p(h.addr), vp(x), vp(out), -1)
+        o = orc.forward(x, st)
+        np.testing.assert_array_equal(out[:orc.nout], o[:orc.nout])
+
+
+@pytest.mark.parametrize("name", ["vad", "s2i"])
+def test_nnsp_exec_per_frame(name):
+    data = synth_net(name, 8)
+    orc = OracleNet(data, thresh_prob=3000, th_count=1)
+    h = _lib.NetHandle(data)
+    _KEEP.append(h)
+    feat = _lib.FeatureClass()
+    inst = _lib.NNSPClass()
+    thr = np.array([3000], np.int16)
+    cnt = np.array([1], np.int16)
+    nn_id = {"s2i": 0, "vad": 1, "kws": 2}[name]
+    assert L().NNSPClass_init(C.byref(inst), C.c_void_p(h.addr), C.byref(feat), bytes([nn_id]), vp(h.mean),
+                              vp(h.stdR), vp(thr), vp(cnt)) == 0
+    L().NNSPClass_reset(C.byref(inst))
+    T = 14
+    pcm = synthetic_pcm(1, T, seed=77)
+    o_trig, _, o_feat, _ = orc.run(pcm)
+    for t in range(T):
+        frame = np.ascontiguousarray(pcm[0, t])
+        trig = L().NNSPClass_exec(C.byref(inst), vp(frame))
+        assert trig == o_trig[0, t], f"frame {t}"
+        ctx5 = np.ctypeslib.as_array(feat.normFeatContext)[200:240]
+        np.testing.assert_array_equal(ctx5, o_feat[0, t], err_msg=f"features frame {t}")
