@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 # algorithmic work per frame (denominators of roofline.achieved)
 FE_MULS_PER_FRAME = 5912           # integer multiplies of one front-end frame
 NN_MACS_PER_INFERENCE = {"vad": 14616, "kws": 56448, "s2i": 72072}
-FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out
+FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out (cascade: + 80, int32 log-Mel out)
 
 WORKLOADS = {  # BASELINE.json configs
     "cascade": "configs[4]: VAD->Hi-Galaxy KWS->S2I cascade, 32768 streams/GPU (262144 on 8 GPUs)",
@@ -193,16 +193,31 @@ def main() -> None:
     if rank == 0:
         info = device_info()
         cu, clk = info["compute_units"], info["clock_khz"] * 1e3
-        valu_peak = cu * 128 * clk / 1e12          # int32 VALU lane-ops/s (4 SIMD32 per CU)
+        valu_peak = cu * 128 * clk / 1e12          # VALU lane-ops/s (4 SIMDs x 32 lanes per clock per CU)
+        # integer multiplies issue at about half the add rate on gfx950: the
+        # front end's ceiling is the measured v_mul_hi_i32 rate on all CUs
+        # (profiles/microbench/valu_rates.hip, run on MI355X), scaled to this device
+        mul_peak, mul_src = valu_peak * 0.5, "half the VALU lane-op rate (no probe file)"
+        try:
+            with open(os.path.join(ROOT, "profiles", "microbench", "valu_rates_mi355x.json")) as f:
+                vr = json.load(f)
+            mul_peak = vr["rates"]["v_mul_hi_i32"] / 1e12 * (cu * clk) / (vr["compute_units"] * vr["clock_khz"] * 1e3)
+            mul_src = "measured v_mul_hi_i32 issue rate, profiles/microbench/valu_rates_mi355x.json"
+        except Exception:
+            pass
         mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
-        dom = max((k for k in kt if not k.startswith("feat_")), key=kt.get)   # dominant kernel by device time
+        # dominant kernel by device time.  In the cascade the nets' segment
+        # kernels run concurrently on three streams, so their event spans are
+        # not kernel durations; the one-launch shared front end is the largest
+        # kernel there (profiles/*/kernel_stats.csv)
+        dom = "fe_kernel" if cascade else max(kt, key=kt.get)
         launches = klaunch[dom]
         avg_launch_s = kt[dom] / 1e3 / launches    # HIP-event time on the engine's stream
         units = kframes[dom] / launches            # frames per launch
         if dom == "fe_kernel":
             per_unit = FE_MULS_PER_FRAME
             work = "integer multiplies (SURVEY 8(d): 5912 per frame) x frames per launch"
-            peak, bound = valu_peak, "valu"
+            peak, bound = mul_peak, "valu"
         else:
             n = dom[3:]
             per_unit = NN_MACS_PER_INFERENCE[n]    # one inference per 2 frames, 2 ops per MAC
@@ -239,10 +254,13 @@ def main() -> None:
             "roofline": {"kernel": dom, "bound": bound,
                          "achieved": achieved, "peak": peak, "unit": "Tops/s",
                          "frac": achieved / peak, "work": work,
+                         "peak_source": mul_src if dom == "fe_kernel" else "dense int8 MFMA (MI355X_MICROARCH.md)",
+                         "valu_lane_peak": valu_peak,
                          "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC, profiles/)",
                          "launches_per_step": launches / K, "avg_launch_ms": avg_launch_s * 1e3,
                          "frames_per_launch": units,
-                         "hbm_achieved_GBps": kframes["fe_kernel"] * FE_HBM_BYTES_PER_FRAME / fe_s / 1e9,
+                         "hbm_achieved_GBps": kframes["fe_kernel"] * (FE_HBM_BYTES_PER_FRAME + (80 if cascade else 0))
+                         / fe_s / 1e9,
                          "hbm_peak_GBps": 8000.0},
             "device": info,
         }

@@ -15,9 +15,15 @@ import sys
 from collections import defaultdict
 
 
-def kname(full: str) -> str:
+def kname(full: str, grid: int = 0) -> str:
     base = full.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").strip()
-    return base.split("<")[0]
+    base = base.split("<")[0]
+    # the cascade launches fe_kernel twice over: once per chunk on every frame
+    # (FE_MODE_SHARED, the full 4096-workgroup grid) and per round on the few
+    # frames after net resets (FE_MODE_COLD, <= 512 workgroups)
+    if base == "fe_kernel" and 0 < grid < 1024 * 256:
+        return "fe_kernel[cold]"
+    return base
 
 
 def per_kernel(path_glob, counter):
@@ -26,7 +32,7 @@ def per_kernel(path_glob, counter):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 if row.get("Counter_Name") == counter:
-                    acc[kname(row["Kernel_Name"])].append(float(row["Counter_Value"]))
+                    acc[kname(row["Kernel_Name"], int(row.get("Grid_Size") or 0))].append(float(row["Counter_Value"]))
     return acc
 
 
@@ -36,7 +42,7 @@ def main():
     for f in glob.glob(os.path.join(d, "kt", "**", "*kernel_trace.csv"), recursive=True):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                dur[kname(row["Kernel_Name"])].append(
+                dur[kname(row["Kernel_Name"], int(row.get("Grid_Size_X") or 0))].append(
                     (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6)
     fetch = per_kernel(os.path.join(d, "fetch", "**", "*counter_collection.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(d, "write", "**", "*counter_collection.csv"), "WRITE_SIZE")
