@@ -164,11 +164,7 @@ def main() -> None:
             kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
             klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + 1
             for n in ("vad", "kws", "s2i"):
-                f, fe, nn, nl = eng.net_stats(n)
-                kt[f"feat_{n}"] = kt.get(f"feat_{n}", 0.0) + fe   # seg_norm + cold-frame front end
-                kframes[f"feat_{n}"] = kframes.get(f"feat_{n}", 0) + f
-                klaunch[f"feat_{n}"] = klaunch.get(f"feat_{n}", 0) + nl
-                kt[f"nn_{n}"] = kt.get(f"nn_{n}", 0.0) + nn
+                f, _, _, nl = eng.net_stats(n)   # per-net device times: instrumented step below
                 kframes[f"nn_{n}"] = kframes.get(f"nn_{n}", 0) + f
                 klaunch[f"nn_{n}"] = klaunch.get(f"nn_{n}", 0) + nl
         else:
@@ -187,6 +183,19 @@ def main() -> None:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    net_ms = {}
+    if cascade:
+        # per-net device time per round (HIP events around each net's work):
+        # one extra, untimed chunk with the events on -- they cost a few
+        # percent, so the timed steps run without them.  The nets run
+        # concurrently on three streams: these spans overlap.
+        eng.set_timing(True)
+        step(bufs[W + K - 1])
+        eng.sync()
+        eng.set_timing(False)
+        for n in ("vad", "kws", "s2i"):
+            f, fe, nn, nl = eng.net_stats(n)
+            net_ms[n] = {"cold_fe_ms": fe, "nn_ms": nn, "frames": f, "rounds": nl}
     frames = S * T * K * world
     value = frames / elapsed
 
@@ -250,6 +259,7 @@ def main() -> None:
                        "frames_per_step": T, "accumulator": "32b" if args.acc32 else "64b",
                        "parallelism": f"stream shards x{world}"},
             "kernels_ms_per_step": {k: v / K for k, v in kt.items()},
+            **({"nets_one_chunk": net_ms} if cascade else {}),
             "frames_scheduled_per_step": {k: v // K for k, v in kframes.items()},
             "roofline": {"kernel": dom, "bound": bound,
                          "achieved": achieved, "peak": peak, "unit": "Tops/s",

@@ -73,11 +73,17 @@ void *nnsp_cascade_stream(nnsp_cascade *c);
  * work past a switch that the switch discarded), device time in ms. */
 int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run, float *ms);
 
+/* Per-round, per-net device timing (HIP events around each net's work in
+ * every round) for nnsp_cascade_last_net_stats.  Off by default: the events
+ * cost a few percent of throughput (environment NNSP_CASCADE_TIMING=1 turns
+ * it on at create time). */
+int nnsp_cascade_set_timing(nnsp_cascade *c, int on);
+
 /* Last chunk, one net (NNSP_ID): frames scheduled on it, the device time of
- * its segment features (normalisation of the shared log-Mel + the front end
- * of the frames right after its resets) and of its NN kernels (proj + recur +
- * context roll) summed over the rounds, and the number of rounds it ran in
- * (one launch of each kernel per round). */
+ * the front end of the frames right after its resets and of its NN kernels
+ * (proj + recur, the controller fused in) summed over the rounds (0 unless
+ * timing is on), and the number of rounds it ran in (one launch of each
+ * kernel per round). */
 int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_run, float *fe_ms,
                                 float *nn_ms, int *launches);
 

@@ -110,6 +110,7 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_exec_device": (I, [P, P, I, P, P, P]),
         "nnsp_cascade_sync": (I, [P]),
         "nnsp_cascade_set_window": (I, [P, I]),
+        "nnsp_cascade_set_timing": (I, [P, I]),
         "nnsp_cascade_stream": (P, [P]),
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),

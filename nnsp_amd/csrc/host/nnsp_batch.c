@@ -343,7 +343,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
         f.ep_lo = b->ep_rec_lo;
         f.ep_n = b->ep_rec_n;
-        TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, stream));
+        TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, seg->ctl, stream));
     } else {
         NnRun r;
         memset(&r, 0, sizeof r);

@@ -47,7 +47,9 @@ struct nnsp_cascade {
     unsigned long long *d_frames;
     int16_t *d_trig[3], *d_out3[3];
     uint8_t *d_mask[3];
-    int32_t *d_list[3], *d_cold_list[3];
+    /* per round parity and net: the round's stream lists (round r reads
+     * [r & 1] while its kernels append the next round's to [(r + 1) & 1]) */
+    int32_t *d_list[2][3], *d_cold_list[2][3];
     int16_t *d_hist[2];
     int hist_cur;
     int32_t *d_lmel;                /* [S][ring][40] shared log-Mel */
@@ -64,9 +66,13 @@ struct nnsp_cascade {
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
+    void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
     int window;                     /* frames per stream and round (0: to the chunk end) */
+    int serial;                     /* NNSP_CASCADE_SERIAL: the nets' work on the main stream (no fork/join) */
+    int fused;                      /* controller fused into the nets' recur kernels (compiled shapes) */
+    int timing;                     /* per-round, per-net device timing (set_timing; NNSP_CASCADE_TIMING) */
     float sfe_ms;                   /* last chunk: shared front end */
     float fe_ms[3], nn_ms[3];       /* last chunk, per net id: features / proj+recur+roll */
     int runs[3];                    /* last chunk, per net id: segment runs */
@@ -123,7 +129,9 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
     for (int n = 0; n < 3; ++n) {
-        if ((e = nnspk_stream_create(&c->ns[n])) || (e = nnspk_event_create(&c->ev_join[n]))) goto fail;
+        if ((e = nnspk_stream_create(&c->ns[n])) || (e = nnspk_event_create(&c->ev_join[n])) ||
+            (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
+            goto fail;
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i)
                 if ((e = nnspk_event_create(&c->ev_t[r][n][i]))) goto fail;
@@ -143,8 +151,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         if ((e = nnspk_malloc((void **)&c->d_trig[i], S * T * 2))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_out3[i], S * T * 6))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_mask[i], S))) goto fail;
-        if ((e = nnspk_malloc((void **)&c->d_list[i], S * 4))) goto fail;
-        if ((e = nnspk_malloc((void **)&c->d_cold_list[i], S * 4))) goto fail;
+        for (int k = 0; k < 2; ++k) {
+            if ((e = nnspk_malloc((void **)&c->d_list[k][i], S * 4))) goto fail;
+            if ((e = nnspk_malloc((void **)&c->d_cold_list[k][i], S * 4))) goto fail;
+        }
         if ((e = nnspk_memset(c->d_mask[i], 0, S, c->stream))) goto fail;
     }
     for (int i = 0; i < 2; ++i)
@@ -173,8 +183,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             a->c[i] = nets[i]->d_c;
             a->post[i] = nets[i]->d_post;
             a->prev_default[i] = c->d_pdef + 40 * i;
-            a->list[i] = c->d_list[i];
-            a->cold_list[i] = c->d_cold_list[i];
+            a->list[i] = c->d_list[0][i]; /* round 0 (casc_begin); set per round */
+            a->cold_list[i] = c->d_cold_list[0][i];
             FeatSrc *fs = &a->fs[i];
             fs->lmel = c->d_lmel;
             fs->fresh = c->d_fresh;
@@ -203,6 +213,14 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     }
     c->window = 12;
     {
+        c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
+        /* the controller runs inside the nets' pipelined recur kernels when all
+         * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
+         * casc_control launch per round instead) */
+        c->fused = !c->serial && getenv("NNSP_CASCADE_CONTROL_KERNEL") == NULL;
+        for (int i = 0; i < 3; ++i)
+            if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
+        c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w) c->window = atoi(w);
     }
@@ -220,10 +238,11 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     if (c->stream) nnspk_sync(c->stream);
     void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_counts,  c->d_frames,  c->d_trig[0], c->d_trig[1],
                     c->d_trig[2], c->d_out3[0],   c->d_out3[1], c->d_out3[2], c->d_mask[0], c->d_mask[1],
-                    c->d_mask[2], c->d_list[0],   c->d_list[1], c->d_list[2], c->d_hist[0], c->d_hist[1],
+                    c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1],
                     c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
-                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round, c->d_cold_list[0],
-                    c->d_cold_list[1], c->d_cold_list[2]};
+                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round, c->d_cold_list[0][0],
+                    c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
+                    c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2]};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 2; ++i) {
         nnspk_event_destroy(c->ev[i]);
@@ -232,6 +251,8 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     nnspk_event_destroy(c->ev_fork);
     for (int n = 0; n < 3; ++n) {
         nnspk_event_destroy(c->ev_join[n]);
+        nnspk_event_destroy(c->ev_rnd[0][n]);
+        nnspk_event_destroy(c->ev_rnd[1][n]);
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
         nnspk_stream_destroy(c->ns[n]);
@@ -261,7 +282,7 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 /* features of net n for this round's segments: the full front end for the
  * frames right after the net's reset (the others are normalised from the
  * shared log-Mel by the kernels that read them, FeatSrc) */
-static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, const int32_t *cnt,
+static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, int T, const int32_t *cnt,
                             const int16_t *hist, void *stream)
 {
     nnsp_batch *b = c->net[n];
@@ -274,7 +295,7 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.stdR = b->d_stdR;
     fa.norm_shift = b->norm_shift;
     fa.feats = b->d_feats;
-    fa.list = c->d_list[n];
+    fa.list = c->d_list[r & 1][n];
     fa.n_list_dev = cnt + n;
     fa.seg_begin = c->d_seg_begin;
     fa.lookback = c->lookback[n];
@@ -286,28 +307,47 @@ static int segment_features(nnsp_cascade *c, int n, const int16_t *pcm, int T, c
     fa.lmel = c->d_lmel;
     fa.fresh = c->d_fresh;
     fa.mode = FE_MODE_COLD;
-    fa.list = c->d_cold_list[n];
+    fa.list = c->d_cold_list[r & 1][n];
     fa.n_list_dev = cnt + 3 + n;
     fa.n_list_rec = NULL;
     return nnspk_launch_fe(&fa, stream);
 }
 
 /* One round, asynchronous: the three nets' segments on their own streams
- * (empty lists exit on the device), then casc_control on the main stream. */
+ * (empty lists exit on the device).  Fused control: each net's recur kernel
+ * runs the controller for its streams and lists them for the next round, so
+ * a net's next round waits only for the other two nets' end of this round.
+ * Otherwise: join, casc_control on the main stream, fork. */
 static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm, int T, const int16_t *hist)
 {
     int32_t *cur = c->d_counts + 6 * (r % 3);
-    TRY(nnspk_event_record(c->ev_fork, c->stream));
+    a->counts = c->d_counts + 6 * ((r + 1) % 3);
+    a->counts_clear = c->d_counts + 6 * ((r + 2) % 3);
+    a->round = r;
     for (int n = 0; n < 3; ++n) {
-        void *st = c->ns[n];
-        const int timed = r < MAX_TIMED;
-        TRY(nnspk_stream_wait(st, c->ev_fork));
+        a->list[n] = c->d_list[(r + 1) & 1][n];
+        a->cold_list[n] = c->d_cold_list[(r + 1) & 1][n];
+    }
+    if (!c->serial && !c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
+    for (int n = 0; n < 3; ++n) {
+        void *st = c->serial ? c->stream : c->ns[n];
+        const int timed = c->timing && r < MAX_TIMED;
+        if (c->fused) {
+            if (r == 0) {
+                TRY(nnspk_stream_wait(st, c->ev_fork)); /* casc_begin */
+            } else {
+                for (int m = 0; m < 3; ++m)
+                    if (m != n) TRY(nnspk_stream_wait(st, c->ev_rnd[(r - 1) & 1][m]));
+            }
+        } else if (!c->serial) {
+            TRY(nnspk_stream_wait(st, c->ev_fork));
+        }
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
-        TRY(segment_features(c, n, pcm, T, cur, hist, st));
+        TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
         nnsp_segment seg;
         memset(&seg, 0, sizeof seg);
-        seg.list = c->d_list[n];
+        seg.list = c->d_list[r & 1][n];
         seg.n_list_dev = cur + n;
         seg.seg_begin = c->d_seg_begin;
         seg.lookback = c->lookback[n];
@@ -319,16 +359,27 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         seg.outputs3 = a->outputs3;
         seg.net_id = n;
         seg.fs = a->fs[n];
-        seg.n_list_rec = timed ? c->d_rcount + 3 * r + n : NULL;
-        TRY(nnsp_batch_run_nn(c->net[n], T, c->d_trig[n], NULL, &seg, st));
+        seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
+        seg.ctl = c->fused ? a : NULL;
+        TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
-        TRY(nnspk_event_record(c->ev_join[n], st));
-        TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
+        if (c->fused) {
+            TRY(nnspk_event_record(c->ev_rnd[r & 1][n], st));
+        } else if (!c->serial) {
+            TRY(nnspk_event_record(c->ev_join[n], st));
+            TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
+        }
     }
-    a->counts = c->d_counts + 6 * ((r + 1) % 3);
-    a->counts_clear = c->d_counts + 6 * ((r + 2) % 3);
-    a->round = r;
+    if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
+}
+
+/* fused control: the main stream waits for the nets' last launched round */
+static int join_rounds(nnsp_cascade *c, int r)
+{
+    if (!c->fused || r <= 0) return 0;
+    for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[(r - 1) & 1][n]));
+    return 0;
 }
 
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran, int16_t *detected,
@@ -368,13 +419,19 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
         TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     }
     a.counts = c->d_counts; /* round 0's lists */
+    for (int n = 0; n < 3; ++n) {
+        a.list[n] = c->d_list[0][n];
+        a.cold_list[n] = c->d_cold_list[0][n];
+    }
     TRY(nnspk_launch_casc_begin(&a, c->stream));
+    if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
     /* rounds run without host round trips: launch as many as the last chunk
      * needed, then check the next round's list lengths (one read-back) */
     const int16_t *hist = c->d_hist[c->hist_cur];
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
         for (; r < R; ++r) TRY(launch_round(c, &a, r, pcm, T, hist));
+        TRY(join_rounds(c, r));
         int32_t cnt[3];
         TRY(nnspk_d2h(cnt, c->d_counts + 6 * (r % 3), 12, c->stream));
         TRY(nnspk_sync(c->stream));
@@ -401,12 +458,13 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
         c->runs[n] = 0;
         for (int k = 0; k < r && k < MAX_TIMED; ++k) {
             if (!rc[k][n]) continue;
+            c->runs[n]++;
+            if (!c->timing) continue;
             float fe = 0.f, nn = 0.f;
             TRY(nnspk_event_elapsed(&fe, c->ev_t[k][n][0], c->ev_t[k][n][1]));
             TRY(nnspk_event_elapsed(&nn, c->ev_t[k][n][1], c->ev_t[k][n][2]));
             c->fe_ms[n] += fe;
             c->nn_ms[n] += nn;
-            c->runs[n]++;
         }
     }
     return 0;
@@ -440,6 +498,13 @@ int nnsp_cascade_set_window(nnsp_cascade *c, int frames)
 {
     if (!c || frames < 0) return NNSP_EINVAL;
     c->window = frames;
+    return 0;
+}
+
+int nnsp_cascade_set_timing(nnsp_cascade *c, int on)
+{
+    if (!c) return NNSP_EINVAL;
+    c->timing = on != 0;
     return 0;
 }
 

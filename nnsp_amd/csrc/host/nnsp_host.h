@@ -82,6 +82,7 @@ typedef struct {
     int8_t *net_ran;           /* cascade: the caller's per-frame outputs (NULL skips) */
     int16_t *detected, *outputs3;
     int net_id;
+    const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

@@ -16,47 +16,17 @@
 #include <stdint.h>
 
 #include "nnsp_kabi.h"
+#include "nnsp_casc.h"
 #include "nnsp_nn.h"
 
 using nnsp::feat8;
 
 namespace {
 
+using nnsp::add_frames;
+using nnsp::list_next;
+
 inline int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
-
-// Append s to list[n] for every lane with want; one atomic per wave and net.
-__device__ __forceinline__ void list_push(int32_t* const* lists, int32_t* counts, int n, int s, bool want) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const bool mine = want && n == k;
-        const unsigned long long m = __ballot(mine);
-        if (!m) continue;
-        const int leader = __ffsll((long long)m) - 1;
-        int base = 0;
-        if (lane == leader) base = atomicAdd(&counts[k], __popcll(m));
-        base = __shfl(base, leader);
-        if (mine) lists[k][base + __popcll(m & ((1ull << lane) - 1ull))] = s;
-    }
-}
-
-// list s under net n for the next round; also on n's cold list while the
-// net's STFT buffer still holds zeros from its reset (the front end runs in
-// full for those frames)
-__device__ __forceinline__ void list_next(const CascArgs& a, int n, int s, bool want, int fresh) {
-    list_push(a.list, a.counts, n, s, want);
-    list_push(a.cold_list, a.counts + 3, n, s, want && fresh < 2);
-}
-
-__device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned long long v) {
-    // per net: wave-reduce, one atomic per wave
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        unsigned long long x = n == k ? v : 0ull;
-        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-        if ((threadIdx.x & 63) == 0 && x && a.frames) atomicAdd(&a.frames[k], x);
-    }
-}
 
 __global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -94,34 +64,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
                 for (int k = 0; k < 16; ++k) dq[k] = t + k < e ? tr[t + k] : (int16_t)0;
             }
             const int16_t det = dq[(t - b) & 15];
-            bool move = false, rst = false;
-            int np = st.pos;
-            if (n == 0) {   // s2i (nnCntrlClass.c:173-200)
-                st.cnt_s2i = (uint16_t)((st.cnt_s2i + 1) % a.timeout_s2i);
-                if (det || st.cnt_s2i == a.timeout_s2i - 1) {
-                    np = (st.pos + 1) % a.len_seq;
-                    move = true;
-                    if (det || n != a.seq[np]) {
-                        st.cnt_s2i = 0;
-                        rst = true;
-                    }
-                }
-            } else if (n == 2) {   // kws (nnCntrlClass.c:203-236)
-                st.cnt_kws = (uint16_t)((st.cnt_kws + 1) % a.timeout_kws);
-                if (det || st.cnt_kws == a.timeout_kws - 1) {
-                    np = det ? (st.pos + 1) % a.len_seq : (st.pos - 1) % a.len_seq;
-                    if (np < 0) np += a.len_seq;
-                    move = true;
-                    if (det || n != a.seq[np]) {
-                        st.cnt_kws = 0;
-                        rst = true;
-                    }
-                }
-            } else if (det) {   // vad (nnCntrlClass.c:238-262)
-                np = (st.pos + 1) % a.len_seq;
-                move = rst = true;
-            }
-            if (move) st.pos = (int16_t)np;   // no reset: same net, same state, keep going
+            const bool rst = nnsp::casc_step(a, st, n, det);
             if (rst) {
                 cut = t;
                 break;
@@ -157,12 +100,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
             int4* cs = reinterpret_cast<int4*>(a.c[n] + (size_t)s * NN_MAX_W);
             for (int k = 0; k < NN_MAX_W / 8; ++k) hs[k] = z;
             for (int k = 0; k < NN_MAX_W / 4; ++k) cs[k] = z;
-            NnPost* ps = reinterpret_cast<NnPost*>(a.post[n]) + s;
-            ps->slides = 1;
-            ps->trigger = 0;
-            ps->argmax_last = 0;
-            for (int k = 0; k < 7; ++k) ps->counts[k] = 0;
-            ps->outputs[0] = ps->outputs[1] = ps->outputs[2] = 0;
+            nnsp::post_reset(*(reinterpret_cast<NnPost*>(a.post[n]) + s));
             b_next = cut + 1;
         }
         a.st[s] = st;
@@ -174,8 +112,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
     }
     list_next(a, n_next, s, want, fr_next);
     if (a.last_round && __ballot(want) && (threadIdx.x & 63) == 0) atomicMax(a.last_round, a.round + 1);
-    add_frames(a, n_next,
-               want ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, T - b_next) : T - b_next) : 0ull);
+    add_frames(a, n_next, nnsp::next_frames(a, T, want, b_next));
 }
 
 // nnCntrlClass_reset's controller part + PcmBufClass_reset (nnCntrlClass.c:132-150,

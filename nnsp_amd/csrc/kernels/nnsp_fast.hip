@@ -21,9 +21,11 @@
 // shapes, plus a generic instantiation that reads the shape at run time.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "nnsp_dev.h"
 #include "nnsp_kabi.h"
+#include "nnsp_casc.h"
 #include "nnsp_nn.h"
 
 using namespace nnsp;
@@ -675,15 +677,27 @@ struct alignas(16) PipeTile {
     int32_t nst[16];          // NN steps of each stream's segment
     int32_t beg[16];          // segment start frame
     int32_t end[16];          // segment end frame (exclusive)
+    int32_t cut[16];          // fused control: frame that reset the net (-1: none)
 };
 
+//
+// Fused control (cascade, ca.st non-NULL): the stage-3 wave also runs the
+// controller (nnCntrlClass_exec) frame by frame as the triggers come out.  At
+// the frame that resets the net the stream's segment ends: later frames are
+// neither post-processed nor written, the epilogue stores the reset state
+// (NNSPClass_reset) instead of the carried one, and the stream is listed for
+// its next net -- what casc_control_kernel does after the kernel otherwise.
 template <class SH, bool ACC32>
-__global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRun r) {
+__global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRun r, CascArgs ca) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CF = PipeCfg<SH>;
     using PT = PipeTile<SH>;
     constexpr int RGP = CF::LW, RPW = CF::RPW, RS = PT::RS;
     constexpr int N = SH::NW, nrt = SH::NRT, nkt_r = SH::NKR;
+    const bool ctl = ca.st != nullptr;
+    // the round after next appends to counts_clear: zero it (every net's recur
+    // does; nothing reads or appends to it during this round)
+    if (ctl && blockIdx.x == 0 && threadIdx.x < 6) ca.counts_clear[threadIdx.x] = 0;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
     const int i0 = blockIdx.x * 16;   // tile = 16 consecutive entries of the stream list
     if (i0 >= nrow) return;
@@ -713,7 +727,10 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     const int T = r.T;
     const bool post_w = g == RGP + 2;
     PostState ps = {};
+    CascState cst = {};   // fused control: the stream's controller state
+    int cut = -1;
     if (post_w && lane < 16) {
+        if (ctl && valid) cst = ca.st[s];
         const int b = valid && r.seg_begin ? r.seg_begin[s] : 0;
         const int e = r.seg_len > 0 ? min(T, b + r.seg_len) : T;
         if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
@@ -730,7 +747,10 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     int nsteps = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
-    if (post_w && lane < 16 && valid && phase == 1 && b < e) put_frame(r, s, T, b, ps);   // frame b: no NN, trigger carried
+    if (post_w && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
+        put_frame(r, s, T, b, ps);
+        if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
+    }
     const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
     const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
     v4i gxv[RPW];
@@ -845,7 +865,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                     &R.a3[cur][0][0], RS, tt, lane);
-        } else if (j >= 3 && j - 3 < nsteps) {   // stage 3: step j-3
+        } else if (post_w && j >= 3 && j - 3 < nsteps) {   // stage 3: step j-3
             const int jj = j - 3;
             const int t = b + 2 * jj + phase;
             const bool active = valid && t < e;
@@ -859,34 +879,50 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 int32_t* dst = r.logits + ((size_t)s * T + t) * SH::NOUT;
                 for (int o = q; o < SH::NOUT; o += 4) dst[o] = f32[o];
             }
-            if (lane < 16 && active) {
+            if (lane < 16 && active && cut < 0) {
                 RegLogits<SH::NOUT> lg;
 #pragma unroll
                 for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
                 post_proc(ps, img, lg);
                 put_frame(r, s, T, t, ps);
-                if (t + 1 < e) put_frame(r, s, T, t + 1, ps);
+                if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) {
+                    cut = t;
+                } else if (t + 1 < e) {
+                    put_frame(r, s, T, t + 1, ps);
+                    if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = t + 1;
+                }
             }
         }
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
         __syncthreads();
     }
-    // ---- state out: LSTM step nsteps-1 wrote h[nsteps & 1]
+    if (ctl) {
+        if (post_w && lane < 16) R.cut[lane] = valid ? cut : -1;
+        __syncthreads();
+    }
+    // ---- state out: LSTM step nsteps-1 wrote h[nsteps & 1]; a stream whose
+    //      net was reset gets the zero state (NeuralNetClass_setDefault)
     const int hb = nsteps & 1;
     for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
         const int st = idx / N, u = idx - st * N;
         if (i0 + st < nrow) {
             const int gs = sid(i0 + st);
-            r.h[(size_t)gs * NN_MAX_W + u] = R.h[hb][st][u];
-            r.c[(size_t)gs * NN_MAX_W + u] = R.c[st][u];
+            const bool rs = ctl && R.cut[st] >= 0;
+            r.h[(size_t)gs * NN_MAX_W + u] = rs ? (int16_t)0 : R.h[hb][st][u];
+            r.c[(size_t)gs * NN_MAX_W + u] = rs ? 0 : R.c[st][u];
         }
     }
     if (post_w && lane < 16 && valid && b < e) {
-        ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
+        if (cut >= 0)
+            nnsp::post_reset(ps);
+        else
+            ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
     // ---- feature context (normFeatContext slots 1..5) := last 5 of prev5 ++ feats[b..e):
-    // all of the tile's reads before any write (a stream's old slots feed its new ones)
+    // all of the tile's reads before any write (a stream's old slots feed its new ones).
+    // A reset net (FeatureClass_setDefault): slots 1..4 := the default, slot 5
+    // keeps the feature of the frame that reset it (T4).
     int4 cv[2];
     int ci[2];
 #pragma unroll
@@ -898,8 +934,13 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
             const int L = R.end[st] - R.beg[st];
             if (L > 0) {
                 const int gs = sid(i0 + st), jx = L + m;
-                cv[k] = jx < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + jx) * 40 + 8 * part)
-                               : feat8(r.fs, r.feats, gs, T, R.beg[st], R.beg[st] + jx - 5, part);
+                const int ct = ctl ? R.cut[st] : -1;
+                if (ct >= 0)
+                    cv[k] = m < 4 ? reinterpret_cast<const int4*>(ca.prev_default[r.net_id])[part]
+                                  : feat8(r.fs, r.feats, gs, T, R.beg[st], ct, part);
+                else
+                    cv[k] = jx < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + jx) * 40 + 8 * part)
+                                   : feat8(r.fs, r.feats, gs, T, R.beg[st], R.beg[st] + jx - 5, part);
                 ci[k] = gs * 25 + c;
             }
         }
@@ -908,6 +949,27 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
 #pragma unroll
     for (int k = 0; k < 2; ++k)
         if (ci[k] >= 0) reinterpret_cast<int4*>(r.prev5)[ci[k]] = cv[k];
+    if (ctl && post_w) {
+        // ---- controller bookkeeping (casc_control_kernel's tail): frames since
+        //      the reset of the net the stream runs next (its feat8 reads above
+        //      are done), position, next segment start, next round's lists
+        bool want = false;
+        int n_next = 0, b_next = T, fr_next = 2;
+        if (lane < 16 && valid) {
+            fr_next = cut >= 0 ? 0 : min(2, (int)ca.fresh[s] + (e - b));
+            b_next = cut >= 0 ? cut + 1 : e;
+            ca.fresh[s] = (int8_t)fr_next;
+            ca.st[s] = cst;
+            ca.seg_begin[s] = b_next;
+            if (b_next < T) {
+                want = true;
+                n_next = ca.seq[cst.pos];
+            }
+        }
+        nnsp::list_next(ca, n_next, s, want, fr_next);
+        if (ca.last_round && __ballot(want) && lane == 0) atomicMax(ca.last_round, ca.round + 1);
+        nnsp::add_frames(ca, n_next, nnsp::next_frames(ca, T, want, b_next));
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -963,8 +1025,9 @@ const void* pick_recur(int shape, int nrt, bool acc32) {
     return recur_fn<ShapeGen, 8>(acc32);
 }
 
-int launch(const void* fn, dim3 grid, dim3 blk, size_t lds, void* stream, const NnImage* img, const FastRun* r) {
-    void* args[2] = {(void*)img, (void*)r};
+int launch(const void* fn, dim3 grid, dim3 blk, size_t lds, void* stream, const NnImage* img, const FastRun* r,
+           const CascArgs* ca = nullptr) {
+    void* args[3] = {(void*)img, (void*)r, (void*)ca};
     hipError_t e = hipLaunchKernel(fn, grid, blk, args, lds, (hipStream_t)stream);
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -991,14 +1054,18 @@ int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, int wave
     return launch(pick_proj(r->shape, img->acc32 || r->ep32), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
 }
 
-int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, void* stream) {
+int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const CascArgs_* ctl, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n, r->shape);
     const int nrow = r->n_list_dev ? r->S : (r->list ? r->n_list : r->S);
     if (nrow <= 0) return 0;
     int waves = 0;
     size_t tb = 0;
-    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb))
-        return launch(fn, dim3((nrow + 15) / 16), dim3(64 * waves), lds, stream, img, r);
+    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb)) {
+        CascArgs none;
+        memset(&none, 0, sizeof none);
+        return launch(fn, dim3((nrow + 15) / 16), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
+    }
+    if (ctl) return (int)hipErrorInvalidValue;   // fused control needs the pipelined kernel
     const int tiles = (nrow + 15) / 16;
     const int blocks = (tiles + tpw - 1) / tpw;
     return launch(pick_recur(r->shape, img->L[r->li].nrt, img->acc32 || r->ep32), dim3(blocks), dim3(64 * RW * tpw), lds,

@@ -194,7 +194,10 @@ int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, cons
                             int n, void *stream);
 size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape);
 int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, int waves, void *stream);
-int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, void *stream);
+/* ctl non-NULL: the cascade controller runs fused into the pipelined recur
+ * kernel (compiled shapes only); CascArgs is declared below */
+struct CascArgs_;
+int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, const struct CascArgs_ *ctl, void *stream);
 int nnspk_set_lds_limit(void);
 int nnspk_malloc(void **p, size_t n);
 int nnspk_free(void *p);
@@ -225,7 +228,7 @@ typedef struct {
     int16_t pad;
 } CascState;
 
-typedef struct {
+typedef struct CascArgs_ {
     int32_t S, T, len_seq, timeout_kws, timeout_s2i;
     int32_t seg_len;          /* frames per round and stream (0: to the chunk end) */
     int16_t seq[8];           /* net id per sequence position (0 s2i, 1 vad, 2 kws) */

@@ -86,8 +86,22 @@ def test_cascade_matches_oracle(th, acc32, window):
     assert r >= 1 and frames >= S * chunks[-1]
 
 
-def test_cascade_short_lookback_timeouts_and_order():
+@pytest.mark.parametrize("th", ["lively", "slow"])
+def test_cascade_control_kernel(th, monkeypatch):
+    # the controller as its own kernel per round (casc_control_kernel) instead
+    # of fused into the nets' recur kernels: same results
+    monkeypatch.setenv("NNSP_CASCADE_CONTROL_KERNEL", "1")
+    S, chunks = 150, [100, 37, 1, 63]
+    oc, gc, _ = _build(TH[th], S, max(chunks), False, (1, 2, 0), 80, 60, 80, 50)
+    gc.set_window(12)
+    assert _check(oc, gc, _pcm(S, sum(chunks), 12), chunks) > 50
+
+
+@pytest.mark.parametrize("ctl", ["fused", "kernel"])
+def test_cascade_short_lookback_timeouts_and_order(ctl, monkeypatch):
     # odd look-backs, tiny timeouts (counter wrap), a different sequence order
+    if ctl == "kernel":
+        monkeypatch.setenv("NNSP_CASCADE_CONTROL_KERNEL", "1")
     S, chunks = 70, [30, 30, 17, 50]
     oc, gc, _ = _build(TH["slow"], S, 50, False, (1, 0, 2), 17, 7, 3, 5)
     gc.set_window(5)
