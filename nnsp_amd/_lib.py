@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libnnsp_mi355x.so")
+# NNSP_LIB: another in-tree build of the same library (development A/B runs)
+LIB_PATH = os.environ.get("NNSP_LIB") or os.path.join(HERE, "libnnsp_mi355x.so")
 
 _lib = None
 

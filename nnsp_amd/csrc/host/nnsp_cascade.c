@@ -309,7 +309,6 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     fa.mode = FE_MODE_COLD;
     fa.list = c->d_cold_list[r & 1][n];
     fa.n_list_dev = cnt + 3 + n;
-    fa.n_list_rec = NULL;
     return nnspk_launch_fe(&fa, stream);
 }
 
@@ -414,6 +413,10 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
         fa.ring = c->ring;
         fa.abs0 = c->abs0;
         fa.lmel = c->d_lmel;
+        if (T >= c->H) { /* the next chunk's look-back history, stored by the front end */
+            fa.hist_out = c->d_hist[c->hist_cur ^ 1];
+            fa.hist_frames = c->H;
+        }
         TRY(nnspk_event_record(c->ev_fe[0], c->stream));
         TRY(nnspk_launch_fe(&fa, c->stream));
         TRY(nnspk_event_record(c->ev_fe[1], c->stream));
@@ -441,7 +444,8 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     c->launched = r;
     /* voice buffer: keep the last H frames for the next chunk's look-back;
      * the shared front end's STFT buffer keeps the last 2 frames */
-    TRY(nnspk_launch_hist_roll(c->d_hist[c->hist_cur ^ 1], hist, pcm, c->S, T, c->H, c->stream));
+    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
+        TRY(nnspk_launch_hist_roll(c->d_hist[c->hist_cur ^ 1], hist, pcm, c->S, T, c->H, c->stream));
     c->hist_cur ^= 1;
     TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     c->abs0 = (c->abs0 + T) % c->ring;

@@ -23,6 +23,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <type_traits>
+
 #include "nnsp_dev.h"
 #include "nnsp_kabi.h"
 #include "nnsp_casc.h"
@@ -89,6 +91,18 @@ __device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, 
 
 __host__ __device__ inline size_t ep_bytes(int n) { return ((size_t)n * sizeof(EpRow) + 15) & ~(size_t)15; }
 
+// epilogue constant as the kernel consumes it: the int32 accumulator kernels
+// wrap-add only its low word (ep_out<true>), so they load 4 bytes of it
+template <bool ACC32>
+using CstT = typename std::conditional<ACC32, int32_t, int64_t>::type;
+template <bool ACC32>
+__device__ __forceinline__ CstT<ACC32> ep_cst(const EpRow& e) {
+    if constexpr (ACC32)
+        return reinterpret_cast<const int32_t*>(&e.cst)[0];
+    else
+        return e.cst;
+}
+
 // shift_64b + clamp (acc64) or shift_32b (acc32) of acc + cst.  rsh/lsh = the
 // layer's output shift split by sign (lsh > 0 never happens for the reference nets).
 template <bool ACC32>
@@ -152,7 +166,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 #pragma unroll
         for (int r0 = 0; r0 < NRT; r0 += CH) {
             v4i w[CH][NKT];
-            int64_t cst[CH][4];
+            CstT<ACC32> cst[CH][4];
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 const int rt = r0 + c;
@@ -163,7 +177,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int row = 16 * rt + 4 * q + i;
-                        cst[c][i] = row < rows ? ep[row].cst : 0;
+                        cst[c][i] = row < rows ? ep_cst<ACC32>(ep[row]) : 0;
                     }
                 }
             }
@@ -237,10 +251,6 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
     using PW = ProjWave<SH>;
     PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
-    stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
-    stage_ep(ep, img, r.ep_lo, r.ep_n, false);
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
-    __syncthreads();
     constexpr bool GEN = SH::generic;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PW& P = pw[wv];
@@ -261,6 +271,13 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
     if (r.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *r.n_list_rec = nrow;
     const long long ngrp = (nrow + G - 1) / G;
     const long long ntiles = ngrp * ntps;
+    // device-sized lists (cascade rounds): workgroups with no tile exit
+    // before staging anything
+    if ((long long)blockIdx.x * (blockDim.x >> 6) >= ntiles) return;
+    stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
+    stage_ep(ep, img, r.ep_lo, r.ep_n, false);
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    __syncthreads();
     // stream k of a tile: list entry, segment start b, length L, NN phase
     struct Seg { int s, b, L, ph; bool ok; };
     auto seg_of = [&](long long grp, int k) {
@@ -404,6 +421,12 @@ template <int N>
 struct RegLogits {
     int32_t v[N];
     __device__ __forceinline__ int32_t operator[](int i) const { return v[i]; }
+};
+
+// logits of one stream read from its LDS row on use
+struct LdsLogits {
+    const int32_t* p;
+    __device__ __forceinline__ int32_t operator[](int i) const { return p[i]; }
 };
 
 template <class SH, int RPW, bool ACC32>   // RPW: LSTM row tiles per wave = ceil(nrt / RG)
@@ -786,7 +809,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 // cell state, the previous h kept for inactive streams) before
                 // the first store: loads cannot be moved across LDS stores
                 v4i w[RPW][nkt_r];
-                int64_t cst[RPW][4];
+                CstT<ACC32> cst[RPW][4];
                 int32_t c_old[RPW];
                 int16_t h_old[RPW];
 #pragma unroll
@@ -798,7 +821,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                         for (int kt = 0; kt < nkt_r; ++kt)
                             w[k][kt] = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * nkt_r + kt) * 1024 + 16 * lane);
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) cst[k][i] = epl[16 * rt + i].cst;
+                        for (int i = 0; i < 4; ++i) cst[k][i] = ep_cst<ACC32>(epl[16 * rt + i]);
                         c_old[k] = u < N ? R.c[sc][u] : 0;
                         h_old[k] = u < N ? R.h[cur][sc][u] : (int16_t)0;
                     }
@@ -880,10 +903,9 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 for (int o = q; o < SH::NOUT; o += 4) dst[o] = f32[o];
             }
             if (lane < 16 && active && cut < 0) {
-                RegLogits<SH::NOUT> lg;
-#pragma unroll
-                for (int o = 0; o < SH::NOUT; ++o) lg.v[o] = f32[o];
-                post_proc(ps, img, lg);
+                // logits read from LDS where the post-processing uses them
+                // (s2i: 7, and 2 x 17 only on a detection) -- no register copy
+                post_proc(ps, img, LdsLogits{f32});
                 put_frame(r, s, T, t, ps);
                 if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) {
                     cut = t;

@@ -54,7 +54,11 @@ typedef struct {
     int32_t *lmel;
     const int8_t *fresh;
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device */
-    int32_t *n_list_rec;      /* seg_norm: non-NULL, block 0 records *n_list_dev there */
+    /* FE_MODE_SHARED, non-NULL: the PCM of the chunk's last hist_frames frames
+     * (T >= hist_frames) is also stored to hist_out [S][hist_frames][160] --
+     * the look-back history of the next chunk, written while the samples are
+     * in registers anyway (replaces a separate history roll) */
+    int16_t *hist_out;
 } FeArgs;
 
 /* Cascade: where a net's segment features come from -- the shared log-Mel

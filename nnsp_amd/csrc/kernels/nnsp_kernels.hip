@@ -177,7 +177,8 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.  Each wave
 // runs a contiguous range of frames (consecutive frames of a stream re-read
 // two thirds of their window from L1/L2) and prefetches the next frame's PCM.
-__global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
+// (256, 5): at most 96 VGPRs, five waves per SIMD
+__global__ __launch_bounds__(256, 5) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
     __shared__ int64_t Ms[4][64];
@@ -264,6 +265,13 @@ __global__ __launch_bounds__(256) void fe_kernel(FeArgs a) {
         }
         if (cur.t >= cur.lim) continue;   // wave-uniform
         const int s = cur.s, t = cur.t;
+        if (a.hist_out && t >= a.T - a.hist_frames) {
+            // frame t's own 160 samples: raw[2] of lanes 32..63 (samples 0..63),
+            // raw[3] of lanes 0..47 (64..159)
+            int16_t* h = a.hist_out + ((size_t)s * a.hist_frames + (t - (a.T - a.hist_frames))) * 160;
+            if (lane >= 32) *reinterpret_cast<uint32_t*>(h + 2 * lane - 64) = raw[2];
+            if (lane < 48) *reinterpret_cast<uint32_t*>(h + 64 + 2 * lane) = raw[3];
+        }
         const unsigned fo = (unsigned)s * (unsigned)a.T + (unsigned)t;   // output frame index
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30;
         // complex c = (x[2c], x[2c+1]), c = 64*m + lane
@@ -858,7 +866,9 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     const long long nfr = (long long)nrow * W;
     long long blocks = (nfr + 3) / 4;
     if (blocks > 256 * 16) blocks = 256 * 16;
-    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 512) blocks = 512;   // at most 2 frames per switch
+    // cold frames (<= 2 per reset, device-sized list): enough workgroups for
+    // about one frame per wave -- their latency sits on each round's critical path
+    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
     hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
     return ok(hipGetLastError());
 }

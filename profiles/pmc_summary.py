@@ -20,8 +20,8 @@ def kname(full: str, grid: int = 0) -> str:
     base = base.split("<")[0]
     # the cascade launches fe_kernel twice over: once per chunk on every frame
     # (FE_MODE_SHARED, the full 4096-workgroup grid) and per round on the few
-    # frames after net resets (FE_MODE_COLD, <= 512 workgroups)
-    if base == "fe_kernel" and 0 < grid < 1024 * 256:
+    # frames after net resets (FE_MODE_COLD, <= 2048 workgroups)
+    if base == "fe_kernel" and 0 < grid < 4096 * 256:
         return "fe_kernel[cold]"
     return base
 

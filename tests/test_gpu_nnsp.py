@@ -63,6 +63,15 @@ def test_batch_matches_oracle(name, acc32, path, monkeypatch):
 
 
 @pytest.mark.parametrize("name", NETS)
+def test_acc64_int64_kernels(name, monkeypatch):
+    # acc64 nets run the int32-accumulator kernels when the host bound proves
+    # no overflow (ep32; true for these shapes); NNSP_NO_EP32 forces the
+    # int64-epilogue instantiations of proj / recur, which must agree too
+    monkeypatch.setenv("NNSP_NO_EP32", "1")
+    _compare(name, False, S=37, chunks=[24, 7, 1, 10])
+
+
+@pytest.mark.parametrize("name", NETS)
 def test_many_streams_one_long_chunk(name):
     _compare(name, False, S=600, chunks=[61, 3])
 
