@@ -64,7 +64,7 @@ int nnsp_cascade_sync(nnsp_cascade *c);
 
 /* Scheduling knob (results do not depend on it): each round runs every
  * listed stream for at most this many frames (0: to the chunk end).  Smaller
- * windows waste less work past a net switch but take more rounds.  Default 12
+ * windows waste less work past a net switch but take more rounds.  Default 16
  * (environment NNSP_CASCADE_WINDOW overrides it at create time). */
 int nnsp_cascade_set_window(nnsp_cascade *c, int frames);
 void *nnsp_cascade_stream(nnsp_cascade *c);

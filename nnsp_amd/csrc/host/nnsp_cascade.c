@@ -10,17 +10,17 @@
  *      shared value of the frame it reads (the current one for VAD, the one
  *      frs_vbufBk frames back for KWS / S2I);
  *   2. casc_begin lists every stream under the net at its position;
- *   3. rounds of { for each net with listed streams: its features for the
- *      segment (seg_norm normalises the shared log-Mel with the net's
- *      mean / stdR; the 0-2 frames right after the net's reset, whose STFT
- *      buffer still holds zeros, run the full front end in FE_MODE_COLD), then
- *      the NN half (proj -> recur -> context roll); casc_control replays the
- *      controller over the round's triggers, cuts each stream's segment at its
- *      first net switch, requests the departing net's reset and lists the
- *      stream for the next round; the resets run } until no stream is listed;
- *   4. the PCM history (what the look-back and the cold frames read) and the
- *      shared front end's PCM tail roll forward.
- * The host reads back three list lengths per round and nothing else.
+ *   3. rounds of { for each net with listed streams, on its own HIP stream:
+ *      the full front end of the 0-2 frames right after the net's reset,
+ *      whose STFT buffer still holds zeros (FE_MODE_COLD; every other frame's
+ *      features are the shared log-Mel normalised on the fly by the kernels
+ *      that read them), then the NN half (proj -> recur).  recur runs the
+ *      controller as the triggers come out, cuts each stream's segment at its
+ *      first net switch, stores the departing net's reset state and lists the
+ *      stream for the next round } until no stream is listed;
+ *   4. the shared front end's PCM tail rolls forward (the PCM history that
+ *      the look-back and the cold frames read was stored by step 1).
+ * The host reads back three list lengths per batch of rounds and nothing else.
  */
 #include <stdlib.h>
 #include <string.h>
@@ -36,6 +36,7 @@
 
 #define HIST_MAX 99   /* PcmBufClass keeps 100 frames: look-back 0..99 */
 #define MAX_TIMED 32  /* rounds per chunk with per-net device timing */
+#define ZERO_BYTES (3 * 8 + (18 + 1 + MAX_TIMED * 3) * 4)
 
 struct nnsp_cascade {
     nnsp_batch *net[3];
@@ -45,7 +46,7 @@ struct nnsp_cascade {
     CascState *d_st;
     int32_t *d_seg_begin, *d_counts;
     unsigned long long *d_frames;
-    int16_t *d_trig[3], *d_out3[3];
+    int16_t *d_trig[3];             /* per net: triggers for casc_control (control-kernel mode only) */
     uint8_t *d_mask[3];
     /* per round parity and net: the round's stream lists (round r reads
      * [r & 1] while its kernels append the next round's to [(r + 1) & 1]) */
@@ -61,6 +62,7 @@ struct nnsp_cascade {
     int16_t *d_pdef;                /* [3][40] FeatureClass_setDefault context value per net */
     int32_t *d_rcount;              /* [MAX_TIMED][3] list lengths each round ran with */
     int32_t *d_last_round;          /* last round a stream was listed for (+1) */
+    void *d_zero;                   /* frames, counts, last_round, rcount (one allocation) */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
     void *ev[2];
@@ -137,19 +139,20 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
                 if ((e = nnspk_event_create(&c->ev_t[r][n][i]))) goto fail;
     }
     if ((e = nnspk_malloc((void **)&c->d_st, S * sizeof(CascState)))) goto fail;
+    /* the per-chunk counters, one allocation zeroed by one memset per chunk */
+    if ((e = nnspk_malloc((void **)&c->d_zero, ZERO_BYTES))) goto fail;
+    c->d_frames = (unsigned long long *)c->d_zero;                 /* [3] */
+    c->d_counts = (int32_t *)((char *)c->d_zero + 3 * 8);         /* [18] */
+    c->d_last_round = c->d_counts + 18;                             /* [1] */
+    c->d_rcount = c->d_last_round + 1;                              /* [MAX_TIMED][3] */
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
-    if ((e = nnspk_malloc((void **)&c->d_counts, 18 * 4))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_rcount, MAX_TIMED * 3 * 4))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_last_round, 4))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_frames, 3 * 8))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_lmel, S * (size_t)c->ring * 40 * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_fresh, S))) goto fail;
     for (int i = 0; i < 3; ++i) {
         if ((e = nnspk_malloc((void **)&c->d_trig[i], S * T * 2))) goto fail;
-        if ((e = nnspk_malloc((void **)&c->d_out3[i], S * T * 6))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_mask[i], S))) goto fail;
         for (int k = 0; k < 2; ++k) {
             if ((e = nnspk_malloc((void **)&c->d_list[k][i], S * 4))) goto fail;
@@ -176,7 +179,6 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         a->last_round = c->d_last_round;
         for (int i = 0; i < 3; ++i) {
             a->trig[i] = c->d_trig[i];
-            a->out3[i] = c->d_out3[i];
             a->feats[i] = nets[i]->d_feats;
             a->prev5[i] = nets[i]->d_prev5;
             a->h[i] = nets[i]->d_h;
@@ -211,7 +213,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         nnspk_free(tl);
         if (e) goto fail;
     }
-    c->window = 12;
+    c->window = 16; /* profiles/sweep_window.sh on MI355X: 14 ~ 16 > 12 at 32768 streams */
     {
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
         /* the controller runs inside the nets' pipelined recur kernels when all
@@ -236,11 +238,11 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
 {
     if (!c) return;
     if (c->stream) nnspk_sync(c->stream);
-    void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_counts,  c->d_frames,  c->d_trig[0], c->d_trig[1],
-                    c->d_trig[2], c->d_out3[0],   c->d_out3[1], c->d_out3[2], c->d_mask[0], c->d_mask[1],
+    void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_zero,    c->d_trig[0], c->d_trig[1],
+                    c->d_trig[2], c->d_mask[0],   c->d_mask[1],
                     c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1],
                     c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
-                    c->d_ran,     c->d_pdef,      c->d_rcount,  c->d_last_round, c->d_cold_list[0][0],
+                    c->d_ran,     c->d_pdef,      c->d_cold_list[0][0],
                     c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
                     c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2]};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
@@ -396,10 +398,7 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
     TRY(nnspk_event_record(c->ev[0], c->stream));
-    TRY(nnspk_memset(c->d_counts, 0, 18 * 4, c->stream));
-    TRY(nnspk_memset(c->d_frames, 0, 3 * 8, c->stream));
-    TRY(nnspk_memset(c->d_last_round, 0, 4, c->stream));
-    TRY(nnspk_memset(c->d_rcount, 0, MAX_TIMED * 3 * 4, c->stream));
+    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream)); /* counts, frames, last round, rcount */
     {   /* 1. log-Mel of every frame (net-independent) */
         FeArgs fa;
         memset(&fa, 0, sizeof fa);

@@ -239,7 +239,6 @@ typedef struct CascArgs_ {
     CascState *st;            /* [S] */
     int32_t *seg_begin;       /* [S] first frame of this round's segment (T: done) */
     const int16_t *trig[3];   /* per net id: [S][T] triggers of the round's segments */
-    const int16_t *out3[3];   /* per net id: [S][T][3] NNSPClass.outputs after each frame */
     const int16_t *feats[3];  /* per net id: [S][T][40] */
     int16_t *prev5[3];        /* per net id: [S][5][40] */
     int16_t *h[3];            /* per net id: [S][NN_MAX_W] LSTM state (one LSTM layer) */
