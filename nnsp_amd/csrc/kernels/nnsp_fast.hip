@@ -667,24 +667,34 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
 
 // ---------------------------------------------------------------------------
 // recur_pipe_kernel (the compiled shapes): one 16-stream tile per workgroup of
-// RG LSTM waves and 3 tail waves, a 4-stage pipeline across NN steps:
+// LW LSTM waves and 4 tail waves, a 5-stage pipeline across NN steps (S2I: 3
+// tail waves, stages 3 and 4 on one):
 //   LSTM waves  iteration j: step j   -- Wh.h + gx, gate epilogue, cell and
 //                                        hidden update (lstm.c:48-124)
 //   tail wave 1 iteration j: step j-1 -- FC relu6  (h  -> a2)
 //   tail wave 2 iteration j: step j-2 -- FC relu6  (a2 -> a3)
-//   tail wave 3 iteration j: step j-3 -- FC linear (a3 -> logits), outputs,
-//                                        post-processing, trigger stores
-// Only the LSTM stage is recurrent; the FC stages hang off it one step apart,
-// so a step costs the slowest stage instead of their sum.  One workgroup
-// barrier per iteration; h, a2 and a3 are double-buffered by iteration
-// parity (stage k reads what stage k-1 wrote one iteration earlier, and that
-// buffer is rewritten only after the next barrier).
+//   tail wave 3 iteration j: step j-3 -- FC linear (a3 -> logits a4)
+//   tail wave 4 iteration j: step j-4 -- outputs, post-processing, trigger
+//                                        stores (and the fused controller)
+// Only the LSTM stage is recurrent; the other stages hang off it one step
+// apart, so a step costs the slowest stage instead of their sum (the
+// post-processing alone, 16 lanes of mostly serial work, was as long as an FC
+// layer -- profiles/recur_clocks.py).  One workgroup barrier per iteration;
+// h, a2, a3 and a4 are double-buffered by iteration parity (stage k reads
+// what stage k-1 wrote one iteration earlier, and that buffer is rewritten
+// only after the next barrier).
 // ---------------------------------------------------------------------------
 template <class SH>
 struct PipeCfg {
     static constexpr int LW = SH::NRT <= 8 ? 4 : (SH::NRT + 1) / 2;   // LSTM waves: <= 2 row tiles each
     static constexpr int RPW = (SH::NRT + LW - 1) / LW;      // LSTM row tiles per wave
-    static constexpr int NWV = LW + 3;                       // waves per workgroup
+    // the last FC layer and the post-processing on waves of their own (a
+    // 5-stage pipeline) for the 2-output nets; S2I keeps them on one wave: a
+    // 13th wave would cap the kernel at 128 VGPRs, and the spills cost more
+    // than the split gains (profiles/recur_clocks.py)
+    static constexpr int SPLIT = SH::NOUT <= 2 ? 1 : 0;
+    static constexpr int NWV = LW + 3 + SPLIT;               // waves per workgroup
+    static_assert(NWV <= 12, "recur_pipe_kernel: at most 3 waves per SIMD");
 };
 
 template <class SH>
@@ -694,7 +704,7 @@ struct alignas(16) PipeTile {
     int16_t h[2][16][RS];
     int16_t a2[2][16][RS];
     int16_t a3[2][16][RS];
-    int16_t a4[16][RS];       // stage 3: int32 logits
+    int16_t a4[2][16][RS];    // stage 3 -> 4: int32 logits
     int32_t c[16][CW];
     int32_t phase[16];
     int32_t nst[16];          // NN steps of each stream's segment
@@ -748,7 +758,8 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
         R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
     }
     const int T = r.T;
-    const bool post_w = g == RGP + 2;
+    constexpr int SPL = CF::SPLIT;
+    const bool post_w = g == RGP + 2 + SPL;   // the post-processing wave
     PostState ps = {};
     CascState cst = {};   // fused control: the stream's controller state
     int cut = -1;
@@ -795,8 +806,12 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     long long* clk = (r.dbg_clk && blockIdx.x == 0 && lane == 0 && (g == 0 || g >= RGP))
                          ? r.dbg_clk + 2 * (g == 0 ? 0 : g - RGP + 1)
                          : nullptr;
-    for (int j = 0; j < nsteps + 3; ++j) {
-        const int cur = j & 1;
+    // one pipeline iteration; the buffer parity is a template constant (the
+    // loop runs two iterations per trip), so every LDS access of the stages
+    // has a constant offset -- indexing the double buffers with a run-time
+    // parity cost the S2I post wave ~1100 of its ~6000 cycles per step
+    auto iteration = [&](const int j, auto CUR) {
+        constexpr int cur = decltype(CUR)::value;
         if (clk && j < 64) clk[j * 16] = (long long)__builtin_amdgcn_s_memtime();
         if (g < RGP) {
             if (j < nsteps) {
@@ -888,16 +903,23 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                     &R.a3[cur][0][0], RS, tt, lane);
-        } else if (post_w && j >= 3 && j - 3 < nsteps) {   // stage 3: step j-3
-            const int jj = j - 3;
+        } else if (SPL && g == RGP + 2) {   // stage 3 (split): step j-3
+            if (j >= 3 && j - 3 < nsteps)
+                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
+                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
+                    &R.a4[cur][0][0], RS, tt, lane);
+        } else if (post_w && j >= 3 + SPL && j - 3 - SPL < nsteps) {   // post: step j-3-SPL
+            const int jj = j - 3 - SPL;
             const int t = b + 2 * jj + phase;
             const bool active = valid && t < e;
-            fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
-                L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS, &R.a4[0][0], RS,
-                tt, lane);
-            wave_lds_sync();
+            if (!SPL) {   // the last FC layer on this wave too
+                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
+                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
+                    &R.a4[cur][0][0], RS, tt, lane);
+                wave_lds_sync();
+            }
             // outputs and post-processing (nn_speech.c:92-124)
-            const int32_t* f32 = reinterpret_cast<const int32_t*>(&R.a4[sc][0]);
+            const int32_t* f32 = reinterpret_cast<const int32_t*>(&R.a4[SPL ? cur ^ 1 : cur][sc][0]);
             if (active && r.logits) {
                 int32_t* dst = r.logits + ((size_t)s * T + t) * SH::NOUT;
                 for (int o = q; o < SH::NOUT; o += 4) dst[o] = f32[o];
@@ -905,7 +927,10 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
             if (lane < 16 && active && cut < 0) {
                 // logits read from LDS where the post-processing uses them
                 // (s2i: 7, and 2 x 17 only on a detection) -- no register copy
-                post_proc(ps, img, LdsLogits{f32});
+                if (SH::NOUT >= 41 && img.nn_id == 0)
+                    post_proc_s2i_lds(ps, img, f32);
+                else
+                    post_proc(ps, img, LdsLogits{f32});
                 put_frame(r, s, T, t, ps);
                 if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) {
                     cut = t;
@@ -917,6 +942,10 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
         }
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
         __syncthreads();
+    };
+    for (int j = 0; j < nsteps + 3 + SPL; j += 2) {
+        iteration(j, std::integral_constant<int, 0>{});
+        if (j + 1 < nsteps + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
     }
     if (ctl) {
         if (post_w && lane < 16) R.cut[lane] = valid ? cut : -1;

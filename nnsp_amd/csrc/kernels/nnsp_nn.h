@@ -105,6 +105,44 @@ struct LogitRow {
     }
 };
 
+// s2i_post_proc (nn_speech.c:191-227) with its logits in an LDS row (16-byte
+// aligned): the 7 intent logits come in with two 16-byte loads; the two
+// 17-way slot argmaxes read LDS only on a detection.  Same results as
+// post_proc's s2i branch.
+__device__ __forceinline__ void post_proc_s2i_lds(PostState& ps, const NnImage& img, const int32_t* f32) {
+    const int4 a = *reinterpret_cast<const int4*>(f32);
+    const int4 b = *reinterpret_cast<const int4*>(f32 + 4);
+    const int32_t v[7] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z};
+    ps.trigger = 0;
+    ps.outputs[0] = ps.outputs[1] = ps.outputs[2] = 0;
+    int am = 0;
+    int32_t m = v[0];
+#pragma unroll
+    for (int i = 1; i < 7; ++i)
+        if (v[i] >= m) { m = v[i]; am = i; }
+    if (ps.argmax_last == 0 || ps.argmax_last == am) {
+        if (am != 0) {
+            int16_t cam = 0;
+#pragma unroll
+            for (int i = 1; i < 7; ++i)
+                if (i == am) {
+                    ps.counts[i] = (int16_t)(ps.counts[i] + 1);
+                    cam = ps.counts[i];
+                }
+            if (cam > img.th_count) {
+                ps.trigger = 1;
+                ps.outputs[0] = (int16_t)am;
+                ps.outputs[1] = (int16_t)argmax_lw(f32, 17, 7);
+                ps.outputs[2] = (int16_t)argmax_lw(f32, 17, 24);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
+    }
+    ps.argmax_last = (int16_t)am;
+}
+
 template <typename LG>
 __device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, const LG& lg) {
     if (img.nn_id == 0) {  // s2i_post_proc

@@ -31,7 +31,10 @@ _lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clock
 st = clk[:53]
 step = np.diff(st[:, 0])
 print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; iteration cycles median {np.median(step[3:48]):.0f}")
-for k, nm in enumerate(("lstm wave 0", "stage 1 fc", "stage 2 fc", "stage 3 fc+post")):
+names = ("lstm wave 0", "stage 1 fc", "stage 2 fc", "stage 3 fc", "stage 4 post")
+if net == "s2i":   # 4-stage pipeline: the last FC layer and the post-processing on one wave
+    names = ("lstm wave 0", "stage 1 fc", "stage 2 fc", "stage 3 fc+post")
+for k, nm in enumerate(names):
     d = st[3:50, 2 * k + 1] - st[3:50, 2 * k]
     lag = st[3:50, 2 * k] - st[3:50, 0]
     print(f"  {nm:16s} work median {np.median(d):7.0f}  start lag {np.median(lag):6.0f}")
