@@ -193,6 +193,11 @@ def main() -> None:
         step(bufs[W + K - 1])
         eng.sync()
         eng.set_timing(False)
+        rl, rfe, rnn = eng.round_stats()
+        net_ms["rounds"] = {"streams_listed": rl.tolist(),
+                            "cold_fe_ms": [[round(float(x), 4) for x in r] for r in rfe],
+                            "nn_ms": [[round(float(x), 4) for x in r] for r in rnn],
+                            "net_order": ["s2i", "vad", "kws"]}
         for n in ("vad", "kws", "s2i"):
             f, fe, nn, nl = eng.net_stats(n)
             net_ms[n] = {"cold_fe_ms": fe, "nn_ms": nn, "frames": f, "rounds": nl}

@@ -91,6 +91,13 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
  * frame of every stream, one launch). */
 int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms);
 
+/* Last chunk, per round k < max_rounds and net i (NNSP_ID): the number of
+ * streams listed ([3k + i] of lists) and, when timing is on, the device ms of
+ * the net's cold-frame front end and NN kernels in that round (else 0).  Any
+ * output may be NULL.  Returns the number of rounds recorded (at most 32), or
+ * a negative error code. */
+int nnsp_cascade_last_rounds(nnsp_cascade *c, int max_rounds, int32_t *lists, float *fe_ms, float *nn_ms);
+
 /* current_pos_seq of every stream -> host int8 [S]. */
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
 

@@ -115,6 +115,7 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_stream": (P, [P]),
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),
+        "nnsp_cascade_last_rounds": (I, [P, I, P, P, P]),
         "nnsp_cascade_last_fe_stats": (I, [P, C.POINTER(C.c_float)]),
         "nnsp_cascade_last_net_stats": (I, [P, I, C.POINTER(C.c_longlong), C.POINTER(C.c_float),
                                             C.POINTER(C.c_float), C.POINTER(I)]),

@@ -78,6 +78,8 @@ struct nnsp_cascade {
     float sfe_ms;                   /* last chunk: shared front end */
     float fe_ms[3], nn_ms[3];       /* last chunk, per net id: features / proj+recur+roll */
     int runs[3];                    /* last chunk, per net id: segment runs */
+    int rc[MAX_TIMED][3];           /* last chunk: list length of each round and net */
+    float rfe[MAX_TIMED][3], rnn[MAX_TIMED][3]; /* last chunk, timing on: per round and net ms */
 };
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
@@ -456,6 +458,10 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     TRY(nnspk_sync(c->stream));
     c->last_rounds = last + 1;
     TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
+    memcpy(c->rc, rc, sizeof rc);
+    memset(c->rfe, 0, sizeof c->rfe);
+    memset(c->rnn, 0, sizeof c->rnn);
+    for (int k = r; k < MAX_TIMED; ++k) c->rc[k][0] = c->rc[k][1] = c->rc[k][2] = 0;
     for (int n = 0; n < 3; ++n) {
         c->fe_ms[n] = c->nn_ms[n] = 0.f;
         c->runs[n] = 0;
@@ -468,6 +474,8 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
             TRY(nnspk_event_elapsed(&nn, c->ev_t[k][n][1], c->ev_t[k][n][2]));
             c->fe_ms[n] += fe;
             c->nn_ms[n] += nn;
+            c->rfe[k][n] = fe;
+            c->rnn[k][n] = nn;
         }
     }
     return 0;
@@ -552,6 +560,20 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
     if (nn_ms) *nn_ms = c->nn_ms[nn_id];
     if (launches) *launches = c->runs[nn_id];
     return 0;
+}
+
+int nnsp_cascade_last_rounds(nnsp_cascade *c, int max_rounds, int32_t *lists, float *fe_ms, float *nn_ms)
+{
+    if (!c || max_rounds < 0) return NNSP_EINVAL;
+    TRY(nnspk_sync(c->stream));
+    const int n = c->launched < MAX_TIMED ? c->launched : MAX_TIMED;
+    for (int k = 0; k < max_rounds && k < n; ++k)
+        for (int i = 0; i < 3; ++i) {
+            if (lists) lists[3 * k + i] = c->rc[k][i];
+            if (fe_ms) fe_ms[3 * k + i] = c->rfe[k][i];
+            if (nn_ms) nn_ms[3 * k + i] = c->rnn[k][i];
+        }
+    return n;
 }
 
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos)

@@ -290,8 +290,14 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
         g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
         return g;
     };
+    // development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0's first tiles
+    long long* clk = (r.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? r.dbg_clk + 12 : nullptr;
+    int it = 0;
+#define PCLK(k) \
+    if (clk && it < 64) clk[it * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime()
     for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
-         tile += (long long)gridDim.x * (blockDim.x >> 6)) {
+         tile += (long long)gridDim.x * (blockDim.x >> 6), ++it) {
+        PCLK(0);
         const long long grp = tile / ntps;
         const int j0 = 16 * (int)(tile - grp * ntps);
         // lanes 0..G-1 load the tile's stream descriptors; the others read them by shuffle
@@ -323,6 +329,7 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
             *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
         }
         wave_lds_sync();
+        PCLK(1);
         // this lane's row sc: stream kr of the tile, its step j0 + jr
         const int kr = sc / SPT, jr = sc - kr * SPT;
         const Seg me = seg_k(kr);
@@ -335,6 +342,7 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
             fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
                                                           in, in_stride, &P.act[0][0][0], PW::AS, tt, lane);
             wave_lds_sync();
+            PCLK(2);
             in = &P.act[0][0][0];
             in_stride = PW::AS;
         } else {
@@ -382,7 +390,9 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
             }
         }
         wave_lds_sync();
+        PCLK(3);
     }
+#undef PCLK
 }
 
 // ---------------------------------------------------------------------------

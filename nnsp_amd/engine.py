@@ -178,6 +178,16 @@ class NNSPCascade:
         _lib.check(_lib.lib().nnsp_cascade_last_fe_stats(self.h, C.byref(ms)), "fe_stats")
         return ms.value
 
+    def round_stats(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """Last chunk, [round][net id]: streams listed, cold-FE ms, NN ms (ms only with timing on)."""
+        lists = np.zeros((32, 3), np.int32)
+        fe = np.zeros((32, 3), np.float32)
+        nn = np.zeros((32, 3), np.float32)
+        n = _lib.lib().nnsp_cascade_last_rounds(self.h, 32, _lib.ptr(lists), _lib.ptr(fe), _lib.ptr(nn))
+        if n < 0:
+            _lib.check(n, "nnsp_cascade_last_rounds")
+        return lists[:n], fe[:n], nn[:n]
+
     def positions(self) -> np.ndarray:
         pos = np.zeros(self.S, np.int8)
         _lib.check(_lib.lib().nnsp_cascade_positions(self.h, _lib.ptr(pos)), "positions")
