@@ -12,6 +12,7 @@
 //   k_*       : batched single-stage kernels backing the legacy scalar API.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "nnsp_dev.h"
 #include "nnsp_kabi.h"
@@ -39,9 +40,7 @@ __device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (F
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
 
 struct FeLane {
-    uint32_t win[4];      // window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
-    uint32_t mc[6];       // Mel segment coefficients as int16 pairs
-    int mj0, mfirst, mcnt;
+    int mj0, mfirst, mcnt;   // Mel segment start bin; first segment and segment count of bank `lane`
 };
 
 // Block-shared constant tables (LDS).
@@ -49,6 +48,9 @@ struct FeTables {
     int2 tw[3][3][64];    // per stage, twiddle (k, 2k, 3k) of each lane's butterfly: (cos, sin)
     int4 split[256];      // per bin k: (A_re, A_im, B_re, 0) of realCoefA/BQ31 at 16k
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
+    uint4 win[64];        // per lane: window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
+    uint2 mc[3][64];      // per lane: Mel segment coefficients as int16 pairs (LDS, not VGPRs:
+                          // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
 };
 
 __device__ __forceinline__ void fe_tables_init(FeTables& T) {
@@ -61,6 +63,24 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T) {
         T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint32_t w[4], c[6];
+        for (int m = 0; m < 4; ++m) {
+            const int i = 128 * m + 2 * lane;
+            w[m] = i < 480 ? ((uint32_t)(uint16_t)nnsp_tbl_window[i] | ((uint32_t)(uint16_t)nnsp_tbl_window[i + 1] << 16))
+                           : 0u;
+        }
+        const int* sg = nnsp_tbl_melseg + 4 * lane;
+        const int mn = sg[2];
+        for (int i = 0; i < 6; ++i) {
+            const int lo = 2 * i < mn ? nnsp_tbl_mel[sg[3] + 2 * i] : 0;
+            const int hi = 2 * i + 1 < mn ? nnsp_tbl_mel[sg[3] + 2 * i + 1] : 0;
+            c[i] = (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
+        }
+        T.win[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+        for (int j = 0; j < 3; ++j) T.mc[j][lane] = make_uint2(c[2 * j], c[2 * j + 1]);
+    }
 }
 
 __device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int s, int lane) {
@@ -71,19 +91,7 @@ __device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int s, int lane) {
 }
 
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
-    for (int m = 0; m < 4; ++m) {
-        const int i = 128 * m + 2 * lane;
-        L.win[m] = i < 480 ? ((uint32_t)(uint16_t)nnsp_tbl_window[i] | ((uint32_t)(uint16_t)nnsp_tbl_window[i + 1] << 16))
-                           : 0u;
-    }
-    const int* sg = nnsp_tbl_melseg + 4 * lane;
-    L.mj0 = sg[1];
-    const int mn = sg[2];
-    for (int i = 0; i < 6; ++i) {
-        const int lo = 2 * i < mn ? nnsp_tbl_mel[sg[3] + 2 * i] : 0;
-        const int hi = 2 * i + 1 < mn ? nnsp_tbl_mel[sg[3] + 2 * i + 1] : 0;
-        L.mc[i] = (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
-    }
+    L.mj0 = nnsp_tbl_melseg[4 * lane + 1];
     L.mfirst = 0;
     L.mcnt = 0;
     for (int k = 0; k < 64; ++k) {
@@ -177,8 +185,8 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // One frame: window -> rfft -> pspec -> mel -> log10 -> normalise.  Each wave
 // runs a contiguous range of frames (consecutive frames of a stream re-read
 // two thirds of their window from L1/L2) and prefetches the next frame's PCM.
-// (256, 5): at most 96 VGPRs, five waves per SIMD
-__global__ __launch_bounds__(256, 5) void fe_kernel(FeArgs a) {
+// (256, 6): at most 80 VGPRs, six waves per SIMD (window and Mel coefficients in LDS)
+__global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
     __shared__ int64_t Ms[4][64];
@@ -276,10 +284,14 @@ __global__ __launch_bounds__(256, 5) void fe_kernel(FeArgs a) {
         // ---- window (spectrogram_module.c:103-119): x[i] = win[i]*buf[i], Q30;
         // complex c = (x[2c], x[2c+1]), c = 64*m + lane
         int32_t v[8];
+        {
+            const uint4 w4 = TB.win[lane];
+            const uint32_t wn[4] = {w4.x, w4.y, w4.z, w4.w};
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
-            v[2 * m] = (int32_t)(int16_t)(L.win[m] & 0xffff) * (int32_t)(int16_t)(raw[m] & 0xffff);
-            v[2 * m + 1] = (int32_t)(int16_t)(L.win[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
+            for (int m = 0; m < 4; ++m) {
+                v[2 * m] = (int32_t)(int16_t)(wn[m] & 0xffff) * (int32_t)(int16_t)(raw[m] & 0xffff);
+                v[2 * m + 1] = (int32_t)(int16_t)(wn[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
+            }
         }
         wave_cfft256(v, X, TB, lane);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
@@ -312,10 +324,16 @@ __global__ __launch_bounds__(256, 5) void fe_kernel(FeArgs a) {
         {
             int64_t mac = 0;
 #pragma unroll
-            for (int i = 0; i < 6; ++i) {
-                const int2 pv = make_int2(P[L.mj0 + 2 * i], P[L.mj0 + 2 * i + 1]);
-                mac = mad_i64_i32((int32_t)(int16_t)(L.mc[i] & 0xffff), pv.x, mac);
-                mac = mad_i64_i32((int32_t)L.mc[i] >> 16, pv.y, mac);
+            for (int j = 0; j < 3; ++j) {
+                const uint2 c2 = TB.mc[j][lane];
+                const uint32_t cc[2] = {c2.x, c2.y};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int i = 2 * j + h;
+                    const int2 pv = make_int2(P[L.mj0 + 2 * i], P[L.mj0 + 2 * i + 1]);
+                    mac = mad_i64_i32((int32_t)(int16_t)(cc[h] & 0xffff), pv.x, mac);
+                    mac = mad_i64_i32((int32_t)cc[h] >> 16, pv.y, mac);
+                }
             }
             Mp[lane] = mac;
         }
@@ -865,7 +883,14 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (a->mode == FE_MODE_COLD && W > 2) W = 2;
     const long long nfr = (long long)nrow * W;
     long long blocks = (nfr + 3) / 4;
-    if (blocks > 256 * 16) blocks = 256 * 16;
+    // whole multiples of the resident workgroups (256 CUs x 6 at 80 VGPRs):
+    // each wave runs a contiguous frame range, so a partial last wave of
+    // workgroups is pure tail
+    static const long long cap = [] {
+        const char* e = getenv("NNSP_FE_BLOCKS");
+        return e && atoll(e) > 0 ? atoll(e) : 256LL * 6 * 4;
+    }();
+    if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
