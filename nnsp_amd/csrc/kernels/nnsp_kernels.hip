@@ -35,6 +35,7 @@ using namespace nnsp;
 // The stage-4 outputs go to LDS at their natural bin k = rev8(c) (CMSIS's
 // bit reversal), where the split reads bins k and 256-k.  LDS slots are
 // swizzled (zslot) so that every one of these accesses is bank-conflict-free.
+#define FE_MEL_MAXSEG 3   // max lane segments per Mel bank (nnsp_tbl_melseg)
 #define FE_X_DW 512   // dwords of one frame's complex buffer (256 complex)
 __device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (FE_MODE_COLD)
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
@@ -247,16 +248,28 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     };
     // lane's window samples 128*m + 2*lane, +1 of frames t-2, t-1, t
     auto load_frame = [&](const Pos& p, uint32_t (&r)[4]) {
+        const int o = 2 * lane;
+        const int x0 = p.t - 2 - a.lookback;
+        if (!cold && p.t - 2 >= p.b && x0 >= 0) {
+            // common case (wave-uniform): frames t-2..t are consecutive in the
+            // chunk, so the window is 480 contiguous samples from one pointer
+            const int16_t* q = a.pcm + ((size_t)p.s * a.T + x0) * 160 + o;
+            r[0] = *reinterpret_cast<const uint32_t*>(q);
+            r[1] = *reinterpret_cast<const uint32_t*>(q + 128);
+            r[2] = *reinterpret_cast<const uint32_t*>(q + 256);
+            r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(q + 384) : 0u;
+            return;
+        }
         const int16_t* p0 = frame_ptr(p, p.t - 2);
         const int16_t* p1 = frame_ptr(p, p.t - 1);
         const int16_t* p2 = frame_ptr(p, p.t);
-        const int o = 2 * lane;
         r[0] = *reinterpret_cast<const uint32_t*>(p0 + o);
         r[1] = *reinterpret_cast<const uint32_t*>(lane < 16 ? p0 + 128 + o : p1 + o - 32);
         r[2] = *reinterpret_cast<const uint32_t*>(lane < 32 ? p1 + 96 + o : p2 + o - 64);
         r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(p2 + 64 + o) : 0u;
     };
     if (fbeg >= fend) return;
+    const unsigned ring0 = a.mode == FE_MODE_SHARED ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
     Pos nx;
     nx.i = fbeg / W;
     nx.k = fbeg - nx.i * W;
@@ -341,11 +354,18 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         // ---- log10 (fixlog10.c:53-61), normalise (feature_module.c:67-73)
         if (lane < 40) {
             int64_t mac = 0;
-            for (int k = 0; k < L.mcnt; ++k) mac += Mp[L.mfirst + k];
+            // a bank spans at most FE_MEL_MAXSEG lane segments (the table is
+            // generated that way; tests/test_tables.py checks it): unrolled
+#pragma unroll
+            for (int k = 0; k < FE_MEL_MAXSEG; ++k)
+                if (k < L.mcnt) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
             if (a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
             if (a.mode == FE_MODE_SHARED) {
-                a.lmel[((size_t)s * a.ring + (unsigned)(a.abs0 + t) % (unsigned)a.ring) * 40 + lane] = lg;
+                // (abs0 + t) % ring with t < T <= ring: one conditional subtract
+                unsigned slot = ring0 + (unsigned)t;
+                if (slot >= (unsigned)a.ring) slot -= (unsigned)a.ring;
+                a.lmel[((size_t)s * a.ring + slot) * 40 + lane] = lg;
             } else {
                 const int64_t d = (int64_t)lg - mean;
                 a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
