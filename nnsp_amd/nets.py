@@ -6,10 +6,11 @@ an FC over the 6x40 context -> LSTM -> FC -> FC -> FC.  Their shapes and
 fixed-point formats are the ``NeuralNetClass`` initialisers of
 evb/src/def_nn1_vad.c:29-110, def_nn2_kws_galaxy.c:29-111, def_nn0_s2i.c:29-110.
 
-The reference's weight tables are random (reference README.md:67, :111), so
-the benchmark and the GPU-box tests use seeded synthetic weights of exactly
-those shapes and formats, drawn with per-layer spreads that match the shipped
-tables (int8 std 3-30, int16 bias std 2e3-1.2e4).
+Weights: ``ref_net`` loads the reference's own tables (def_nn*.c, dumped as
+data into tests/golden/ref_nets.npz); ``synth_net`` draws seeded synthetic
+weights of exactly those shapes and formats, with per-layer spreads that match
+the shipped tables (int8 std 3-30, int16 bias std 2e3-1.2e4) -- the reference's
+tables are themselves random (reference README.md:67, :111).
 
 Byte layout (``pack_fc`` / ``pack_lstm``): the CMSIS-NN interleaved order the
 shipped ARM path walks (ns-nnsp/src/affine.c:80-149; producer
@@ -18,6 +19,7 @@ tests/test_layout.py when the reference is present).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -38,6 +40,7 @@ class NetSpec:
     acts: list[int]
     # synthetic-weight spreads per layer: (std of W, std of Wrec, bias mean, bias std)
     spread: list[tuple] = field(default_factory=list)
+    nid: int | None = None   # NNSP_ID of a net not named vad/kws/s2i (post-processing kind)
 
     @property
     def nl(self) -> int:
@@ -49,7 +52,7 @@ class NetSpec:
 
     @property
     def nn_id(self) -> int:
-        return NN_ID[self.name]
+        return self.nid if self.nid is not None else NN_ID[self.name]
 
 
 SPECS = {
@@ -127,7 +130,7 @@ def _pack_index(N: int, K: int) -> np.ndarray:
     return np.concatenate(parts)
 
 
-def pack_lstm(w: np.ndarray) -> np.ndarray:
+def pack_lstm(w: np.ndarray, dtype=np.int8) -> np.ndarray:
     """Natural gate-major W[4N][K] (rows: i block, j block, f block, o block;
     python/c_code_table_converter.py:64-73 order) -> per-4-unit-group
     [i rows][j rows][f rows][o rows] interleaved stream (c_weight_man.py:61-92)."""
@@ -137,17 +140,64 @@ def pack_lstm(w: np.ndarray) -> np.ndarray:
     for u0 in range(0, N, 4):
         for k in range(4):
             parts += _pack_block(g[k][u0:u0 + 4])
-    return np.concatenate(parts).astype(np.int8)
+    return np.concatenate(parts).astype(dtype)
 
 
-def pack_lstm_bias(b: np.ndarray) -> np.ndarray:
+def pack_lstm_bias(b: np.ndarray, dtype=np.int16) -> np.ndarray:
     N = b.shape[0] // 4
     g = [b[k * N:(k + 1) * N] for k in range(4)]
     parts = []
     for u0 in range(0, N, 4):
         for k in range(4):
             parts.append(g[k][u0:u0 + 4])
-    return np.concatenate(parts).astype(np.int16)
+    return np.concatenate(parts).astype(dtype)
+
+
+def unpack_lstm(blob: np.ndarray, N: int, K: int) -> np.ndarray:
+    """Inverse of pack_lstm: interleaved stream -> natural gate-major W[4N][K]."""
+    ids = pack_lstm(np.arange(4 * N * K).reshape(4 * N, K).astype(np.int64), dtype=np.int64)
+    out = np.zeros(4 * N * K, dtype=np.int8)
+    out[ids] = np.asarray(blob, dtype=np.int8)[: 4 * N * K]
+    return out.reshape(4 * N, K)
+
+
+def unpack_lstm_bias(blob: np.ndarray, N: int) -> np.ndarray:
+    ids = pack_lstm_bias(np.arange(4 * N), dtype=np.int64)
+    out = np.zeros(4 * N, dtype=np.int16)
+    out[ids] = np.asarray(blob, dtype=np.int16)[: 4 * N]
+    return out
+
+
+# --------------------------------------------------------------------------
+# the reference's portable (ARM_OPTIMIZED=0) byte order, affine.c:291-309:
+# per row block (4 rows, remainder last), per column pair, per row, the pair's
+# two bytes; the odd-column tail one byte per row.  Only the oracle's pinning
+# fixtures use it (tests/golden/make_golden.py feeds the reference's portable
+# build with it); the shipped tables are in the interleaved order above.
+# --------------------------------------------------------------------------
+def _pack_block_portable(m: np.ndarray) -> list[np.ndarray]:
+    R, K = m.shape
+    out = [m[:, 2 * p:2 * p + 2].reshape(-1).copy() for p in range(K // 2)]
+    if K % 2:
+        out.append(m[:, K - 1].copy())
+    return out
+
+
+def pack_fc_portable(w: np.ndarray) -> np.ndarray:
+    parts = []
+    for r0 in range(0, w.shape[0], 4):
+        parts += _pack_block_portable(w[r0:r0 + 4])
+    return np.concatenate(parts).astype(np.int8)
+
+
+def pack_lstm_portable(w: np.ndarray) -> np.ndarray:
+    N = w.shape[0] // 4
+    g = [w[k * N:(k + 1) * N] for k in range(4)]
+    parts = []
+    for u0 in range(0, N, 4):
+        for k in range(4):
+            parts += _pack_block_portable(g[k][u0:u0 + 4])
+    return np.concatenate(parts).astype(np.int8)
 
 
 # --------------------------------------------------------------------------
@@ -176,10 +226,92 @@ class NetData:
                 Bp.append(self.B[i].astype(np.int16))
         return Wp, Wrp, Bp
 
+    def packed_portable(self):
+        """Byte streams in the reference's ARM_OPTIMIZED=0 order (biases as packed())."""
+        Wp, Wrp, Bp = [], [], []
+        for i, t in enumerate(self.spec.types):
+            if t == LSTM:
+                Wp.append(pack_lstm_portable(self.W[i]))
+                Wrp.append(pack_lstm_portable(self.Wr[i]))
+                Bp.append(pack_lstm_bias(self.B[i]))
+            else:
+                Wp.append(pack_fc_portable(self.W[i]))
+                Wrp.append(None)
+                Bp.append(self.B[i].astype(np.int16))
+        return Wp, Wrp, Bp
 
-def synth_net(name: str, seed: int = 1234) -> NetData:
-    spec = SPECS[name]
-    rng = np.random.default_rng([seed, spec.nn_id])
+    @classmethod
+    def from_packed(cls, spec: NetSpec, Wp, Wrp, Bp, mean, stdR) -> "NetData":
+        """A net from the byte streams a def_nn*.c file holds (interleaved order)."""
+        W, Wr, B = [], [], []
+        for i, t in enumerate(spec.types):
+            K, N = spec.sizes[i], spec.sizes[i + 1]
+            if t == LSTM:
+                W.append(unpack_lstm(Wp[i], N, K))
+                Wr.append(unpack_lstm(Wrp[i], N, N))
+                B.append(unpack_lstm_bias(Bp[i], N))
+            else:
+                W.append(unpack_fc(Wp[i], N, K))
+                Wr.append(None)
+                B.append(np.asarray(Bp[i], np.int16)[:N].copy())
+        return cls(spec, W, Wr, B, np.asarray(mean, np.int32).copy(), np.asarray(stdR, np.int32).copy())
+
+
+# The reference's own three nets: the tables of evb/src/def_nn0_s2i.c,
+# def_nn1_vad.c and def_nn2_kws_galaxy.c (weights, biases, feature mean/stdR,
+# every NeuralNetClass field), dumped as data by tests/golden/make_golden.py
+# from those files compiled here; the GPU box has no reference tree.
+REF_NETS_NPZ = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                            "ref_nets.npz")
+
+
+def ref_net(name: str, path: str | None = None) -> NetData:
+    """NetData of the reference's def_nn*.c net ``name`` ("vad", "kws", "s2i")."""
+    z = np.load(path or REF_NETS_NPZ, allow_pickle=False)
+    nl = int(z[f"{name}_numlayers"])
+    spec = NetSpec(name, [int(v) for v in z[f"{name}_size_layer"][:nl + 1]],
+                   [int(v) for v in z[f"{name}_layer_type"][:nl]], [int(v) for v in z[f"{name}_qbit_kernel"][:nl]],
+                   [int(v) for v in z[f"{name}_qbit_input"][:nl]], [int(v) for v in z[f"{name}_qbit_bias"][:nl]],
+                   [int(v) for v in z[f"{name}_activation_type"][:nl]])
+    Wp = [z[f"{name}_kernel{i}"] for i in range(nl)]
+    Wrp = [z[f"{name}_kernel_rec{i}"] if f"{name}_kernel_rec{i}" in z else None for i in range(nl)]
+    Bp = [z[f"{name}_bias{i}"] for i in range(nl)]
+    return NetData.from_packed(spec, Wp, Wrp, Bp, z[f"{name}_mean"], z[f"{name}_stdR"])
+
+
+def get_net(name: str, weights: str = "ref", seed: int = 1234) -> NetData:
+    """weights "ref": the reference's def_nn*.c tables; "synth": seeded synthetic."""
+    if weights == "ref":
+        return ref_net(name)
+    if weights == "synth":
+        return synth_net(name, seed)
+    raise ValueError(f"weights must be 'ref' or 'synth', not {weights!r}")
+
+
+# Net shapes beyond the three reference nets (SURVEY 8(f) N3): any FC/LSTM
+# stack of <= 10 layers the NeuralNetClass struct can describe -- rows not a
+# multiple of 4 (affine.c:103-149), odd K (:157-184), 3 and 7 layers, two
+# LSTM layers, a 256-wide FC layer.  Post-processing kind by nid.
+GEN_SPECS = {
+    "gen3": NetSpec("gen3", [240, 30, 21, 2], [FC, LSTM, FC], [7, 5, 6], [8, 15, 13], [14, 13, 15],
+                    [TANH, TANH, LINEAR], [(12, 0, 500, 6000), (6, 12, 300, 7000), (20, 0, 0, 6000)], nid=1),
+    "odd": NetSpec("odd", [240, 33, 21, 7, 2], [FC, LSTM, FC, FC], [7, 5, 5, 7], [8, 15, 15, 12],
+                   [14, 13, 15, 15], [TANH, TANH, RELU6, LINEAR],
+                   [(12, 0, 500, 6000), (6, 12, 300, 7000), (15, 0, 2000, 5000), (25, 0, 0, 6000)], nid=2),
+    "lstm2": NetSpec("lstm2", [240, 64, 48, 36, 20, 12, 41, 41], [FC, LSTM, LSTM, FC, FC, FC, FC],
+                     [7, 5, 5, 5, 5, 6, 5], [8, 15, 15, 15, 12, 12, 12], [14, 13, 13, 15, 15, 15, 14],
+                     [TANH, TANH, TANH, RELU6, RELU6, RELU6, LINEAR],
+                     [(12, 0, 500, 6000), (5, 10, 300, 7000), (6, 10, 300, 7000), (12, 0, 2000, 5000),
+                      (14, 0, 2000, 5000), (16, 0, 2000, 5000), (12, 0, -8000, 9000)], nid=0),
+    "wide": NetSpec("wide", [240, 256, 28, 256, 2], [FC, LSTM, FC, FC], [7, 5, 5, 7], [8, 15, 15, 12],
+                    [14, 13, 15, 15], [TANH, TANH, RELU6, LINEAR],
+                    [(10, 0, 500, 6000), (3, 12, 300, 7000), (15, 0, 2000, 5000), (8, 0, 0, 6000)], nid=1),
+}
+
+
+def synth_net(name: str | NetSpec, seed: int = 1234) -> NetData:
+    spec = name if isinstance(name, NetSpec) else (SPECS.get(name) or GEN_SPECS[name])
+    rng = np.random.default_rng([seed, spec.nn_id] + ([] if spec.name in SPECS else [len(spec.types)]))
 
     def i8(shape, std):
         return np.clip(np.round(rng.normal(0.0, std, shape)), -128, 127).astype(np.int8)

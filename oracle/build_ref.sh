@@ -1,25 +1,62 @@
 #!/usr/bin/env bash
-# Container-only: compile the reference ns-nnsp C files that build from their
-# own sources with the host gcc (no stand-in headers, no stand-in libraries)
-# into oracle/_ref/libnnsp_ref_partial.so.  TEST INFRASTRUCTURE ONLY.
+# Container-only: compile reference ns-nnsp C files, where they lie under
+# /root/reference, with the host gcc -- no stand-in headers, no stand-in
+# libraries, no copied sources.  Outputs go to oracle/_ref/ only (git-ignored).
+# TEST INFRASTRUCTURE ONLY: the checker of the oracle, never the product.
 #
-# Left out, because they cannot be built here without stand-ins:
-#   affine.c / affine_acc32b.c  ARM_OPTIMIZED=1 path needs the ARM DSP
-#                               intrinsics (__SXTB16/__SMLALD/__SMLAD), which the
-#                               vendored cmsis_gcc.h defines only as ARM asm;
-#   fft_arm.c                   calls CMSIS-DSP arm_rfft_q31 (ships as a Cortex-M
-#                               binary only, evb/libs/libCMSISDSP.a).
-# Their symbols stay undefined in the .so (it is loaded with RTLD_LAZY and the
-# tests never call a path that reaches them).
+#  libnnsp_ref_partial.so      the shipped (ARM_OPTIMIZED=1) build's files that
+#                              compile as they are: activation, fixlog10, mel,
+#                              window, spectrogram_module, feature_module,
+#                              neural_nets, nn_speech, lstm.  Left out:
+#                              affine.c / affine_acc32b.c (their ARM path needs
+#                              the ARM DSP intrinsics, which the vendored
+#                              cmsis_gcc.h defines only as ARM asm) and
+#                              fft_arm.c (calls CMSIS-DSP arm_rfft_q31, shipped
+#                              only as a Cortex-M binary).  Their symbols stay
+#                              undefined (loaded with RTLD_LAZY; never reached).
+#  libnnsp_ref_nn_portable.so  the reference's own portable NN build: affine.c,
+#                              affine_acc32b.c, lstm.c, neural_nets.c,
+#                              activation.c with the reference's compile-time
+#                              switches set on the command line
+#                              (ambiq_nnsp_debug.h's guard macro predefined,
+#                              AMBIQ_NNSP_DEBUG=0, ARM_OPTIMIZED=0) and the
+#                              vendored CMSIS Core include for cmsis_gcc.h.
+#                              Same arithmetic as the shipped path after the MAC
+#                              loop (affine.c:186-253 vs :311-339); it walks the
+#                              weights in the portable order and applies the
+#                              align shift that is dead in the shipped build (T1).
+#  libnnsp_ref_nets.so         evb/src/def_nn{0_s2i,1_vad,2_kws_galaxy}.c (the
+#                              reference's three nets as data) against the
+#                              reference headers, linked with the portable NN
+#                              build so their layer_func addresses resolve.
 set -euo pipefail
 REF=${REF:-/root/reference}
 OUT=$(cd "$(dirname "$0")" && pwd)/_ref
 [ -d "$REF/ns-nnsp/src" ] || { echo "reference not present: skip"; exit 0; }
 mkdir -p "$OUT"
 SRC=$REF/ns-nnsp/src
-gcc -O2 -fPIC -shared -w -fwrapv -I"$REF/ns-nnsp/includes-api" \
+API=$REF/ns-nnsp/includes-api
+CORE=$REF/evb/includes/extern/CMSIS/CMSIS_5-5.9.0/CMSIS/Core/Include
+
+gcc -O2 -fPIC -shared -w -fwrapv -I"$API" \
     "$SRC/activation.c" "$SRC/fixlog10.c" "$SRC/melSpecProc.c" "$SRC/melSpec_coeff.c" \
     "$SRC/window_stft_coef.c" "$SRC/spectrogram_module.c" "$SRC/feature_module.c" \
     "$SRC/neural_nets.c" "$SRC/nn_speech.c" "$SRC/lstm.c" \
     -o "$OUT/libnnsp_ref_partial.so"
-echo "$OUT/libnnsp_ref_partial.so"
+
+gcc -O2 -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NNSP_DEBUG=0 -DARM_OPTIMIZED=0 \
+    -I"$API" -I"$CORE" \
+    "$SRC/affine.c" "$SRC/affine_acc32b.c" "$SRC/lstm.c" "$SRC/neural_nets.c" "$SRC/activation.c" \
+    -Wl,-z,defs -o "$OUT/libnnsp_ref_nn_portable.so"
+
+gcc -O2 -fPIC -shared -w -I"$API" \
+    "$REF/evb/src/def_nn0_s2i.c" "$REF/evb/src/def_nn1_vad.c" "$REF/evb/src/def_nn2_kws_galaxy.c" \
+    -L"$OUT" -lnnsp_ref_nn_portable -Wl,-rpath,'$ORIGIN' -Wl,-z,defs -o "$OUT/libnnsp_ref_nets.so"
+
+# the reference timed beside the oracle on the same cores (container
+# calibration, BASELINE.md / SURVEY 8(d)): -O3 -march=native like the oracle
+gcc -O3 -march=native -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NNSP_DEBUG=0 -DARM_OPTIMIZED=0 \
+    -I"$API" -I"$CORE" \
+    "$SRC/affine.c" "$SRC/affine_acc32b.c" "$SRC/lstm.c" "$SRC/neural_nets.c" "$SRC/activation.c" \
+    -Wl,-z,defs -o "$OUT/libnnsp_ref_nn_portable_o3.so"
+echo "$OUT"

@@ -312,7 +312,7 @@ static void shift_acc(i64 *a, int sh, int n, int acc32) /* shift_64b :565-591 / 
  * reference's pp_kernel / pp_bias; *po advances by the activation's width. */
 static void affine_rows(int R, const int8_t **pw, const int16_t **pb, const int16_t *x, int K,
                         int qk, int qb, int qi, i64 *acc, int acc32, int is_out, int act,
-                        char **po)
+                        char **po, int portable)
 {
     const int8_t *w = *pw;
     const int qs = pb ? (qi + qk > 15 ? qi + qk : 15) : qi + qk;
@@ -345,7 +345,9 @@ static void affine_rows(int R, const int8_t **pw, const int16_t **pb, const int1
     if (acc32)
         for (int r = 0; r < R; ++r) s[r] = w32(s[r]);
     /* affine.c:186-187: the "align acc" shift acts on pt_accum, which is
-     * overwritten below -- dead in the shipped build (trap T1). */
+     * overwritten below -- dead in the shipped build (trap T1).  The portable
+     * build (affine.c:311-313) applies it to the live sums. */
+    if (portable) shift_acc(s, qs - (qi + qk), R, acc32);
     if (pb) {
         const int16_t *b = *pb;
         const int sh = qs - qb;
@@ -372,12 +374,12 @@ static void affine_rows(int R, const int8_t **pw, const int16_t **pb, const int1
 
 static void rc_rows(int R, char **po, const int8_t **pw, const int8_t **pwr, const int16_t **pb,
                     const int16_t *x, const int16_t *h, int K, int Kr, int qk, int qb, int qi,
-                    int qir, int act, int acc32) /* affine.c:348-407 */
+                    int qir, int act, int acc32, int portable) /* affine.c:348-407 */
 {
     i64 acc[4] = {0, 0, 0, 0};
-    affine_rows(R, pw, NULL, x, K, qk, qb, qi, acc, acc32, 0, act, po);
+    affine_rows(R, pw, NULL, x, K, qk, qb, qi, acc, acc32, 0, act, po, portable);
     shift_acc(acc, qir - qi, R, acc32);
-    affine_rows(R, pwr, pb, h, Kr, qk, qb, qir, acc, acc32, 1, act, po);
+    affine_rows(R, pwr, pb, h, Kr, qk, qb, qir, acc, acc32, 1, act, po, portable);
 }
 
 void or_affine_krows(int32_t R, const int8_t *w, const int16_t *b, const int16_t *x, int32_t K, int32_t qk,
@@ -386,7 +388,7 @@ void or_affine_krows(int32_t R, const int8_t *w, const int16_t *b, const int16_t
     const int8_t *pw = w;
     const int16_t *pb = b;
     char *po = (char *)out;
-    affine_rows(R, &pw, b ? &pb : NULL, x, K, qk, qb, qi, acc, acc32, is_out, act, &po);
+    affine_rows(R, &pw, b ? &pb : NULL, x, K, qk, qb, qi, acc, acc32, is_out, act, &po, 0);
 }
 
 void or_rc_layer(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b, const int16_t *x,
@@ -397,34 +399,35 @@ void or_rc_layer(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b,
     const int8_t *pw = w, *pwr = wr;
     const int16_t *pb = b;
     for (int r0 = 0; r0 < N; r0 += 4)
-        rc_rows(N - r0 >= 4 ? 4 : N - r0, &po, &pw, &pwr, b ? &pb : NULL, x, h, K, Kr, qk, qb, qi, qir, act, acc32);
+        rc_rows(N - r0 >= 4 ? 4 : N - r0, &po, &pw, &pwr, b ? &pb : NULL, x, h, K, Kr, qk, qb, qi, qir, act, acc32,
+                0);
 }
 
 void or_shift(int64_t *a, int32_t sh, int32_t n, int32_t acc32) { shift_acc(a, sh, n, acc32); }
 
 static void fc_layer(char *out, const int8_t *w, const int16_t *b, const int16_t *x, int N, int K,
-                     int qk, int qb, int qi, int act, int acc32) /* affine.c:409-490 */
+                     int qk, int qb, int qi, int act, int acc32, int portable) /* affine.c:409-490 */
 {
     char *po = out;
     for (int r0 = 0; r0 < N; r0 += 4) {
         const int R = N - r0 >= 4 ? 4 : N - r0;
         i64 acc[4] = {0, 0, 0, 0};
-        affine_rows(R, &w, &b, x, K, qk, qb, qi, acc, acc32, 1, act, &po);
+        affine_rows(R, &w, &b, x, K, qk, qb, qi, acc, acc32, 1, act, &po, portable);
     }
 }
 
 static void lstm_layer(i16 *out, const int8_t *w, const int8_t *wr, const int16_t *b,
                        const int16_t *x, i16 *h, i32 *c, int N, int K, int qk, int qb, int qi,
-                       int qir, int acc32) /* lstm.c:15-214 */
+                       int qir, int acc32, int portable) /* lstm.c:15-214 */
 {
     for (int u0 = 0; u0 < N; u0 += 4) {
         const int R = N - u0 >= 4 ? 4 : N - u0;
         i16 gi[4], gj[4], gf[4], go[4];
         char *p;
-        p = (char *)gi; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
-        p = (char *)gj; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_TANH, acc32);
-        p = (char *)gf; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
-        p = (char *)go; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32);
+        p = (char *)gi; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32, portable);
+        p = (char *)gj; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_TANH, acc32, portable);
+        p = (char *)gf; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32, portable);
+        p = (char *)go; rc_rows(R, &p, &w, &wr, &b, x, h, K, N, qk, qb, qi, qir, OR_SIGMOID, acc32, portable);
         for (int r = 0; r < R; ++r) {
             const i64 cv = ((i64)gi[r] * gj[r] + (i64)gf[r] * c[u0 + r]) >> 15;
             c[u0 + r] = sat32(cv);
@@ -433,6 +436,19 @@ static void lstm_layer(i16 *out, const int8_t *w, const int8_t *wr, const int16_
         }
     }
     memcpy(h, out, (size_t)N * sizeof(i16)); /* h updated after all groups (T6) */
+}
+
+void or_fc(int32_t N, const int8_t *w, const int16_t *b, const int16_t *x, int32_t K, int32_t qk, int32_t qb,
+           int32_t qi, int32_t act, int32_t acc32, int32_t portable, void *out)
+{
+    fc_layer((char *)out, w, b, x, N, K, qk, qb, qi, act, acc32, portable);
+}
+
+void or_lstm(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b, const int16_t *x, int16_t *h,
+             int32_t *c, int32_t K, int32_t qk, int32_t qb, int32_t qi, int32_t qir, int32_t acc32,
+             int32_t portable, int16_t *out)
+{
+    lstm_layer(out, w, wr, b, x, h, c, N, K, qk, qb, qi, qir, acc32, portable);
 }
 
 void or_nn_reset(const or_net *net, or_stream *st) /* neural_nets.c:27-42 */
@@ -463,11 +479,11 @@ void or_net_forward(const or_net *net, or_stream *st, const int16_t *in, int32_t
         const int qir = i + 1 < OR_MAX_LAYERS ? net->qi[i + 1] : 0;
         if (net->type[i] == OR_LSTM) {
             lstm_layer(nxt, net->W[i], net->Wr[i], net->B[i], cur, st->h[l], st->c[l], N, K,
-                       net->qk[i], net->qb[i], net->qi[i], qir, net->acc32);
+                       net->qk[i], net->qb[i], net->qi[i], qir, net->acc32, net->portable);
             ++l;
         } else {
             fc_layer((char *)nxt, net->W[i], net->B[i], cur, N, K, net->qk[i], net->qb[i],
-                     net->qi[i], net->act[i], net->acc32);
+                     net->qi[i], net->act[i], net->acc32, net->portable);
         }
         i16 *t = cur; cur = nxt; nxt = t;
     }

@@ -13,9 +13,15 @@
  *     against reference C files compiled here from their own sources
  *     (oracle/_ref -> tests/golden/ref_stages.npz, tests/test_oracle_pinned.py);
  *   - weight layout: pinned against python/nnsp_pack/c_weight_man.py;
- *   - affine/LSTM MAC kernels (affine.c ARM path needs ARM DSP intrinsics)
- *     and the CMSIS arm_rfft_q31 (binary-only third-party code): restated,
- *     "parity unpinned" beyond the checks listed in DESIGN.md.
+ *   - affine / rc / LSTM / NeuralNetClass_exe: pinned against the
+ *     reference's own portable NN build (affine.c, affine_acc32b.c, lstm.c,
+ *     neural_nets.c compiled with ARM_OPTIMIZED=0 -> tests/golden/ref_nn.npz)
+ *     on re-packed weights, including the reference's three nets; that build
+ *     differs from the shipped one only in the byte walk (pinned by
+ *     layout.npz) and the live align shift (or_net.portable = 1 reproduces
+ *     it; the shipped build's dead shift is trap T1);
+ *   - CMSIS arm_rfft_q31 (binary-only third-party code): restated, "parity
+ *     unpinned" beyond its tables and a float-DFT check.
  */
 #ifndef NNSP_ORACLE_H
 #define NNSP_ORACLE_H
@@ -46,6 +52,7 @@ typedef struct {
     const int8_t *W[OR_MAX_LAYERS];
     const int8_t *Wr[OR_MAX_LAYERS];
     const int16_t *B[OR_MAX_LAYERS];
+    int32_t portable; /* 1: the ARM_OPTIMIZED=0 build's live align shift (affine.c:311-313), 0: shipped (T1) */
 } or_net;
 
 /* Per-stream state of one NNSPClass + FeatureClass + LSTM h/c. */
@@ -91,6 +98,13 @@ void or_rc_layer(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b,
                  const int16_t *h, int32_t K, int32_t Kr, int32_t qk, int32_t qb, int32_t qi, int32_t qir,
                  int32_t act, int32_t acc32, void *out);
 void or_shift(int64_t *a, int32_t sh, int32_t n, int32_t acc32);
+/* fc_8x16(_acc32b) / lstm_8x16(_acc32b) on a whole layer (natural order of the
+ * interleaved weight stream; h / c updated in place).  portable: see or_net. */
+void or_fc(int32_t N, const int8_t *w, const int16_t *b, const int16_t *x, int32_t K, int32_t qk, int32_t qb,
+           int32_t qi, int32_t act, int32_t acc32, int32_t portable, void *out);
+void or_lstm(int32_t N, const int8_t *w, const int8_t *wr, const int16_t *b, const int16_t *x, int16_t *h,
+             int32_t *c, int32_t K, int32_t qk, int32_t qb, int32_t qi, int32_t qir, int32_t acc32,
+             int32_t portable, int16_t *out);
 
 /* NN */
 void or_nn_reset(const or_net *net, or_stream *st);

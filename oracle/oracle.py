@@ -22,7 +22,7 @@ class or_net(C.Structure):
     _fields_ = [("nl", C.c_int32), ("size", C.c_int32 * (MAXL + 1)), ("type", C.c_int32 * MAXL),
                 ("qk", C.c_int32 * MAXL), ("qi", C.c_int32 * MAXL), ("qb", C.c_int32 * MAXL),
                 ("act", C.c_int32 * MAXL), ("acc32", C.c_int32), ("W", C.c_void_p * MAXL),
-                ("Wr", C.c_void_p * MAXL), ("B", C.c_void_p * MAXL)]
+                ("Wr", C.c_void_p * MAXL), ("B", C.c_void_p * MAXL), ("portable", C.c_int32)]
 
 
 class or_cfg(C.Structure):
@@ -65,7 +65,8 @@ def p(a):
 class OracleNet:
     """or_net + or_cfg built from nnsp_amd.nets.NetData (packed byte layout)."""
 
-    def __init__(self, data, acc32: bool = False, thresh_prob: int = 32767 >> 1, th_count: int = 4):
+    def __init__(self, data, acc32: bool = False, thresh_prob: int = 32767 >> 1, th_count: int = 4,
+                 portable: bool = False):
         spec = data.spec
         Wp, Wrp, Bp = data.packed()
         self.keep = []
@@ -87,6 +88,7 @@ class OracleNet:
                 self.keep.append(wr)
                 n.Wr[i] = wr.ctypes.data
         n.acc32 = int(acc32)
+        n.portable = int(portable)   # the ARM_OPTIMIZED=0 build's live align shift (pinning only)
         self.net = n
         self.mean = np.ascontiguousarray(data.mean, np.int32)
         self.stdR = np.ascontiguousarray(data.stdR, np.int32)
@@ -126,7 +128,7 @@ class OracleNet:
             lib().or_nnsp_reset(C.byref(self.net), C.c_void_p(states[s].ctypes.data), C.byref(self.cfg))
 
     def forward(self, x240: np.ndarray, state: np.ndarray, n_layers: int = -1) -> np.ndarray:
-        out = np.zeros(64, np.int32)
+        out = np.zeros(160, np.int32)
         x = np.ascontiguousarray(x240, np.int16)
         lib().or_net_forward(C.byref(self.net), C.c_void_p(state.ctypes.data), p(x), p(out), n_layers)
         return out
@@ -167,6 +169,32 @@ class OracleCascade:
         o3 = np.zeros((S, T, 3), np.int16)
         lib().or_run_cascade(C.byref(self.cfg), p(states), S, T, p(pcm), p(ran), p(det), p(o3))
         return ran, det, o3, states
+
+
+def fc(w: np.ndarray, b: np.ndarray, x: np.ndarray, qk: int, qb: int, qi: int, act: int, acc32: bool,
+       portable: bool = False) -> np.ndarray:
+    """fc_8x16(_acc32b) on natural W[N][K] (packed here in the shipped order)."""
+    from nnsp_amd.nets import LINEAR, pack_fc
+    N, K = w.shape
+    wp = np.ascontiguousarray(pack_fc(w))
+    bb = None if b is None else np.ascontiguousarray(b, np.int16)
+    xx = np.ascontiguousarray(x, np.int16)
+    y = np.zeros(N, np.int32 if act == LINEAR else np.int16)
+    lib().or_fc(N, p(wp), p(bb), p(xx), K, qk, qb, qi, act, int(acc32), int(portable), p(y))
+    return y.astype(np.int32)
+
+
+def lstm(w, wr, b, x, h, c, qk, qb, qi, qir, acc32: bool, portable: bool = False) -> np.ndarray:
+    """lstm_8x16(_acc32b) on natural gate-major W[4N][K]; h (int16[N]) and c
+    (int32[N]) are updated in place."""
+    from nnsp_amd.nets import pack_lstm, pack_lstm_bias
+    N, K = w.shape[0] // 4, w.shape[1]
+    wp, wrp = np.ascontiguousarray(pack_lstm(w)), np.ascontiguousarray(pack_lstm(wr))
+    bp = np.ascontiguousarray(pack_lstm_bias(b))
+    xx = np.ascontiguousarray(x, np.int16)
+    y = np.zeros(N, np.int16)
+    lib().or_lstm(N, p(wp), p(wrp), p(bp), p(xx), p(h), p(c), K, qk, qb, qi, qir, int(acc32), int(portable), p(y))
+    return y
 
 
 def rfft512(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:

@@ -12,6 +12,18 @@ reference tree).
                    my_argmax, binary_post_proc, s2i_post_proc),
                    feature_module.c (FeatureClass_setDefault)
   layout.npz       python/nnsp_pack/c_weight_man.py (weight byte layout)
+  ref_nets.npz     evb/src/def_nn{0_s2i,1_vad,2_kws_galaxy}.c as data: every
+                   NeuralNetClass field of net_s2i / net_vad / net_kws_galaxy,
+                   the int8 kernels and int16 biases byte for byte (interleaved
+                   order), feature_mean / feature_stdR (oracle/_ref/libnnsp_ref_nets.so)
+  ref_nn.npz       the reference's portable NN build (ARM_OPTIMIZED=0,
+                   oracle/_ref/libnnsp_ref_nn_portable.so) on weights re-packed
+                   into its byte order: fc_8x16 / lstm_8x16 / rc_8x16 and their
+                   _acc32b twins called directly, and NeuralNetClass_exe over
+                   consecutive calls (LSTM state carried) on the three reference
+                   nets and on the N3 shapes of nnsp_amd.nets.GEN_SPECS
+
+Usage: make_golden.py [stages] [nets] [nn]   (default: all)
 """
 from __future__ import annotations
 
@@ -25,9 +37,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_partial.so")
+REF_NN_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nn_portable.so")
+REF_NETS_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nets.so")
 REF_PY = "/root/reference/python"
 
-from nnsp_amd._lib import FeatureClass, NNSPClass  # noqa: E402  (ABI mirrors)
+from nnsp_amd._lib import FeatureClass, NeuralNetClass, NNSPClass  # noqa: E402  (ABI mirrors)
+from nnsp_amd import nets as N  # noqa: E402
 
 
 def P(a):
@@ -51,9 +66,7 @@ def log_inputs(rng):
     return np.clip(x, 0, 2**31 - 1).astype(np.int32)
 
 
-def main() -> None:
-    if not os.path.exists(REF_SO):
-        sys.exit("build oracle/_ref first (oracle/build_ref.sh)")
+def stages() -> None:
     R = C.CDLL(REF_SO, mode=os.RTLD_LAZY)
     rng = np.random.default_rng(20261015)
     out = {}
@@ -200,7 +213,181 @@ def main() -> None:
         lay[f"lstm_{j}_out_wr"] = ar.astype(np.int64).astype(np.int8)
         lay[f"lstm_{j}_out_b"] = bb.astype(np.int64).astype(np.int16)
     np.savez_compressed(os.path.join(HERE, "layout.npz"), **lay)
-    print("wrote", os.listdir(HERE))
+
+
+NET_SYMS = {"vad": ("net_vad", "vad"), "kws": ("net_kws_galaxy", "kws_galaxy"), "s2i": ("net_s2i", "s2i")}
+
+
+def nets() -> None:
+    """The three def_nn*.c nets, every table and field, as data."""
+    L = C.CDLL(REF_NETS_SO)
+    out = {}
+    for name, (sym, suffix) in NET_SYMS.items():
+        net = NeuralNetClass.in_dll(L, sym)
+        nl = net.numlayers
+        out[f"{name}_numlayers"] = np.int32(nl)
+        for f in ("size_layer", "net_layer_type", "qbit_kernel", "qbit_input", "qbit_bias", "activation_type"):
+            key = "layer_type" if f == "net_layer_type" else f
+            out[f"{name}_{key}"] = np.array(list(getattr(net, f)), np.int32)
+        for i in range(nl):
+            K, Nn = net.size_layer[i], net.size_layer[i + 1]
+            lstm = net.net_layer_type[i] == N.LSTM
+            rows = 4 * Nn if lstm else Nn
+            out[f"{name}_kernel{i}"] = np.ctypeslib.as_array((C.c_int8 * (rows * K)).from_address(net.pt_kernel[i])).copy()
+            out[f"{name}_bias{i}"] = np.ctypeslib.as_array((C.c_int16 * rows).from_address(net.pt_bias[i])).copy()
+            if lstm:
+                out[f"{name}_kernel_rec{i}"] = np.ctypeslib.as_array(
+                    (C.c_int8 * (rows * Nn)).from_address(net.pt_kernel_rec[i])).copy()
+        for what in ("mean", "stdR"):
+            out[f"{name}_{what}"] = np.ctypeslib.as_array((C.c_int32 * 40).in_dll(L, f"feature_{what}_{suffix}")).copy()
+    np.savez_compressed(os.path.join(HERE, "ref_nets.npz"), **out)
+
+
+class PortableNet:
+    """A NeuralNetClass over the portable reference build, weights re-packed
+    into its byte order (affine.c:291-309), private LSTM h/c."""
+
+    def __init__(self, R, data, acc32):
+        spec = data.spec
+        Wp, Wrp, Bp = data.packed_portable()
+        self.keep, self.h, self.c = [], [], []
+        n = NeuralNetClass()
+        n.numlayers = spec.nl
+        for i, s in enumerate(spec.sizes):
+            n.size_layer[i] = s
+        acts = {N.RELU6: "relu6_fix", N.TANH: "tanh_fix", N.SIGMOID: "sigmoid_fix", N.LINEAR: "linear_fix"}
+        for i, t in enumerate(spec.types):
+            n.net_layer_type[i] = t
+            n.qbit_kernel[i], n.qbit_input[i], n.qbit_bias[i] = spec.qk[i], spec.qi[i], spec.qb[i]
+            n.activation_type[i] = spec.acts[i]
+            n.act_func[i] = C.cast(getattr(R, acts[spec.acts[i]]), C.c_void_p).value
+            fn = ("lstm_8x16" if t == N.LSTM else "fc_8x16") + ("_acc32b" if acc32 else "")
+            n.layer_func[i] = C.cast(getattr(R, fn), C.c_void_p).value
+            w, b = np.ascontiguousarray(Wp[i], np.int8), np.ascontiguousarray(Bp[i], np.int16)
+            self.keep += [w, b]
+            n.pt_kernel[i], n.pt_bias[i] = w.ctypes.data, b.ctypes.data
+            if t == N.LSTM:
+                wr = np.ascontiguousarray(Wrp[i], np.int8)
+                h = np.zeros(spec.sizes[i + 1], np.int16)
+                c = np.zeros(spec.sizes[i + 1], np.int32)
+                self.keep.append(wr)
+                self.h.append(h)
+                self.c.append(c)
+                n.pt_kernel_rec[i], n.pt_hstate[i], n.pt_cstate[i] = wr.ctypes.data, h.ctypes.data, c.ctypes.data
+        self.net, self.R, self.spec = n, R, spec
+        R.NeuralNetClass_setDefault(C.byref(n))
+
+    def exe(self, x):
+        out = np.zeros(160, np.int32)
+        xx = np.ascontiguousarray(x, np.int16)
+        self.R.NeuralNetClass_exe(C.byref(self.net), P(xx), P(out), C.c_int8(-1))
+        if self.spec.acts[-1] == N.LINEAR:
+            return out[:self.spec.nout].copy()
+        return out.view(np.int16)[:self.spec.nout].astype(np.int32)
+
+
+def nn_inputs(rng, n, K):
+    """Layer inputs: feature-like (Q8 normalised log-Mel), wide, full range."""
+    a = np.clip(np.round(rng.normal(0, 700, (n, K))), -32768, 32767)
+    a[n // 2: 3 * n // 4] = rng.integers(-6000, 6000, (n - n // 2 - (n - 3 * n // 4), K))
+    a[3 * n // 4:] = rng.integers(-32768, 32768, (n - 3 * n // 4, K))
+    return a.astype(np.int16)
+
+
+# direct layer calls: (N, K, qk, qb, qi, act); cases with qi + qk < 15 and a
+# bias hit the align shift that the shipped build leaves dead (T1)
+FC_CASES = [(4, 240, 7, 14, 8, N.TANH), (28, 240, 6, 13, 8, N.TANH), (5, 28, 5, 15, 15, N.RELU6),
+            (7, 33, 5, 15, 12, N.RELU6), (2, 28, 7, 15, 12, N.LINEAR), (41, 72, 5, 14, 12, N.LINEAR),
+            (3, 9, 6, 18, 12, N.SIGMOID), (1, 1, 7, 9, 10, N.TANH), (6, 7, 4, 12, 15, N.LINEAR),
+            (256, 240, 7, 14, 8, N.TANH), (9, 256, 5, 15, 12, N.RELU6), (64, 64, 5, 15, 15, N.RELU6)]
+# (N, K, qk, qb, qi, qir): qir != qi exercises rc_Krows' shift of the input half
+LSTM_CASES = [(28, 240, 5, 13, 15, 15), (5, 7, 5, 13, 15, 15), (6, 33, 5, 14, 15, 15),
+              (1, 3, 6, 14, 15, 15), (7, 28, 5, 13, 15, 13), (4, 12, 4, 12, 15, 17), (72, 72, 5, 14, 15, 15),
+              (3, 10, 7, 12, 8, 8)]
+
+
+def nn() -> None:
+    R = C.CDLL(REF_NN_SO)
+    R.NeuralNetClass_exe.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int8]
+    i16 = C.c_int16
+    rng = np.random.default_rng(20261016)
+    out = {}
+    # ---- fc_8x16 / fc_8x16_acc32b (affine.c:409-490)
+    for k, (Nn, K, qk, qb, qi, act) in enumerate(FC_CASES):
+        w = rng.integers(-128, 128, (Nn, K)).astype(np.int8)
+        if k % 3 == 1:
+            w = np.clip(np.round(rng.normal(0, 12, (Nn, K))), -128, 127).astype(np.int8)
+        b = rng.integers(-32768, 32768, Nn).astype(np.int16)
+        x = nn_inputs(rng, 8, K)
+        wp = N.pack_fc_portable(w)
+        afn = C.cast(getattr(R, {N.RELU6: "relu6_fix", N.TANH: "tanh_fix", N.SIGMOID: "sigmoid_fix",
+                                 N.LINEAR: "linear_fix"}[act]), C.c_void_p)
+        for acc32 in (0, 1):
+            f = R.fc_8x16_acc32b if acc32 else R.fc_8x16
+            ys = np.zeros((8, Nn), np.int32)
+            for r in range(8):
+                y = np.zeros(2 * Nn + 2, np.int16)
+                f(P(y), P(wp), None, P(b), P(x[r]), None, None, i16(Nn), i16(K), i16(Nn), i16(qk), i16(qb),
+                  i16(qi), i16(0), C.c_int(act), afn)
+                ys[r] = y.view(np.int32)[:Nn] if act == N.LINEAR else y[:Nn]
+            out[f"fc{k}_y{32 if acc32 else 64}"] = ys
+        out[f"fc{k}_w"], out[f"fc{k}_b"], out[f"fc{k}_x"] = w, b, x
+        out[f"fc{k}_cfg"] = np.array([Nn, K, qk, qb, qi, act], np.int32)
+    # ---- lstm_8x16 / lstm_8x16_acc32b (lstm.c:15-415), 4 calls carrying h / c
+    for k, (Nn, K, qk, qb, qi, qir) in enumerate(LSTM_CASES):
+        w = np.clip(np.round(rng.normal(0, 10, (4 * Nn, K))), -128, 127).astype(np.int8)
+        wr = np.clip(np.round(rng.normal(0, 14, (4 * Nn, Nn))), -128, 127).astype(np.int8)
+        if k % 2:
+            w = rng.integers(-128, 128, (4 * Nn, K)).astype(np.int8)
+        b = rng.integers(-20000, 20000, 4 * Nn).astype(np.int16)
+        x = nn_inputs(rng, 4, K)
+        if qi < 15:
+            x = (x // 64).astype(np.int16)
+        wp, wrp, bp = N.pack_lstm_portable(w), N.pack_lstm_portable(wr), N.pack_lstm_bias(b)
+        for acc32 in (0, 1):
+            f = R.lstm_8x16_acc32b if acc32 else R.lstm_8x16
+            h = np.zeros(Nn, np.int16)
+            c = np.zeros(Nn, np.int32)
+            ys, hs, cs = np.zeros((4, Nn), np.int16), np.zeros((4, Nn), np.int16), np.zeros((4, Nn), np.int32)
+            for r in range(4):
+                y = np.zeros(Nn + 4, np.int16)
+                f(P(y), P(wp), P(wrp), P(bp), P(x[r]), P(h), P(c), i16(Nn), i16(K), i16(Nn), i16(qk), i16(qb),
+                  i16(qi), i16(qir), C.c_int(N.TANH), C.cast(R.tanh_fix, C.c_void_p))
+                ys[r], hs[r], cs[r] = y[:Nn], h, c
+            tag = 32 if acc32 else 64
+            out[f"lstm{k}_y{tag}"], out[f"lstm{k}_h{tag}"], out[f"lstm{k}_c{tag}"] = ys, hs, cs
+        out[f"lstm{k}_w"], out[f"lstm{k}_wr"], out[f"lstm{k}_b"], out[f"lstm{k}_x"] = w, wr, b, x
+        out[f"lstm{k}_cfg"] = np.array([Nn, K, qk, qb, qi, qir], np.int32)
+    # ---- NeuralNetClass_exe over consecutive calls: the reference nets (their
+    #      own tables, re-packed) and the N3 shapes (synthetic weights)
+    cases = [("vad", N.ref_net("vad")), ("kws", N.ref_net("kws")), ("s2i", N.ref_net("s2i"))]
+    cases += [(g, N.synth_net(g, 77)) for g in N.GEN_SPECS]
+    for name, data in cases:
+        x = nn_inputs(rng, 24, data.spec.sizes[0])
+        out[f"net_{name}_x"] = x
+        if name in N.GEN_SPECS:
+            for i in range(data.spec.nl):
+                out[f"net_{name}_W{i}"], out[f"net_{name}_B{i}"] = data.W[i], data.B[i]
+                if data.Wr[i] is not None:
+                    out[f"net_{name}_Wr{i}"] = data.Wr[i]
+        for acc32 in (0, 1):
+            pn = PortableNet(R, data, acc32)
+            ys = np.stack([pn.exe(x[r]) for r in range(len(x))])
+            tag = 32 if acc32 else 64
+            out[f"net_{name}_y{tag}"] = ys
+            out[f"net_{name}_h{tag}"] = np.concatenate(pn.h) if pn.h else np.zeros(0, np.int16)
+            out[f"net_{name}_c{tag}"] = np.concatenate(pn.c) if pn.c else np.zeros(0, np.int32)
+    np.savez_compressed(os.path.join(HERE, "ref_nn.npz"), **out)
+
+
+def main() -> None:
+    for so in (REF_SO, REF_NN_SO, REF_NETS_SO):
+        if not os.path.exists(so):
+            sys.exit("build oracle/_ref first (oracle/build_ref.sh)")
+    which = sys.argv[1:] or ["stages", "nets", "nn"]
+    for w in which:   # nets before nn: nn re-packs the dumped reference nets
+        {"stages": stages, "nets": nets, "nn": nn}[w]()
+    print("wrote", sorted(os.listdir(HERE)))
 
 
 if __name__ == "__main__":

@@ -95,3 +95,43 @@ def test_struct_abi_matches_headers():
 @pytest.mark.skipif(not os.path.isdir("/root/reference/ns-nnsp"), reason="reference absent")
 def test_struct_abi_matches_reference_headers():
     assert _layout(os.path.join(ROOT, "include")) == _layout("/root/reference/ns-nnsp/includes-api")
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/evb/src"), reason="reference absent")
+@pytest.mark.parametrize("acc32", [False, True])
+def test_reference_def_nets_compile_and_link_unchanged(tmp_path, acc32):
+    """The reference's evb/src/def_nn{0_s2i,1_vad,2_kws_galaxy}.c compile
+    unchanged against include/ and link against libnnsp_mi355x.so (the drop-in
+    claim); their layer_func / act_func entries resolve to this
+    library's fc_8x16 / lstm_8x16 (or the _acc32b twins under DEF_ACC32BIT_OPT,
+    evb/Makefile:30-32) and activations, and their tables equal the committed
+    tests/golden/ref_nets.npz dump."""
+    import subprocess
+
+    import numpy as np
+
+    from nnsp_amd import nets
+
+    src = "/root/reference/evb/src"
+    so = str(tmp_path / "libdefnets.so")
+    cmd = ["gcc", "-O1", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include")]
+    cmd += ["-DDEF_ACC32BIT_OPT"] if acc32 else []
+    cmd += [os.path.join(src, f) for f in ("def_nn0_s2i.c", "def_nn1_vad.c", "def_nn2_kws_galaxy.c")]
+    cmd += ["-L", os.path.dirname(_lib.LIB_PATH), "-lnnsp_mi355x", "-Wl,-rpath," + os.path.dirname(_lib.LIB_PATH),
+            "-Wl,-z,defs", "-Wl,--allow-shlib-undefined", "-o", so]
+    subprocess.check_call(cmd)
+    L = _lib.lib()
+    D = C.CDLL(so)
+    z = np.load(nets.REF_NETS_NPZ)
+    for name, sym in (("vad", "net_vad"), ("kws", "net_kws_galaxy"), ("s2i", "net_s2i")):
+        n = _lib.NeuralNetClass.in_dll(D, sym)
+        for i in range(n.numlayers):
+            lstm = n.net_layer_type[i] == nets.LSTM
+            want = ("lstm_8x16" if lstm else "fc_8x16") + ("_acc32b" if acc32 else "")
+            assert n.layer_func[i] == _lib.fn_addr(want), (name, i)
+            act = ["relu6_fix", "tanh_fix", "sigmoid_fix", "linear_fix"][n.activation_type[i]]
+            assert n.act_func[i] == _lib.fn_addr(act), (name, i)
+            K, N = n.size_layer[i], n.size_layer[i + 1]
+            rows = 4 * N if lstm else N
+            kern = np.ctypeslib.as_array((C.c_int8 * (rows * K)).from_address(n.pt_kernel[i]))
+            np.testing.assert_array_equal(kern, z[f"{name}_kernel{i}"])
