@@ -5,34 +5,58 @@ Metric (BASELINE.json): audio frames/s (16 kHz, 10 ms hop) per node at
 1/2/4/8 GPUs, bit-exact vs the reference.  One frame = 160 samples of one
 stream.  The default workload is BASELINE configs[4], the one the 1/2/4/8-GPU
 curve is quoted on: the full VAD -> Hi-Galaxy KWS -> S2I cascade
-(nnCntrlClass_exec per frame) with 32768 streams per GPU (262144 on 8 GPUs).
---net vad|kws|s2i runs configs[1..3] (one net, 8192 streams/GPU).
+(nnCntrlClass_exec per frame, evb/src/nnCntrlClass.c:152-272) with 32768
+streams per GPU (262144 on 8 GPUs).  --net vad|kws|s2i runs configs[1..3] (one
+net, 8192 streams/GPU).
+
+Nets: the reference's own three nets (--weights ref, default: the def_nn*.c
+tables, tests/golden/ref_nets.npz); --weights synth uses seeded synthetic
+weights of the same shapes (a stress case: they trigger several times per
+second on noise, so the cascade switches nets far more often).
+
+Input (SURVEY 8(d)): SplitMix64 int16 noise in [-4096, 4095] per stream;
+every 4th stream instead replays python/test_wavs/{speech,galaxy,galaxy_s2i}.wav
+(tests/golden/test_wavs.npz) cyclically from offset (s*1601) mod 160000
+(--input noise: noise only).  Generated on the device before the timed region;
+nothing crosses PCIe inside it.
 
 A "step" is one chunk of --frames frames (default 100 = 1 s of audio) for
 every stream of the GPU's shard; streams carry their state across steps
-(continuous audio).  Input PCM is generated on the device (SplitMix64,
-oracle.synthetic_pcm) before the timed region; nothing crosses PCIe inside it.
+(continuous audio).
 
-Multi-GPU: one process per GPU (torch.distributed, RCCL backend); every rank
-owns its own shard of --streams streams (weak scaling, no data-path
-collective); value = all frames of all ranks / max over ranks of the timed
-wall time.
+Multi-GPU: one process per GPU (torch.distributed over RCCL, initialised
+whenever torch.distributed.run launched the process, world size 1 included);
+rank r owns a contiguous stream shard (nnsp_amd.shard.shard_streams; weak
+scaling: --streams per GPU, strong: --total-streams split), no data-path
+collective; value = frames of all ranks / max over ranks of the timed wall
+time.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from nnsp_amd.shard import dist_env, reduce_run, shard_streams  # noqa: E402
+
 # SURVEY 8(d): algorithmic work per frame (denominators of roofline.achieved)
 FE_MULS_PER_FRAME = 5912           # integer multiplies of one front-end frame
 NN_MACS_PER_INFERENCE = {"vad": 14616, "kws": 56448, "s2i": 72072}
 FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out (cascade: + 80, int32 log-Mel out)
+# NN per inference (one per 2 frames): the 2 new context frames in (cascade:
+# int32 log-Mel, 2 x 160 B) + per-frame outputs of its 2 frames (net, trigger,
+# outputs[3]: 2 x 9 B)
+NN_HBM_BYTES_PER_INFERENCE = 2 * 160 + 2 * 9
+SEED = 0x4E4E5350
+AMP = 4096
+STRONG_TOTAL = 262144              # BASELINE configs[4]: streams per node
 
 WORKLOADS = {  # BASELINE.json configs
     "cascade": "configs[4]: VAD->Hi-Galaxy KWS->S2I cascade, 32768 streams/GPU (262144 on 8 GPUs)",
@@ -42,103 +66,145 @@ WORKLOADS = {  # BASELINE.json configs
 }
 
 
-def cpu_baseline(net: str, acc32: bool, seconds: float = 1.5, procs: int | None = None) -> dict:
-    """Oracle ("port") timed on the host cores, one process per core (the
-    reference library is not re-entrant, so the reference scales by processes)."""
+# ---------------------------------------------------------------------------
+# CPU baseline: the oracle ("port"), one process per usable core
+# ---------------------------------------------------------------------------
+def host_cpu() -> dict:
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    host = os.cpu_count() or 1
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
+    quota = None
+    try:   # cgroup v2 CPU quota: the share of the host this job may use
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):   # the box exports the job's CPU share
+        if os.environ.get(k, "").isdigit():
+            quota = min(quota or 10**9, int(os.environ[k]))
+    if quota:
+        usable = min(usable, quota)
+    return {"model": model, "host_cores": host, "usable_cores": usable, "cgroup_or_env_quota": quota}
+
+
+def native_oracle() -> tuple[str | None, str]:
+    """Compile the oracle -O3 -march=native for the host it runs on (SURVEY
+    8(d)); the prebuilt -O3 build is the fallback."""
+    src = os.path.join(ROOT, "oracle", "nnsp_oracle.c")
+    out = os.path.join(tempfile.mkdtemp(prefix="nnsp_oracle_"), "liboracle_native.so")
+    try:
+        subprocess.run(["gcc", "-O3", "-march=native", "-fwrapv", "-fPIC", "-shared", "-o", out, src],
+                       check=True, capture_output=True, timeout=120)
+        return out, "gcc -O3 -march=native -fwrapv"
+    except Exception:
+        return None, "prebuilt oracle/liboracle.so (-O3; gcc -march=native build unavailable)"
+
+
+def cpu_baseline(net: str, acc32: bool, weights: str, mix: bool, seconds: float, procs: int | None = None) -> dict:
+    """The C oracle timed on the host cores, one process per core (the
+    reference library keeps global scratch and is not re-entrant, so it scales
+    by processes -- SURVEY 8(d))."""
     import multiprocessing as mp
 
-    procs = procs or min(16, os.cpu_count() or 1)
+    cpu = host_cpu()
+    procs = procs or cpu["usable_cores"]
+    lib, flags = native_oracle()
     with mp.get_context("fork").Pool(procs) as pool:
-        t0 = time.perf_counter()
-        res = pool.starmap(_cpu_worker, [(net, acc32, seconds, i) for i in range(procs)])
-        wall = time.perf_counter() - t0
-    frames = sum(res)
-    return {"value": frames / wall, "unit": "frames/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} processes x ~{seconds:.1f} s of continuous synthetic streams "
-                      f"(32 streams x 100-frame chunks each), {net} net, "
-                      f"{'32' if acc32 else '64'}b accumulator; C oracle -O3"}
+        res = pool.starmap(_cpu_worker, [(net, acc32, weights, mix, seconds, i, lib) for i in range(procs)])
+    rate = sum(f / t for f, t in res)   # the processes run concurrently: their rates add
+    return {"value": rate, "unit": "frames/s", "cores": procs, "kind": "port",
+            "cpu_model": cpu["model"], "host_cores": cpu["host_cores"], "quota": cpu["cgroup_or_env_quota"],
+            "build": flags,
+            "sample": f"{procs} concurrent processes x ~{seconds:.0f} s each of 32 continuous streams in 100-frame "
+                      f"chunks (the bench's input mix and weights, inputs generated before the timed loop), "
+                      f"{net}, {'32' if acc32 else '64'}b accumulator; value = sum of per-process frames / timed s"}
 
 
-def _cpu_worker(net: str, acc32: bool, seconds: float, idx: int) -> int:
+def _cpu_worker(net: str, acc32: bool, weights: str, mix: bool, seconds: float, idx: int,
+                lib: str | None) -> tuple[int, float]:
+    if lib:
+        os.environ["NNSP_ORACLE_LIB"] = lib
+    sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    from oracle import OracleCascade, OracleNet, synthetic_pcm
+    from oracle import OracleCascade, OracleNet, load_wavs, synthetic_pcm
 
-    from nnsp_amd.nets import synth_net
+    from nnsp_amd.nets import get_net
 
-    S, T = 32, 100
+    wavs = load_wavs() if mix else None
+    S, T, NC = 32, 100, 16
     if net == "cascade":
-        orc = OracleCascade({n: OracleNet(synth_net(n), acc32=acc32) for n in ("vad", "kws", "s2i")})
+        orc = OracleCascade({n: OracleNet(get_net(n, weights), acc32=acc32) for n in ("vad", "kws", "s2i")})
         st = orc.new_states(S)
         run = lambda pcm: orc.run(pcm, st)  # noqa: E731
     else:
-        orc = OracleNet(synth_net(net), acc32=acc32)
+        orc = OracleNet(get_net(net, weights), acc32=acc32)
         st = orc.new_states(S)
         run = lambda pcm: orc.run(pcm, st, want_logits=False, want_feats=False)  # noqa: E731
-    frames, t0, c = 0, time.perf_counter(), 0
+    chunks = [synthetic_pcm(S, T, SEED, t0=c * T, s0=idx * S, amp=AMP, wavs=wavs) for c in range(NC)]
+    frames, c = 0, 0
+    t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
-        run(synthetic_pcm(S, T, s0=idx * S, t0=c * T))
+        run(chunks[c % NC])
         frames += S * T
         c += 1
-    return frames
+    return frames, time.perf_counter() - t0
 
 
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--net", default="cascade", choices=sorted(WORKLOADS))
-    ap.add_argument("--streams", type=int, default=0,
-                    help="streams per GPU (default 32768 for the cascade, 8192 for one net)")
-    ap.add_argument("--window", type=int, default=-1, help="cascade frames per round (-1: library default)")
-    ap.add_argument("--frames", type=int, default=100, help="frames per step (chunk)")
-    ap.add_argument("--acc32", action="store_true")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=1.5)
-    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
-    args = ap.parse_args()
+# ---------------------------------------------------------------------------
+# GPU run
+# ---------------------------------------------------------------------------
+def make_engine(net: str, S: int, T: int, acc32: bool, weights: str, window: int):
+    from nnsp_amd.engine import NNSPBatch, NNSPCascade
+    from nnsp_amd.nets import get_net
 
+    if net == "cascade":
+        nets = {n: NNSPBatch(get_net(n, weights), S, T, acc32=acc32) for n in ("vad", "kws", "s2i")}
+        eng = NNSPCascade(nets)
+        if window >= 0:
+            eng.set_window(window)
+        return eng
+    return NNSPBatch(get_net(net, weights), S, T, acc32=acc32)
+
+
+def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
+    """Create, warm up and time one workload on this rank's shard."""
+    import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
-
     from nnsp_amd import _lib
-    from nnsp_amd.engine import NNSPBatch, device_info
 
-    _lib.check(_lib.lib().nnsp_set_device(local if world > 1 else 0), "set_device")
-    S = args.streams or (32768 if args.net == "cascade" else 8192)
     T, K, W = args.frames, args.steps, args.warmup
     cascade = args.net == "cascade"
-    if cascade:
-        from nnsp_amd.engine import NNSPCascade
-
-        nets = {n: NNSPBatch(n, S, T, acc32=args.acc32) for n in ("vad", "kws", "s2i")}
-        eng = NNSPCascade(nets)
-        if args.window >= 0:
-            eng.set_window(args.window)
-    else:
-        eng = NNSPBatch(args.net, S, T, acc32=args.acc32)
+    eng = make_engine(args.net, S, T, args.acc32, weights, args.window)
+    dwav = None
+    if args.input == "mix":
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        z = np.load(os.path.join(ROOT, "tests", "golden", "test_wavs.npz"))
+        wav = np.stack([z[k] for k in ("speech", "galaxy", "galaxy_s2i")])
+        dwav = torch.from_numpy(wav).to("cuda")
     # inputs resident in HBM before timing: one chunk buffer per step
     bufs = [torch.empty((S, T, 160), dtype=torch.int16, device="cuda") for _ in range(W + K)]
     for i, b in enumerate(bufs):
-        _lib.check(_lib.lib().nnsp_synth_pcm(b.data_ptr(), S, T, 0x4E4E5350, rank * S, i * T, 4096,
-                                             eng.stream), "synth_pcm")
+        _lib.check(_lib.lib().nnsp_synth_pcm_mix(b.data_ptr(), S, T, SEED, s0, i * T, AMP,
+                                                 dwav.data_ptr() if dwav is not None else None,
+                                                 3 if dwav is not None else 0, 160000, 4, eng.stream), "synth_pcm")
     trig = torch.empty((S, T), dtype=torch.int16, device="cuda")
     out3 = torch.empty((S, T, 3), dtype=torch.int16, device="cuda")
+    ran = torch.empty((S, T), dtype=torch.int8, device="cuda")
 
     def step(buf):
         if cascade:   # per frame: the NNSP_ID that ran, its trigger and outputs
-            eng.exec_device(buf.data_ptr(), T, None, trig.data_ptr(), out3.data_ptr())
+            eng.exec_device(buf.data_ptr(), T, ran.data_ptr(), trig.data_ptr(), out3.data_ptr())
         else:
             eng.exec_device(buf.data_ptr(), T, trig.data_ptr())
 
@@ -150,141 +216,220 @@ def main() -> None:
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    kt = {}            # kernel -> total ms over the timed steps
-    kframes = {}       # kernel -> frames (fe) or NN frames it processed
-    klaunch = {}       # kernel -> launches
-    rounds = 0
+    fe_ms, nn_ms, rounds, sched = 0.0, 0.0, 0, 0
     t0 = time.perf_counter()
     for i in range(K):
         step(bufs[W + i])
         if cascade:
-            r, _, _ = eng.last_stats()
+            r, f, _ = eng.last_stats()
             rounds += r
-            kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + eng.fe_stats()   # shared log-Mel, one launch
-            kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
-            klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + 1
-            for n in ("vad", "kws", "s2i"):
-                f, _, _, nl = eng.net_stats(n)   # per-net device times: instrumented step below
-                kframes[f"nn_{n}"] = kframes.get(f"nn_{n}", 0) + f
-                klaunch[f"nn_{n}"] = klaunch.get(f"nn_{n}", 0) + nl
+            sched += f
+            fe_ms += eng.fe_stats()       # shared log-Mel, one launch (HIP events on the cascade's stream)
         else:
-            f, n = eng.last_timing()   # syncs the stream: per-step kernel times
-            kt["fe_kernel"] = kt.get("fe_kernel", 0.0) + f
-            kt[f"nn_{args.net}"] = kt.get(f"nn_{args.net}", 0.0) + n
-            kframes["fe_kernel"] = kframes.get("fe_kernel", 0) + S * T
-            kframes[f"nn_{args.net}"] = kframes.get(f"nn_{args.net}", 0) + S * T
-            klaunch["fe_kernel"] = klaunch.get("fe_kernel", 0) + 1
-            klaunch[f"nn_{args.net}"] = klaunch.get(f"nn_{args.net}", 0) + 1
+            f, n = eng.last_timing()      # HIP events on the batch's stream around fe / proj+recur
+            fe_ms += f
+            nn_ms += n
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist:
         dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    net_ms = {}
+    out = {"elapsed": elapsed, "frames": S * T * K, "fe_ms": fe_ms / K, "S": S}
     if cascade:
-        # per-net device time per round (HIP events around each net's work):
-        # one extra, untimed chunk with the events on -- they cost a few
-        # percent, so the timed steps run without them.  The nets run
-        # concurrently on three streams: these spans overlap.
+        out["rounds_per_step"] = rounds / K
+        out["nn_frames_per_step"] = sched / K
+        # one extra, untimed chunk instrumented: the nets' work serialised on
+        # one stream with HIP events around each net's cold front end and NN
+        # kernels of every round (the events cost a few percent, and the
+        # timed steps run the nets concurrently on three streams)
+        eng.set_serial(True)
         eng.set_timing(True)
         step(bufs[W + K - 1])
         eng.sync()
         eng.set_timing(False)
-        rl, rfe, rnn = eng.round_stats()
-        net_ms["rounds"] = {"streams_listed": rl.tolist(),
-                            "cold_fe_ms": [[round(float(x), 4) for x in r] for r in rfe],
-                            "nn_ms": [[round(float(x), 4) for x in r] for r in rnn],
-                            "net_order": ["s2i", "vad", "kws"]}
-        for n in ("vad", "kws", "s2i"):
-            f, fe, nn, nl = eng.net_stats(n)
-            net_ms[n] = {"cold_fe_ms": fe, "nn_ms": nn, "frames": f, "rounds": nl}
-    frames = S * T * K * world
-    value = frames / elapsed
+        eng.set_serial(False)
+        out["instrumented"] = {n: dict(zip(("frames", "cold_fe_ms", "nn_ms", "rounds"), eng.net_stats(n)))
+                               for n in ("vad", "kws", "s2i")}
+        out["instrumented"]["shared_fe_ms"] = eng.fe_stats()
+        rl, _, _ = eng.round_stats()
+        out["streams_listed_per_round"] = rl.tolist()
+    else:
+        out["nn_ms"] = nn_ms / K
+    eng.close()
+    return out
 
+
+def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[dict, dict]:
+    """The dominant kernel's roofline and the NN's (SURVEY 8(d) per-unit work)."""
+    cu, clk = info["compute_units"], info["clock_khz"] * 1e3
+    valu_peak = cu * 128 * clk / 1e12          # VALU lane-ops/s (4 SIMDs x 32 lanes per clock per CU)
+    mul_peak, mul_src = valu_peak * 0.5, "half the VALU lane-op rate (no probe file)"
+    try:   # measured v_mul_hi_i32 issue rate (profiles/microbench/valu_rates.hip), scaled to this device
+        with open(os.path.join(ROOT, "profiles", "microbench", "valu_rates_mi355x.json")) as f:
+            vr = json.load(f)
+        mul_peak = vr["rates"]["v_mul_hi_i32"] / 1e12 * (cu * clk) / (vr["compute_units"] * vr["clock_khz"] * 1e3)
+        mul_src = "measured v_mul_hi_i32 issue rate, profiles/microbench/valu_rates_mi355x.json"
+    except Exception:
+        pass
+    mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
+    cascade = args.net == "cascade"
+    S, T = res["S"], args.frames
+    kern = (profile or {}).get("kernels", {})
+    # front end: one launch per step over all S*T frames (cascade: shared log-Mel)
+    fe_ms = res["fe_ms"]
+    fe_frames = S * T
+    fe_ach = fe_frames * FE_MULS_PER_FRAME / (fe_ms / 1e3) / 1e12
+    fe_traffic = kern.get("fe_kernel", {}).get("hbm_bytes_per_launch")
+    fe_alg = fe_frames * (FE_HBM_BYTES_PER_FRAME + (80 if cascade else 0))
+    fe = {"kernel": "fe_kernel", "bound": "valu", "achieved": fe_ach, "peak": mul_peak, "unit": "Tops/s",
+          "frac": fe_ach / mul_peak, "traffic": fe_traffic,
+          "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)",
+          "algorithmic_bytes_per_launch": fe_alg,
+          "work": "5912 integer multiplies per frame (SURVEY 8(d)) x frames per launch",
+          "peak_source": mul_src, "valu_lane_peak": valu_peak, "avg_launch_ms": fe_ms,
+          "frames_per_launch": fe_frames, "launches_per_step": 1,
+          "hbm_achieved_GBps": fe_alg / (fe_ms / 1e3) / 1e9, "hbm_peak_GBps": 8000.0}
+    # NN: MACs x 2 ops x inferences / the NN kernels' device time
+    if cascade:
+        ins = res["instrumented"]
+        nn_ms = sum(ins[n]["nn_ms"] for n in ("vad", "kws", "s2i"))
+        ops = sum(ins[n]["frames"] / 2 * NN_MACS_PER_INFERENCE[n] * 2 for n in ("vad", "kws", "s2i"))
+        inf = sum(ins[n]["frames"] for n in ("vad", "kws", "s2i")) / 2
+        how = ("one instrumented chunk, nets serialised on one stream, HIP events around each net's proj+recur "
+               "per round; inferences = frames scheduled / 2 (speculative work past a switch included)")
+        cold_ms = sum(ins[n]["cold_fe_ms"] for n in ("vad", "kws", "s2i"))
+    else:
+        nn_ms = res["nn_ms"]
+        inf = S * T / 2
+        ops = inf * NN_MACS_PER_INFERENCE[args.net] * 2
+        how = "HIP events around proj+recur on the batch's stream, every timed step"
+        cold_ms = 0.0
+    nn_ach = ops / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
+    nn_traffic = None
+    if kern:
+        nn_traffic = sum(v.get("hbm_bytes_per_step", 0) for k, v in kern.items()
+                         if k.startswith(("proj_kernel", "recur")))
+    nn = {"kernels": "proj_kernel + recur_pipe_kernel (all nets)", "bound": "mfma", "achieved": nn_ach,
+          "peak": mfma_peak, "unit": "Tops/s", "frac": nn_ach / mfma_peak, "ms_per_step": nn_ms,
+          "cold_fe_ms_per_step": cold_ms, "inferences_per_step": inf, "how": how,
+          "work": "int8xint16 MACs per inference (VAD 14616, KWS 56448, S2I 72072) x 2 ops",
+          "algorithmic_bytes_per_step": inf * NN_HBM_BYTES_PER_INFERENCE,
+          "traffic_bytes_per_step": nn_traffic or None,
+          "traffic_over_algorithmic": (nn_traffic / (inf * NN_HBM_BYTES_PER_INFERENCE)) if nn_traffic else None}
+    # the dominant kernel: the one with the larger device time per step
+    if nn_ms > fe_ms:
+        dom = {"kernel": nn["kernels"], "bound": "mfma", "achieved": nn_ach, "peak": mfma_peak, "unit": "Tops/s",
+               "frac": nn["frac"], "traffic": nn_traffic, "avg_launch_ms": nn_ms, "work": nn["work"]}
+        return dom, {"fe": fe, "nn": nn}
+    return fe, {"nn": nn}
+
+
+def load_profile(args, S: int, weights: str) -> dict | None:
+    try:
+        with open(args.profile_json) as f:
+            pj = json.load(f)
+    except Exception:
+        return None
+    if (pj.get("workload") == args.net and pj.get("streams") == S and pj.get("frames") == args.frames
+            and pj.get("weights", "synth") == weights and pj.get("input", "noise") == args.input):
+        return pj
+    return None
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--net", default="cascade", choices=sorted(WORKLOADS))
+    ap.add_argument("--streams", type=int, default=0,
+                    help="streams per GPU (weak scaling; default 32768 for the cascade, 8192 for one net)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="strong: --total-streams split over the ranks")
+    ap.add_argument("--total-streams", type=int, default=STRONG_TOTAL)
+    ap.add_argument("--window", type=int, default=-1, help="cascade frames per round (-1: library default)")
+    ap.add_argument("--frames", type=int, default=100, help="frames per step (chunk)")
+    ap.add_argument("--acc32", action="store_true")
+    ap.add_argument("--weights", default="ref", choices=["ref", "synth"])
+    ap.add_argument("--input", default="mix", choices=["mix", "noise"])
+    ap.add_argument("--no-stress", action="store_true",
+                    help="skip the second cascade line on synthetic weights (N=1 only)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    args = ap.parse_args()
+
+    rank, world, local, launched = dist_env()
+    import torch
+
+    dist = None
+    torch.cuda.set_device(local if launched else 0)
+    if launched:   # torch.distributed.run: RCCL process group, world size 1 included
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from nnsp_amd import _lib
+    from nnsp_amd.engine import device_info
+
+    _lib.check(_lib.lib().nnsp_set_device(local if launched else 0), "set_device")
+    if args.scaling == "weak":
+        per = args.streams or (32768 if args.net == "cascade" else 8192)
+        s0, S = shard_streams(rank, world, per_rank=per)
+    else:
+        s0, S = shard_streams(rank, world, total=args.total_streams)
+    res = run_workload(args, S, s0, args.weights, dist)
+    elapsed, frames = reduce_run(dist, res["elapsed"], res["frames"], device="cuda")
+    stress = None
+    if args.net == "cascade" and world == 1 and not args.no_stress and args.weights == "ref":
+        r2 = run_workload(args, S, s0, "synth")
+        stress = {"weights": "synth", "value": r2["frames"] / r2["elapsed"],
+                  "ms_per_step": r2["elapsed"] / args.steps * 1e3, "rounds_per_step": r2["rounds_per_step"],
+                  "speculation_overhead": r2["nn_frames_per_step"] / (S * args.frames) - 1.0,
+                  "shared_fe_ms": r2["fe_ms"],
+                  "nn_ms": {n: r2["instrumented"][n]["nn_ms"] for n in ("vad", "kws", "s2i")}}
     if rank == 0:
         info = device_info()
-        cu, clk = info["compute_units"], info["clock_khz"] * 1e3
-        valu_peak = cu * 128 * clk / 1e12          # VALU lane-ops/s (4 SIMDs x 32 lanes per clock per CU)
-        # integer multiplies issue at about half the add rate on gfx950: the
-        # front end's ceiling is the measured v_mul_hi_i32 rate on all CUs
-        # (profiles/microbench/valu_rates.hip, run on MI355X), scaled to this device
-        mul_peak, mul_src = valu_peak * 0.5, "half the VALU lane-op rate (no probe file)"
-        try:
-            with open(os.path.join(ROOT, "profiles", "microbench", "valu_rates_mi355x.json")) as f:
-                vr = json.load(f)
-            mul_peak = vr["rates"]["v_mul_hi_i32"] / 1e12 * (cu * clk) / (vr["compute_units"] * vr["clock_khz"] * 1e3)
-            mul_src = "measured v_mul_hi_i32 issue rate, profiles/microbench/valu_rates_mi355x.json"
-        except Exception:
-            pass
-        mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
-        # dominant kernel by device time.  In the cascade the nets' segment
-        # kernels run concurrently on three streams, so their event spans are
-        # not kernel durations; the one-launch shared front end is the largest
-        # kernel there (profiles/*/kernel_stats.csv)
-        dom = "fe_kernel" if cascade else max(kt, key=kt.get)
-        launches = klaunch[dom]
-        avg_launch_s = kt[dom] / 1e3 / launches    # HIP-event time on the engine's stream
-        units = kframes[dom] / launches            # frames per launch
-        if dom == "fe_kernel":
-            per_unit = FE_MULS_PER_FRAME
-            work = "integer multiplies (SURVEY 8(d): 5912 per frame) x frames per launch"
-            peak, bound = mul_peak, "valu"
-        else:
-            n = dom[3:]
-            per_unit = NN_MACS_PER_INFERENCE[n]    # one inference per 2 frames, 2 ops per MAC
-            work = f"{n} int8xint16 MACs x2 ops x inferences (frames/2) per launch"
-            peak, bound = mfma_peak, "mfma"
-        achieved = units * per_unit / avg_launch_s / 1e12
-        traffic = None
-        try:
-            with open(args.profile_json) as f:
-                pj = json.load(f)
-            if pj.get("workload") == args.net and pj.get("streams") == S and pj.get("frames") == T:
-                traffic = pj["kernels"][dom]["hbm_bytes_per_launch"]
-        except Exception:
-            pass
-        fe_s = kt["fe_kernel"] / 1e3
+        dom, extra = roofline_blocks(args, res, info, load_profile(args, S, args.weights))
+        value = frames / elapsed
         out = {
             "metric": "audio frames/sec (16 kHz, 10 ms hop) per node; bit-exact vs ref",
             "value": value,
             "unit": "frames/s",
             "n_gpus": world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": elapsed / K * 1e3,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "int32 (int16 PCM, q31 FFT, int8xint16 MACs)",
-            "data": "synthetic SplitMix64 int16 PCM generated on device; seeded synthetic weights of the reference net shapes",
+            "data": ("synthetic int16 PCM generated on device (SplitMix64 noise; every 4th stream replays the "
+                     "reference's python/test_wavs)" if args.input == "mix" else
+                     "synthetic SplitMix64 int16 PCM generated on device") +
+                    ("; the reference's own def_nn*.c weights" if args.weights == "ref" else
+                     "; seeded synthetic weights of the reference net shapes"),
             "config": {"workload": WORKLOADS[args.net], "net": args.net, "streams_per_gpu": S,
-                       "frames_per_step": T, "accumulator": "32b" if args.acc32 else "64b",
-                       "parallelism": f"stream shards x{world}"},
-            "kernels_ms_per_step": {k: v / K for k, v in kt.items()},
-            **({"nets_one_chunk": net_ms} if cascade else {}),
-            "frames_scheduled_per_step": {k: v // K for k, v in kframes.items()},
-            "roofline": {"kernel": dom, "bound": bound,
-                         "achieved": achieved, "peak": peak, "unit": "Tops/s",
-                         "frac": achieved / peak, "work": work,
-                         "peak_source": mul_src if dom == "fe_kernel" else "dense int8 MFMA (MI355X_MICROARCH.md)",
-                         "valu_lane_peak": valu_peak,
-                         "traffic": traffic, "traffic_unit": "HBM bytes per launch (PMC, profiles/)",
-                         "launches_per_step": launches / K, "avg_launch_ms": avg_launch_s * 1e3,
-                         "frames_per_launch": units,
-                         "hbm_achieved_GBps": kframes["fe_kernel"] * (FE_HBM_BYTES_PER_FRAME + (80 if cascade else 0))
-                         / fe_s / 1e9,
-                         "hbm_peak_GBps": 8000.0},
+                       "streams_total": S * world if args.scaling == "weak" else args.total_streams,
+                       "frames_per_step": args.frames, "accumulator": "32b" if args.acc32 else "64b",
+                       "weights": args.weights, "input": args.input,
+                       "parallelism": f"stream shards x{world}" + (" (RCCL process group)" if dist else "")},
+            "roofline": dom,
+            **{f"roofline_{k}": v for k, v in extra.items()},
+            "fe_ms_per_step": res["fe_ms"],
             "device": info,
         }
-        if cascade:
-            out["cascade"] = {"rounds_per_step": rounds / K,
-                              "speculation_overhead": sum(kframes[f"nn_{n}"] for n in ("vad", "kws", "s2i"))
-                              / (S * T * K) - 1.0}
+        if args.net == "cascade":
+            out["cascade"] = {"rounds_per_step": res["rounds_per_step"],
+                              "speculation_overhead": res["nn_frames_per_step"] / (S * args.frames) - 1.0,
+                              "instrumented_chunk": res["instrumented"],
+                              "streams_listed_per_round": res["streams_listed_per_round"]}
+            if stress:
+                out["cascade_synthetic_weights"] = stress
+        else:
+            out["nn_ms_per_step"] = res["nn_ms"]
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.net, args.acc32, args.cpu_seconds)
+            out["cpu_baseline"] = cpu_baseline(args.net, args.acc32, args.weights, args.input == "mix",
+                                               args.cpu_seconds)
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

@@ -222,6 +222,15 @@ int32_t ceiling(int32_t input);
 void binary_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger);
 void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger);
 
+/* Error channel of this library's single-stream API (not in the reference,
+ * whose functions return 0 or void).  A HIP or allocation failure inside any
+ * call above makes that call return without touching its outputs (int
+ * results: the error code, pointer results: NULL) and records the first such
+ * error: nnsp_legacy_status() returns it (0: none; nnsp_strerror() describes
+ * it) until nnsp_legacy_clear().  The process is never aborted. */
+int nnsp_legacy_status(void);
+void nnsp_legacy_clear(void);
+
 #ifdef __cplusplus
 }
 #endif

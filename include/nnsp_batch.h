@@ -15,9 +15,10 @@
  * a device image); the LSTM state arrays it points to are not used by a batch.
  *
  * Layouts: pcm [S][T][160] int16 (stream-major chunk); trig [S][T] int16 =
- * NNSPClass_exec's return per frame; logits [S][T][nout] int32 written on the
- * frames where the NN ran (slides == 1), before post-processing overwrites them
- * (trap T7); features [S][T][40] int16 = normFeatContext slot 5 per frame.
+ * NNSPClass_exec's return per frame; logits [S][T][nout] int32 = the NN output
+ * on the frames where the NN ran (slides == 1), before post-processing
+ * overwrites it (trap T7), and 0 on the other frames; features [S][T][40]
+ * int16 = normFeatContext slot 5 per frame.
  */
 #ifndef NNSP_BATCH_H
 #define NNSP_BATCH_H
@@ -81,6 +82,12 @@ int nnsp_batch_set_state(nnsp_batch *b, const void *host, int first, int count);
  * SplitMix64(seed, stream s0+s, sample t0*160+n) -> int16 in [-amp, amp-1]. */
 int nnsp_synth_pcm(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp,
                    void *stream);
+/* The same with recordings mixed in: stream g = s0 + s with
+ * g % every == 0 replays dev_wavs[(g / every) % n_wavs][0 .. wav_len) (device
+ * memory, n_wavs x wav_len int16) cyclically from sample offset
+ * (g * 1601) % wav_len; the others are SplitMix64 as above. */
+int nnsp_synth_pcm_mix(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp,
+                       const int16_t *dev_wavs, int n_wavs, int wav_len, int every, void *stream);
 
 /* Device selection / info (thin wrappers over the HIP runtime). */
 int nnsp_device_count(int *n);

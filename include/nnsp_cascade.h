@@ -54,8 +54,11 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask);
 /* One chunk of T frames: pcm [S][T][160] int16.  Outputs per frame (NULL
  * skips): net_ran [S][T] int8 = NNSP_ID that ran, detected [S][T] int16 = its
  * NNSPClass_exec return, outputs3 [S][T][3] int16 = its NNSPClass.outputs.
- * _device: device pointers, asynchronous on nnsp_cascade_stream (it blocks on
- * the host only for the per-round list lengths). */
+ * _device: device pointers, work on nnsp_cascade_stream and the three net
+ * streams forked from it.  The call returns once the chunk's rounds have
+ * finished on the device: the host reads back the list lengths of the round
+ * after the last one it launched to decide whether more rounds are needed, so
+ * it cannot queue the next chunk while this one runs. */
 int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
                       int16_t *detected, int16_t *outputs3);
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
@@ -78,6 +81,13 @@ int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run,
  * cost a few percent of throughput (environment NNSP_CASCADE_TIMING=1 turns
  * it on at create time). */
 int nnsp_cascade_set_timing(nnsp_cascade *c, int on);
+
+/* Instrumentation: on = the three nets' work of each round runs one net after
+ * the other on the cascade's own stream instead of concurrently on three
+ * forked streams (environment NNSP_CASCADE_SERIAL at create time).  With timing
+ * on, the per-net event spans then time each net's kernels alone.  Results do
+ * not depend on it. */
+int nnsp_cascade_set_serial(nnsp_cascade *c, int on);
 
 /* Last chunk, one net (NNSP_ID): frames scheduled on it, the device time of
  * the front end of the frames right after its resets and of its NN kernels

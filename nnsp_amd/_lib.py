@@ -112,6 +112,7 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_sync": (I, [P]),
         "nnsp_cascade_set_window": (I, [P, I]),
         "nnsp_cascade_set_timing": (I, [P, I]),
+        "nnsp_cascade_set_serial": (I, [P, I]),
         "nnsp_cascade_stream": (P, [P]),
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),
@@ -120,6 +121,7 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_last_net_stats": (I, [P, I, C.POINTER(C.c_longlong), C.POINTER(C.c_float),
                                             C.POINTER(C.c_float), C.POINTER(I)]),
         "nnsp_synth_pcm": (I, [P, I, I, C.c_uint64, I, C.c_int64, I, P]),
+        "nnsp_synth_pcm_mix": (I, [P, I, I, C.c_uint64, I, C.c_int64, I, P, I, I, I, P]),
         "nnsp_device_count": (I, [C.POINTER(I)]),
         "nnsp_set_device": (I, [I]),
         "nnsp_device_info": (I, [C.POINTER(I), C.POINTER(I), C.c_char_p, I]),

@@ -170,6 +170,7 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     *out = b;
     b->S = n_streams;
     b->Tmax = max_frames;
+    b->nn_id = nn_id;
     b->out_linear = out_linear;
     b->norm_shift = 30 - net->qbit_input[0]; /* FeatureClass qbit_output, nn_speech.c:40-44 */
     int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count);
@@ -372,6 +373,8 @@ int nnsp_batch_exec_device(nnsp_batch *b, const int16_t *pcm, int T, int16_t *tr
         nnsp_set_error("nnsp_batch_exec: T must be in 1..%d", b ? b->Tmax : 0);
         return NNSP_EINVAL;
     }
+    /* logits rows of frames without an NN step are defined as 0 */
+    if (logits) TRY(nnspk_memset(logits, 0, (size_t)b->S * T * b->nout * 4, b->stream));
     TRY(nnsp_batch_run(b, pcm, T, trig, logits, NULL, b->stream, 1));
     b->last_T = T;
     return 0;
@@ -471,5 +474,15 @@ int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
 int nnsp_synth_pcm(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp, void *stream)
 {
     if (!dev_out || S <= 0 || T <= 0 || amp <= 0) return NNSP_EINVAL;
-    return nnspk_launch_synth_pcm(dev_out, S, T, (unsigned long long)seed, s0, (long long)t0, amp, stream);
+    return nnspk_launch_synth_pcm(dev_out, S, T, (unsigned long long)seed, s0, (long long)t0, amp, NULL, 0, 0, 0,
+                                  stream);
+}
+
+int nnsp_synth_pcm_mix(int16_t *dev_out, int S, int T, uint64_t seed, int s0, int64_t t0, int amp,
+                       const int16_t *dev_wavs, int n_wavs, int wav_len, int every, void *stream)
+{
+    if (!dev_out || S <= 0 || T <= 0 || amp <= 0 || (dev_wavs && (n_wavs <= 0 || wav_len <= 0 || every <= 0)))
+        return NNSP_EINVAL;
+    return nnspk_launch_synth_pcm(dev_out, S, T, (unsigned long long)seed, s0, (long long)t0, amp, dev_wavs, n_wavs,
+                                  wav_len, every, stream);
 }

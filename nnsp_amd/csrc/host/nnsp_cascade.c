@@ -95,6 +95,11 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             nnsp_set_error("nnsp_cascade_create: three nets of the same stream count required");
             return NNSP_EINVAL;
         }
+        if (nets[i]->nn_id != i) {
+            nnsp_set_error("nnsp_cascade_create: nets[%d] was created with NNSP_ID %d (nets[] is indexed by NNSP_ID: "
+                           "0 s2i, 1 vad, 2 kws)", i, nets[i]->nn_id);
+            return NNSP_EINVAL;
+        }
         if (!nets[i]->fast) {
             nnsp_set_error("nnsp_cascade_create: net %d has no split NN path (one LSTM layer)", i);
             return NNSP_EUNSUPPORTED;
@@ -220,8 +225,9 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
         /* the controller runs inside the nets' pipelined recur kernels when all
          * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
-         * casc_control launch per round instead) */
-        c->fused = !c->serial && getenv("NNSP_CASCADE_CONTROL_KERNEL") == NULL;
+         * casc_control launch per round instead).  Serial mode keeps it: the
+         * cross-net event waits are then waits on the same stream. */
+        c->fused = getenv("NNSP_CASCADE_CONTROL_KERNEL") == NULL;
         for (int i = 0; i < 3; ++i)
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
@@ -516,6 +522,14 @@ int nnsp_cascade_set_timing(nnsp_cascade *c, int on)
 {
     if (!c) return NNSP_EINVAL;
     c->timing = on != 0;
+    return 0;
+}
+
+int nnsp_cascade_set_serial(nnsp_cascade *c, int on)
+{
+    if (!c) return NNSP_EINVAL;
+    TRY(nnspk_sync(c->stream));
+    c->serial = on != 0;
     return 0;
 }
 

@@ -46,6 +46,7 @@ int nnsp_act_of(void *(*fn)(void *, int32_t *, int));
 /* the batch engine's internals, shared with the cascade (nnsp_cascade.c) */
 struct nnsp_batch {
     int S, Tmax, nout, out_linear, norm_shift;
+    int nn_id;                        /* NNSP_ID given at create (post-processing kind) */
     nnsp_image im;
     void *stream;
     void *ev[3];

@@ -14,6 +14,7 @@
  * sigmoid_fix / relu6_fix / linear_fix double as the layer / activation tags
  * that def_nn*.c store in NeuralNetClass and that nnsp_image.c reads.
  */
+#include <setjmp.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,13 +23,38 @@
 
 /* ---------------------------------------------------------------------------
  * per-process GPU context: one HIP stream + a bump-allocated scratch arena
+ * that grows on demand (a call that needs more scratch gets a larger arena;
+ * the old one is freed at the start of the next call, once nothing in flight
+ * uses it), and the sticky error of the last failed call
  * ------------------------------------------------------------------------- */
 static struct {
     void *stream;
-    uint8_t *arena;
+    uint8_t *arena, *retired;
     size_t cap, used;
     int ready;
+    int depth;   /* nesting of public entry points (the outermost holds jb) */
+    jmp_buf jb;
+    int sticky;  /* first error since nnsp_legacy_clear(); 0 = none */
 } G;
+
+static void fail(int code, const char *what)
+{
+    if (!G.sticky) G.sticky = code;
+    nnsp_set_error("libnnsp_mi355x (legacy API): %s failed: %s", what,
+                   code > 0 ? nnspk_error_string(code) : (code == NNSP_ENOMEM ? "out of memory" : "invalid argument"));
+    fprintf(stderr, "%s\n", nnsp_last_error());
+    if (G.depth > 0) longjmp(G.jb, 1);
+    abort(); /* unreachable: every GPU path runs inside a public entry point */
+}
+
+#define CK(x)                     \
+    do {                          \
+        int _e = (x);             \
+        if (_e) fail(_e, #x);     \
+    } while (0)
+
+int nnsp_legacy_status(void) { return G.sticky; }
+void nnsp_legacy_clear(void) { G.sticky = 0; }
 
 static int gctx(void)
 {
@@ -44,32 +70,41 @@ static int gctx(void)
 static void *dscratch(size_t n)
 {
     n = (n + 255) & ~(size_t)255;
-    if (G.used + n > G.cap) return NULL;
+    if (G.used + n > G.cap) {
+        /* grow: pointers handed out earlier in this call stay valid (the old
+         * arena is retired, freed by the next begin()) */
+        size_t cap = G.cap * 2;
+        while (cap < n) cap *= 2;
+        uint8_t *a = NULL;
+        CK(nnspk_malloc((void **)&a, cap));
+        if (G.retired) {   /* a second growth in one call: keep the older arena alive too */
+            CK(nnspk_sync(G.stream));
+            nnspk_free(G.retired);
+        }
+        G.retired = G.arena;
+        G.arena = a;
+        G.cap = cap;
+        G.used = 0;
+    }
     void *p = G.arena + G.used;
     G.used += n;
     return p;
 }
-
-#define CK(x)                                                                           \
-    do {                                                                                \
-        int _e = (x);                                                                   \
-        if (_e) {                                                                       \
-            fprintf(stderr, "libnnsp_mi355x: %s failed: %s\n", #x, nnsp_strerror(_e)); \
-            abort();                                                                    \
-        }                                                                               \
-    } while (0)
 
 const char *nnsp_strerror(int code);
 
 static void begin(void)
 {
     CK(gctx());
+    if (G.retired) { /* the previous call synchronised: nothing uses it any more */
+        nnspk_free(G.retired);
+        G.retired = NULL;
+    }
     G.used = 0;
 }
 static void *up(const void *h, size_t n)
 {
     void *d = dscratch(n);
-    if (!d) CK(NNSP_ENOMEM);
     if (h) CK(nnspk_h2d(d, h, n, G.stream));
     else CK(nnspk_memset(d, 0, n, G.stream));
     return d;
@@ -78,47 +113,97 @@ static void down(void *h, const void *d, size_t n) { CK(nnspk_d2h(h, d, n, G.str
 static void fin(void) { CK(nnspk_sync(G.stream)); }
 
 /* ---------------------------------------------------------------------------
- * net image cache (keyed by NeuralNetClass* or by a single-layer call site)
+ * device image cache.  An image is keyed by the tables' addresses, the layer
+ * description and a 64-bit FNV-1a hash of the weight, recurrent-weight and
+ * bias BYTES, so tables changed in place or rebuilt at reused addresses get a
+ * new image (the reference reads its tables on every call).  Most recently
+ * used first; at most IMG_MAX images, the least recently used freed.
  * ------------------------------------------------------------------------- */
+#define IMG_MAX 32
 typedef struct img_node {
     struct img_node *next;
     const void *key[4];
     int ikey[8];
+    uint64_t bytes;
     nnsp_image im;
     int out_linear;
 } img_node;
 static img_node *g_imgs;
 
-static img_node *img_find(const void *k0, const void *k1, const void *k2, const void *k3,
-                          const int *ik)
+static uint64_t fnv(uint64_t h, const void *p, size_t n)
 {
-    for (img_node *n = g_imgs; n; n = n->next)
+    const uint8_t *b = (const uint8_t *)p;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ULL;
+    }
+    return h;
+}
+
+static uint64_t layer_bytes_hash(uint64_t h, const nnsp_layer_desc *d)
+{
+    const size_t rows = (size_t)(d->type == NN_LSTM ? 4 * d->N : d->N);
+    if (d->W) h = fnv(h, d->W, rows * (size_t)d->K);
+    if (d->Wr) h = fnv(h, d->Wr, rows * (size_t)d->N);
+    if (d->B) h = fnv(h, d->B, rows * 2);
+    return h;
+}
+
+static img_node *img_find(const void *k0, const void *k1, const void *k2, const void *k3, const int *ik,
+                          uint64_t bytes)
+{
+    img_node *prev = NULL;
+    for (img_node *n = g_imgs; n; prev = n, n = n->next)
         if (n->key[0] == k0 && n->key[1] == k1 && n->key[2] == k2 && n->key[3] == k3 &&
-            !memcmp(n->ikey, ik, sizeof n->ikey))
+            !memcmp(n->ikey, ik, sizeof n->ikey) && n->bytes == bytes) {
+            if (prev) { /* move to the front */
+                prev->next = n->next;
+                n->next = g_imgs;
+                g_imgs = n;
+            }
             return n;
+        }
     return NULL;
 }
 
-static img_node *img_add(const void *k0, const void *k1, const void *k2, const void *k3,
-                         const int *ik, const nnsp_layer_desc *L, int nl, int out_linear)
+static img_node *img_add(const void *k0, const void *k1, const void *k2, const void *k3, const int *ik,
+                         uint64_t bytes, const nnsp_layer_desc *L, int nl, int out_linear)
 {
+    int count = 0;
+    img_node *last = NULL, *before_last = NULL;
+    for (img_node *n = g_imgs; n; n = n->next) {
+        ++count;
+        before_last = last;
+        last = n;
+    }
+    if (count >= IMG_MAX && last) { /* evict the least recently used (nothing in flight uses it) */
+        CK(nnspk_sync(G.stream));
+        if (before_last) before_last->next = NULL;
+        else g_imgs = NULL;
+        nnsp_image_free(&last->im);
+        free(last);
+    }
     img_node *n = (img_node *)calloc(1, sizeof *n);
-    if (!n) CK(NNSP_ENOMEM);
+    if (!n) fail(NNSP_ENOMEM, "image cache entry");
     n->key[0] = k0; n->key[1] = k1; n->key[2] = k2; n->key[3] = k3;
     memcpy(n->ikey, ik, sizeof n->ikey);
-    CK(nnsp_image_build(&n->im, L, nl, 0, 0, 0));
-    CK(nnsp_image_upload(&n->im, G.stream));
+    n->bytes = bytes;
+    int e = nnsp_image_build(&n->im, L, nl, 0, 0, 0);
+    if (!e) e = nnsp_image_upload(&n->im, G.stream);
+    if (e) {
+        nnsp_image_free(&n->im);
+        free(n);
+        fail(e, "nnsp_image_build/upload");
+    }
     n->out_linear = out_linear;
     n->next = g_imgs;
     g_imgs = n;
     return n;
 }
 
-/* A NeuralNetClass's device image is cached by everything that defines the
- * net -- its address, and a hash of its shape, qbits, layer / activation
- * functions and weight / bias / state table pointers (the weight tables are
- * const data in def_nn*.c) -- so a struct rebuilt at a reused address with
- * other tables gets its own image. */
+/* A NeuralNetClass's device image: keyed by its address, a hash of its shape,
+ * qbits, layer / activation functions and table pointers, and the hash of
+ * its tables' bytes. */
 static img_node *net_image(const NeuralNetClass *net)
 {
     uint64_t h = 1469598103934665603ULL;
@@ -135,13 +220,15 @@ static img_node *net_image(const NeuralNetClass *net)
         MIX(net->pt_kernel_rec[i]);
     }
 #undef MIX
-    const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
-    img_node *n = img_find(net, NULL, NULL, NULL, ik);
-    if (n) return n;
     nnsp_layer_desc L[NN_MAX_LAYERS];
     int nl = 0, lin = 0;
     CK(nnsp_describe_net(net, L, &nl, &lin));
-    return img_add(net, NULL, NULL, NULL, ik, L, nl, lin);
+    uint64_t bytes = 1469598103934665603ULL;
+    for (int i = 0; i < nl; ++i) bytes = layer_bytes_hash(bytes, &L[i]);
+    const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
+    img_node *n = img_find(net, NULL, NULL, NULL, ik, bytes);
+    if (n) return n;
+    return img_add(net, NULL, NULL, NULL, ik, bytes, L, nl, lin);
 }
 
 /* LSTM h/c of a NeuralNetClass <-> device rows [l][NN_MAX_W] */
@@ -195,10 +282,10 @@ static void *act_call(int type, int32_t *x, void *y, int len)
     fin();
     return (char *)y + ob;
 }
-void *relu6_fix(int16_t *y, int32_t *x, int len) { return act_call(0, x, y, len); }
-void *tanh_fix(int16_t *y, int32_t *x, int len) { return act_call(1, x, y, len); }
-void *sigmoid_fix(int16_t *y, int32_t *x, int len) { return act_call(2, x, y, len); }
-void *linear_fix(int32_t *y, int32_t *x, int len) { return act_call(3, x, y, len); }
+static void *relu6_fix_impl(int16_t *y, int32_t *x, int len) { return act_call(0, x, y, len); }
+static void *tanh_fix_impl(int16_t *y, int32_t *x, int len) { return act_call(1, x, y, len); }
+static void *sigmoid_fix_impl(int16_t *y, int32_t *x, int len) { return act_call(2, x, y, len); }
+static void *linear_fix_impl(int32_t *y, int32_t *x, int len) { return act_call(3, x, y, len); }
 
 /* ---------------------------------------------------------------------------
  * layers (affine.c:409-490, lstm.c:15-214) -- single-layer images
@@ -223,8 +310,9 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
         return -1;
     }
     const int ik[8] = {type, acc32, dim_output, dim_input, qk, qb, qi, (qir << 4) | d.act};
-    img_node *n = img_find(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik);
-    if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, &d, 1, d.act == 3);
+    const uint64_t bytes = layer_bytes_hash(1469598103934665603ULL, &d);
+    img_node *n = img_find(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes);
+    if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes, &d, 1, d.act == 3);
     int16_t in_pad[NN_MAX_K];
     memset(in_pad, 0, sizeof in_pad);
     memcpy(in_pad, input, (size_t)dim_input * 2);
@@ -258,7 +346,7 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
     return 0;
 }
 
-int fc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+static int fc_8x16_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
             int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
             int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
             int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
@@ -269,7 +357,7 @@ int fc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *
                      dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
 }
 
-int fc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+static int fc_8x16_acc32b_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
                    int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
                    int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
                    int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
@@ -280,7 +368,7 @@ int fc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, in
                      dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
 }
 
-int lstm_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+static int lstm_8x16_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
               int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
               int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
               int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
@@ -291,7 +379,7 @@ int lstm_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t
                      dim_output, dim_input, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, NULL);
 }
 
-int lstm_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+static int lstm_8x16_acc32b_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
                      int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
                      int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
                      int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
@@ -316,7 +404,7 @@ void NeuralNetClass_setDefault(NeuralNetClass *pt_inst)
         }
 }
 
-void NeuralNetClass_exe(NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer)
+static void NeuralNetClass_exe_impl(NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer)
 {
     const int nl = debug_layer < 0 ? pt_inst->numlayers : debug_layer;
     if (nl == 0) { /* neural_nets.c:85-91: copy the input through */
@@ -365,7 +453,7 @@ int stftModule_setDefault(stftModule *ps) /* :25-31 */
 
 void arm_fft_init(void) { /* twiddles are compile-time tables; nothing to build */ }
 
-void arm_fft_exec(int32_t *y, int32_t *x) /* fft_arm.c:16-20 -> arm_rfft_q31 */
+static void arm_fft_exec_impl(int32_t *y, int32_t *x) /* fft_arm.c:16-20 -> arm_rfft_q31 */
 {
     begin();
     int32_t *dx = (int32_t *)up(x, 512 * 4);
@@ -400,7 +488,7 @@ static void fe_frame(const int16_t *tail, const int16_t *pcm, const int32_t *mea
     fin();
 }
 
-int stftModule_analyze_arm(void *ps_, int16_t *x, int32_t *y) /* :94-124 */
+static int stftModule_analyze_arm_impl(void *ps_, int16_t *x, int32_t *y) /* :94-124 */
 {
     stftModule *ps = (stftModule *)ps_;
     int16_t tail[320];
@@ -411,7 +499,7 @@ int stftModule_analyze_arm(void *ps_, int16_t *x, int32_t *y) /* :94-124 */
     return 0;
 }
 
-void spec2pspec_arm(int32_t *y, int32_t *x, int len) /* :79-92 */
+static void spec2pspec_arm_impl(int32_t *y, int32_t *x, int len) /* :79-92 */
 {
     if (len <= 0) return;
     begin();
@@ -422,7 +510,7 @@ void spec2pspec_arm(int32_t *y, int32_t *x, int len) /* :79-92 */
     fin();
 }
 
-void melSpecProc(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
+static void melSpecProc_impl(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
 {
     begin();
     int32_t *ds = (int32_t *)up(specs, 257 * 4);
@@ -432,7 +520,7 @@ void melSpecProc(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
     fin();
 }
 
-void norm_oneTwo(int32_t x, int32_t *y, int8_t *shift) /* fixlog10.c:9-28 */
+static void norm_oneTwo_impl(int32_t x, int32_t *y, int8_t *shift) /* fixlog10.c:9-28 */
 {
     begin();
     int32_t *dx = (int32_t *)up(&x, 4);
@@ -445,7 +533,7 @@ void norm_oneTwo(int32_t x, int32_t *y, int8_t *shift) /* fixlog10.c:9-28 */
     *shift = (int8_t)o[1];
 }
 
-void log10_vec(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in) /* :53-61 */
+static void log10_vec_impl(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in) /* :53-61 */
 {
     if (len <= 0) return;
     begin();
@@ -456,7 +544,7 @@ void log10_vec(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in) /* :5
     fin();
 }
 
-void my_log10(int32_t *out, int32_t x) { log10_vec(out, &x, 1, 15); } /* :31-50 */
+static void my_log10_impl(int32_t *out, int32_t x) { log10_vec(out, &x, 1, 15); } /* :31-50 */
 
 void FeatureClass_construct(FeatureClass *ps, const int32_t *norm_mean, const int32_t *norm_stdR,
                             int8_t qbit_output) /* feature_module.c:12-24 */
@@ -469,7 +557,7 @@ void FeatureClass_construct(FeatureClass *ps, const int32_t *norm_mean, const in
     ps->qbit_output = qbit_output;
 }
 
-void FeatureClass_setDefault(FeatureClass *ps) /* :26-45 */
+static void FeatureClass_setDefault_impl(FeatureClass *ps) /* :26-45 */
 {
     stftModule_setDefault(&ps->state_stftModule);
     begin();
@@ -484,7 +572,7 @@ void FeatureClass_setDefault(FeatureClass *ps) /* :26-45 */
     for (int j = 0; j < NUM_FEATURE_CONTEXT - 1; ++j) memcpy(ps->normFeatContext + 40 * j, p5, 80);
 }
 
-void FeatureClass_execute(FeatureClass *ps, int16_t *input) /* :47-74 */
+static void FeatureClass_execute_impl(FeatureClass *ps, int16_t *input) /* :47-74 */
 {
     int16_t tail[320], f5[40];
     memcpy(tail, ps->state_stftModule.dataBuffer + 160, sizeof tail);
@@ -513,7 +601,7 @@ int NNSPClass_init(NNSPClass *pt_inst, void *pt_net, void *pt_feat, char nn_id, 
     return 0;
 }
 
-int NNSPClass_reset(NNSPClass *pt_inst) /* :57-72 */
+static int NNSPClass_reset_impl(NNSPClass *pt_inst) /* :57-72 */
 {
     FeatureClass_setDefault((FeatureClass *)pt_inst->pt_feat);
     NeuralNetClass_setDefault((NeuralNetClass *)pt_inst->pt_net);
@@ -544,7 +632,7 @@ static void post_unpack(NNSPClass *p, const NnPost *q)
     memcpy(p->outputs, q->outputs, sizeof q->outputs);
 }
 
-int16_t NNSPClass_exec(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
+static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
 {
     FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
     NeuralNetClass *net = (NeuralNetClass *)pt_inst->pt_net;
@@ -590,7 +678,7 @@ int16_t NNSPClass_exec(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
     return pt_inst->trigger;
 }
 
-void my_argmax(int32_t *vec, int len, int16_t *Imax) /* :130-144 */
+static void my_argmax_impl(int32_t *vec, int len, int16_t *Imax) /* :130-144 */
 {
     begin();
     int32_t *dv = (int32_t *)up(vec, (size_t)len * 4);
@@ -613,8 +701,8 @@ static int32_t scalar1(int op, int32_t x)
     fin();
     return o;
 }
-int32_t ceiling(int32_t input) { return scalar1(0, input); }      /* :229-235 */
-int32_t compute_pwr2(int32_t input) { return scalar1(1, input); } /* :237-258 */
+static int32_t ceiling_impl(int32_t input) { return scalar1(0, input); }      /* :229-235 */
+static int32_t compute_pwr2_impl(int32_t input) { return scalar1(1, input); } /* :237-258 */
 
 static void post_call(NNSPClass *pt_inst, int32_t *est, int16_t *pt_trigger, int nn_id)
 {
@@ -635,12 +723,12 @@ static void post_call(NNSPClass *pt_inst, int32_t *est, int16_t *pt_trigger, int
     *pt_trigger = ps.trigger;
 }
 
-void binary_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :191-227 */
+static void binary_post_proc_impl(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :191-227 */
 {
     post_call(pt_inst, pt_nn_est, pt_trigger, 1);
 }
 
-void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :146-189 */
+static void s2i_post_proc_impl(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger) /* :146-189 */
 {
     post_call(pt_inst, pt_nn_est, pt_trigger, 0);
 }
@@ -699,7 +787,7 @@ static int affine_rows_call(int16_t R, int16_t **pp_output, int8_t **pp_kernel, 
     return 0;
 }
 
-int affine_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+static int affine_Krows_8x16_impl(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
                       int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
                       int16_t qbit_input, int64_t *pt_accum, int8_t is_out,
                       void *(*act)(void *, int32_t *, int)) /* affine.c:12-259 */
@@ -708,7 +796,7 @@ int affine_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kerne
                             qbit_input, pt_accum, NULL, is_out, act);
 }
 
-int affine_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+static int affine_Krows_8x16_acc32b_impl(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
                              int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
                              int16_t qbit_input, int32_t *pt_accum, int8_t is_out,
                              void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:12-260 */
@@ -764,7 +852,7 @@ static int rc_krows(int16_t R, int16_t **pp_output, int8_t **pp_kernel, int8_t *
     return 0;
 }
 
-int rc_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+static int rc_Krows_8x16_impl(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
                   int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec,
                   int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
                   void *(*act)(void *, int32_t *, int)) /* affine.c:348-407 */
@@ -773,7 +861,7 @@ int rc_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, i
                     dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 0, act);
 }
 
-int rc_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+static int rc_Krows_8x16_acc32b_impl(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
                          int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input,
                          int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input,
                          int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:349-408 */
@@ -782,7 +870,7 @@ int rc_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_ke
                     dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 1, act);
 }
 
-int rc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+static int rc_8x16_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
             int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
             int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
             void *(*act)(void *, int32_t *, int)) /* affine.c:492-563 */
@@ -793,7 +881,7 @@ int rc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *
                         dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, 0, act, &ob);
 }
 
-int rc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+static int rc_8x16_acc32b_impl(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
                    int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec,
                    int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
                    ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)) /* affine_acc32b.c:493-564 */
@@ -814,5 +902,462 @@ static void shift_call(void *x, int shift, int len, int acc32)
     down(x, d, nb);
     fin();
 }
-void shift_64b(int64_t *x, int8_t shift, int len) { shift_call(x, shift, len, 0); } /* affine.c:565-591 */
-void shift_32b(int32_t *x, int8_t shift, int len) { shift_call(x, shift, len, 1); } /* affine_acc32b.c:566-592 */
+static void shift_64b_impl(int64_t *x, int8_t shift, int len) { shift_call(x, shift, len, 0); } /* affine.c:565-591 */
+static void shift_32b_impl(int32_t *x, int8_t shift, int len) { shift_call(x, shift, len, 1); } /* affine_acc32b.c:566-592 */
+
+/* ---------------------------------------------------------------------------
+ * public entry points: a HIP or allocation failure inside any of them unwinds
+ * to the outermost one (longjmp from CK), which returns with its outputs
+ * untouched; the error stays readable through nnsp_legacy_status() /
+ * nnsp_strerror() (the reference has no error channel: its functions return
+ * 0 or void).  Nested entry points (NNSPClass_reset -> FeatureClass_setDefault)
+ * share the outermost jump target.
+ * ------------------------------------------------------------------------- */
+void *relu6_fix(int16_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return NULL;
+        }
+    }
+    void *r = relu6_fix_impl(y, x, len);
+    --G.depth;
+    return r;
+}
+
+void *tanh_fix(int16_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return NULL;
+        }
+    }
+    void *r = tanh_fix_impl(y, x, len);
+    --G.depth;
+    return r;
+}
+
+void *sigmoid_fix(int16_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return NULL;
+        }
+    }
+    void *r = sigmoid_fix_impl(y, x, len);
+    --G.depth;
+    return r;
+}
+
+void *linear_fix(int32_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return NULL;
+        }
+    }
+    void *r = linear_fix_impl(y, x, len);
+    --G.depth;
+    return r;
+}
+
+int fc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+            int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
+            int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
+            int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+            void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = fc_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+int fc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+                   int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
+                   int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+                   int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = fc_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+int lstm_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+              int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
+              int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
+              int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+              void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = lstm_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+int lstm_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
+                     int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
+                     int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+                     int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                     ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = lstm_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+void NeuralNetClass_exe(NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    NeuralNetClass_exe_impl(pt_inst, input, output, debug_layer);
+    --G.depth;
+}
+
+void arm_fft_exec(int32_t *y, int32_t *x)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    arm_fft_exec_impl(y, x);
+    --G.depth;
+}
+
+int stftModule_analyze_arm(void *ps_, int16_t *x, int32_t *y)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = stftModule_analyze_arm_impl(ps_, x, y);
+    --G.depth;
+    return r;
+}
+
+void spec2pspec_arm(int32_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    spec2pspec_arm_impl(y, x, len);
+    --G.depth;
+}
+
+void melSpecProc(int32_t *specs, int32_t *melSpecs)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    melSpecProc_impl(specs, melSpecs);
+    --G.depth;
+}
+
+void norm_oneTwo(int32_t x, int32_t *y, int8_t *shift)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    norm_oneTwo_impl(x, y, shift);
+    --G.depth;
+}
+
+void log10_vec(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    log10_vec_impl(out, x, len, bit_frac_in);
+    --G.depth;
+}
+
+void my_log10(int32_t *out, int32_t x)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    my_log10_impl(out, x);
+    --G.depth;
+}
+
+void FeatureClass_setDefault(FeatureClass *ps)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    FeatureClass_setDefault_impl(ps);
+    --G.depth;
+}
+
+void FeatureClass_execute(FeatureClass *ps, int16_t *input)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    FeatureClass_execute_impl(ps, input);
+    --G.depth;
+}
+
+int NNSPClass_reset(NNSPClass *pt_inst)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = NNSPClass_reset_impl(pt_inst);
+    --G.depth;
+    return r;
+}
+
+int16_t NNSPClass_exec(NNSPClass *pt_inst, int16_t *rawPCM)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return 0;
+        }
+    }
+    int16_t r = NNSPClass_exec_impl(pt_inst, rawPCM);
+    --G.depth;
+    return r;
+}
+
+void my_argmax(int32_t *vec, int len, int16_t *Imax)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    my_argmax_impl(vec, len, Imax);
+    --G.depth;
+}
+
+int32_t ceiling(int32_t input)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return 0;
+        }
+    }
+    int32_t r = ceiling_impl(input);
+    --G.depth;
+    return r;
+}
+
+int32_t compute_pwr2(int32_t input)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return 0;
+        }
+    }
+    int32_t r = compute_pwr2_impl(input);
+    --G.depth;
+    return r;
+}
+
+void binary_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    binary_post_proc_impl(pt_inst, pt_nn_est, pt_trigger);
+    --G.depth;
+}
+
+void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    s2i_post_proc_impl(pt_inst, pt_nn_est, pt_trigger);
+    --G.depth;
+}
+
+int affine_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+                      int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
+                      int16_t qbit_input, int64_t *pt_accum, int8_t is_out,
+                      void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = affine_Krows_8x16_impl(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act);
+    --G.depth;
+    return r;
+}
+
+int affine_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
+                             int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
+                             int16_t qbit_input, int32_t *pt_accum, int8_t is_out,
+                             void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = affine_Krows_8x16_acc32b_impl(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act);
+    --G.depth;
+    return r;
+}
+
+int rc_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+                  int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec,
+                  int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                  void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = rc_Krows_8x16_impl(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
+    --G.depth;
+    return r;
+}
+
+int rc_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
+                         int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input,
+                         int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input,
+                         int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = rc_Krows_8x16_acc32b_impl(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
+    --G.depth;
+    return r;
+}
+
+int rc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+            int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
+            int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
+            void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = rc_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+int rc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
+                   int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec,
+                   int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
+                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = rc_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
+    --G.depth;
+    return r;
+}
+
+void shift_64b(int64_t *x, int8_t shift, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    shift_64b_impl(x, shift, len);
+    --G.depth;
+}
+
+void shift_32b(int32_t *x, int8_t shift, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    shift_32b_impl(x, shift, len);
+    --G.depth;
+}

@@ -181,8 +181,8 @@ int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, co
 int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, const int32_t *list,
                            int n_list, const int32_t *seg_begin, int seg_len, int lookback,
                            const int16_t *hist, int hist_frames, void *stream);
-int nnspk_launch_synth_pcm(int16_t *out, int S, int T, unsigned long long seed, int s0,
-                           long long t0, int amp, void *stream);
+int nnspk_launch_synth_pcm(int16_t *out, int S, int T, unsigned long long seed, int s0, long long t0, int amp,
+                           const int16_t *wavs, int n_wavs, int wav_len, int every, void *stream);
 int nnspk_launch_rfft(int32_t *x, int32_t *y, int n, void *stream);
 int nnspk_launch_pspec(int32_t *y, const int32_t *x, int len, int n, void *stream);
 int nnspk_launch_mel(const int32_t *spec, int32_t *mel, int n, void *stream);

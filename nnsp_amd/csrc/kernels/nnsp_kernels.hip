@@ -875,12 +875,21 @@ __global__ void k_shift(void* x, int sh, int n, int acc32) {
 }
 
 // Synthetic PCM (bench / tests): SplitMix64(seed, stream, sample) -> int16 in
-// [-amp, amp-1]; identical to oracle.synthetic_pcm.
-__global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp) {
+// [-amp, amp-1]; identical to oracle.synthetic_pcm.  With wavs:
+// every `every`-th stream g (g % every == 0) instead replays wav
+// (g / every) % n_wavs cyclically from sample offset (g * 1601) mod wav_len.
+__global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp,
+                            const int16_t* wavs, int n_wavs, int wav_len, int every) {
     const long long n = (long long)S * T * 160;
     for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
         const unsigned long long s = (unsigned long long)(i / (160LL * T)) + (unsigned long long)s0;
         const unsigned long long k = (unsigned long long)(i % (160LL * T)) + (unsigned long long)t0 * 160ULL;
+        if (wavs && every > 0 && s % (unsigned long long)every == 0) {
+            const unsigned long long w = (s / (unsigned long long)every) % (unsigned long long)n_wavs;
+            const unsigned long long L = (unsigned long long)wav_len;
+            out[i] = wavs[w * L + (s * 1601ULL % L + k) % L];
+            continue;
+        }
         unsigned long long z = seed + s * 0x9E3779B97F4A7C15ULL + k * 0xBF58476D1CE4E5B9ULL;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
@@ -962,8 +971,9 @@ int nnspk_launch_tail_roll(int16_t* tail, const int16_t* pcm, int S, int T, cons
 }
 
 int nnspk_launch_synth_pcm(int16_t* out, int S, int T, unsigned long long seed, int s0, long long t0, int amp,
-                           void* stream) {
-    hipLaunchKernelGGL(k_synth_pcm, dim3(4096), dim3(256), 0, (hipStream_t)stream, out, S, T, seed, s0, t0, amp);
+                           const int16_t* wavs, int n_wavs, int wav_len, int every, void* stream) {
+    hipLaunchKernelGGL(k_synth_pcm, dim3(4096), dim3(256), 0, (hipStream_t)stream, out, S, T, seed, s0, t0, amp, wavs,
+                       n_wavs, wav_len, every);
     return ok(hipGetLastError());
 }
 

@@ -152,6 +152,10 @@ class NNSPCascade:
     def set_window(self, frames: int) -> None:
         _lib.check(_lib.lib().nnsp_cascade_set_window(self.h, frames), "nnsp_cascade_set_window")
 
+    def set_serial(self, on: bool) -> None:
+        """The nets' work of a round one after another on one stream (instrumentation)."""
+        _lib.check(_lib.lib().nnsp_cascade_set_serial(self.h, int(on)), "nnsp_cascade_set_serial")
+
     def set_timing(self, on: bool) -> None:
         """Per-round, per-net device timing for net_stats (off by default)."""
         _lib.check(_lib.lib().nnsp_cascade_set_timing(self.h, int(on)), "nnsp_cascade_set_timing")

@@ -12,7 +12,9 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+# NNSP_ORACLE_LIB: another build of nnsp_oracle.c (bench.py's cpu_baseline
+# compiles one with -march=native on the host it runs on)
+LIB = os.environ.get("NNSP_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF = os.path.join(HERE, "_ref", "libnnsp_ref_partial.so")
 
 MAXL = 10
@@ -207,8 +209,11 @@ def rfft512(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
 
 
 def synthetic_pcm(S: int, T: int, seed: int = 0x4E4E5350, t0: int = 0, s0: int = 0,
-                  amp: int = 4096) -> np.ndarray:
-    """SplitMix64(seed, stream, sample) -> int16 in [-amp, amp-1]."""
+                  amp: int = 4096, wavs: np.ndarray | None = None, every: int = 4) -> np.ndarray:
+    """SplitMix64(seed, stream, sample) -> int16 in [-amp, amp-1] (SURVEY 8(d));
+    with wavs ([n_wavs][len] int16): stream g = s0 + s with g % every == 0
+    replays wav (g // every) % n_wavs cyclically from offset (g * 1601) % len
+    (nnsp_synth_pcm_mix on the device)."""
     s = (np.arange(S, dtype=np.uint64) + np.uint64(s0))[:, None]
     n = (np.arange(T * 160, dtype=np.uint64) + np.uint64(t0 * 160))[None, :]
     with np.errstate(over="ignore"):
@@ -216,8 +221,21 @@ def synthetic_pcm(S: int, T: int, seed: int = 0x4E4E5350, t0: int = 0, s0: int =
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
         z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
         z = z ^ (z >> np.uint64(31))
-    v = (z % np.uint64(2 * amp)).astype(np.int64) - amp
-    return v.astype(np.int16).reshape(S, T, 160)
+    v = ((z % np.uint64(2 * amp)).astype(np.int64) - amp).astype(np.int16)
+    if wavs is not None:
+        L = wavs.shape[1]
+        g = np.arange(S, dtype=np.int64) + s0
+        for i in np.nonzero(g % every == 0)[0]:
+            w = wavs[(g[i] // every) % len(wavs)]
+            v[i] = w[(g[i] * 1601 % L + t0 * 160 + np.arange(T * 160, dtype=np.int64)) % L]
+    return v.reshape(S, T, 160)
+
+
+def load_wavs() -> np.ndarray:
+    """python/test_wavs/{speech,galaxy,galaxy_s2i}.wav as [3][160000] int16
+    (committed as tests/golden/test_wavs.npz)."""
+    z = np.load(os.path.join(os.path.dirname(HERE), "tests", "golden", "test_wavs.npz"))
+    return np.stack([z[k] for k in ("speech", "galaxy", "galaxy_s2i")])
 
 
 class or_stream(C.Structure):

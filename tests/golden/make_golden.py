@@ -23,7 +23,11 @@ reference tree).
                    consecutive calls (LSTM state carried) on the three reference
                    nets and on the N3 shapes of nnsp_amd.nets.GEN_SPECS
 
-Usage: make_golden.py [stages] [nets] [nn]   (default: all)
+  test_wavs.npz    python/test_wavs/{speech,galaxy,galaxy_s2i}.wav samples
+                   (16 kHz mono int16, 160000 each): the reference's own test
+                   inputs, replayed by every 4th synthetic stream
+
+Usage: make_golden.py [stages] [nets] [nn] [wavs]   (default: all)
 """
 from __future__ import annotations
 
@@ -380,13 +384,26 @@ def nn() -> None:
     np.savez_compressed(os.path.join(HERE, "ref_nn.npz"), **out)
 
 
+WAVS = ("speech", "galaxy", "galaxy_s2i")
+
+
+def wavs() -> None:
+    import wave
+    out = {}
+    for name in WAVS:
+        with wave.open(os.path.join(REF_PY, "test_wavs", f"{name}.wav")) as w:
+            assert (w.getframerate(), w.getnchannels(), w.getsampwidth()) == (16000, 1, 2)
+            out[name] = np.frombuffer(w.readframes(w.getnframes()), "<i2").astype(np.int16)
+    np.savez_compressed(os.path.join(HERE, "test_wavs.npz"), **out)
+
+
 def main() -> None:
     for so in (REF_SO, REF_NN_SO, REF_NETS_SO):
         if not os.path.exists(so):
             sys.exit("build oracle/_ref first (oracle/build_ref.sh)")
-    which = sys.argv[1:] or ["stages", "nets", "nn"]
+    which = sys.argv[1:] or ["stages", "nets", "nn", "wavs"]
     for w in which:   # nets before nn: nn re-packs the dumped reference nets
-        {"stages": stages, "nets": nets, "nn": nn}[w]()
+        {"stages": stages, "nets": nets, "nn": nn, "wavs": wavs}[w]()
     print("wrote", sorted(os.listdir(HERE)))
 
 
