@@ -192,8 +192,9 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
         z = np.load(os.path.join(ROOT, "tests", "golden", "test_wavs.npz"))
         wav = np.stack([z[k] for k in ("speech", "galaxy", "galaxy_s2i")])
         dwav = torch.from_numpy(wav).to("cuda")
-    # inputs resident in HBM before timing: one chunk buffer per step
-    bufs = [torch.empty((S, T, 160), dtype=torch.int16, device="cuda") for _ in range(W + K)]
+    # inputs resident in HBM before timing: one chunk buffer per step (+1:
+    # the chunk the last step's look-ahead front end reads)
+    bufs = [torch.empty((S, T, 160), dtype=torch.int16, device="cuda") for _ in range(W + K + 1)]
     for i, b in enumerate(bufs):
         _lib.check(_lib.lib().nnsp_synth_pcm_mix(b.data_ptr(), S, T, SEED, s0, i * T, AMP,
                                                  dwav.data_ptr() if dwav is not None else None,
@@ -202,16 +203,19 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     out3 = torch.empty((S, T, 3), dtype=torch.int16, device="cuda")
     ran = torch.empty((S, T), dtype=torch.int8, device="cuda")
 
-    def step(buf):
-        if cascade:   # per frame: the NNSP_ID that ran, its trigger and outputs
-            eng.exec_device(buf.data_ptr(), T, ran.data_ptr(), trig.data_ptr(), out3.data_ptr())
+    def step(buf, nxt=None):
+        if cascade:   # per frame: the NNSP_ID that ran, its trigger and outputs; the
+            # next chunk's front end runs ahead, overlapped with this chunk's nets
+            eng.exec_device(buf.data_ptr(), T, ran.data_ptr(), trig.data_ptr(), out3.data_ptr(),
+                            next_ptr=nxt.data_ptr() if (nxt is not None and not args.no_lookahead) else None,
+                            next_T=T)
         else:
             eng.exec_device(buf.data_ptr(), T, trig.data_ptr())
 
     eng.sync()
     torch.cuda.synchronize()
     for i in range(W):
-        step(bufs[i])
+        step(bufs[i], bufs[i + 1])
     eng.sync()
     if dist:
         dist.barrier()
@@ -219,7 +223,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     fe_ms, nn_ms, rounds, sched = 0.0, 0.0, 0, 0
     t0 = time.perf_counter()
     for i in range(K):
-        step(bufs[W + i])
+        step(bufs[W + i], bufs[W + i + 1])
         if cascade:
             r, f, _ = eng.last_stats()
             rounds += r
@@ -253,6 +257,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
         out["instrumented"]["shared_fe_ms"] = eng.fe_stats()
         rl, _, _ = eng.round_stats()
         out["streams_listed_per_round"] = rl.tolist()
+        out["window"] = dict(zip(("next_chunk", "auto", "last_chunk_cuts"), eng.window()))
     else:
         out["nn_ms"] = nn_ms / K
     eng.close()
@@ -347,7 +352,9 @@ def main() -> None:
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="strong: --total-streams split over the ranks")
     ap.add_argument("--total-streams", type=int, default=STRONG_TOTAL)
-    ap.add_argument("--window", type=int, default=-1, help="cascade frames per round (-1: library default)")
+    ap.add_argument("--window", type=int, default=-1, help="cascade frames per round (-1: automatic per chunk)")
+    ap.add_argument("--no-lookahead", action="store_true",
+                    help="cascade: no look-ahead front end of the next chunk (overlapped with the nets)")
     ap.add_argument("--frames", type=int, default=100, help="frames per step (chunk)")
     ap.add_argument("--acc32", action="store_true")
     ap.add_argument("--weights", default="ref", choices=["ref", "synth"])
@@ -419,7 +426,8 @@ def main() -> None:
             "device": info,
         }
         if args.net == "cascade":
-            out["cascade"] = {"rounds_per_step": res["rounds_per_step"],
+            out["cascade"] = {"rounds_per_step": res["rounds_per_step"], "window": res["window"],
+                              "lookahead_front_end": not args.no_lookahead,
                               "speculation_overhead": res["nn_frames_per_step"] / (S * args.frames) - 1.0,
                               "instrumented_chunk": res["instrumented"],
                               "streams_listed_per_round": res["streams_listed_per_round"]}

@@ -63,13 +63,29 @@ int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ra
                       int16_t *detected, int16_t *outputs3);
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
                              int16_t *detected, int16_t *outputs3);
+/* The same, plus a look-ahead: next_pcm (device, [S][next_T][160]) is the
+ * chunk the NEXT call will receive.  Its shared front end (the log-Mel of
+ * every frame, about half a chunk's device time) is queued behind this chunk's
+ * controller start and runs while the nets' rounds of this chunk run, so the
+ * two overlap.  The next call skips its own front end when it receives exactly
+ * that pointer and T; next_pcm must hold its final samples when passed and stay
+ * unchanged until then (nnsp_cascade_reset drops the look-ahead).  Used when
+ * the nets run concurrently (not in serial mode) and T, next_T >= the
+ * look-back + 1; otherwise it is ignored.  Results are identical. */
+int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *next_pcm,
+                                   int next_T, int8_t *net_ran, int16_t *detected, int16_t *outputs3);
 int nnsp_cascade_sync(nnsp_cascade *c);
 
 /* Scheduling knob (results do not depend on it): each round runs every
  * listed stream for at most this many frames (0: to the chunk end).  Smaller
- * windows waste less work past a net switch but take more rounds.  Default 16
- * (environment NNSP_CASCADE_WINDOW overrides it at create time). */
+ * windows waste less work past a net switch but take more rounds.  -1
+ * (default): chosen per chunk from the previous chunk's net switches per
+ * stream (< 0.5: 0, < 2: 32, else 16; the first chunk uses 16).  The
+ * environment NNSP_CASCADE_WINDOW (>= 0) fixes it at create time. */
 int nnsp_cascade_set_window(nnsp_cascade *c, int frames);
+/* The window the next chunk will use, whether it is automatic, and the
+ * number of segments the last chunk cut at a net switch. */
+int nnsp_cascade_get_window(nnsp_cascade *c, int *frames, int *is_auto, int *last_cuts);
 void *nnsp_cascade_stream(nnsp_cascade *c);
 
 /* Last chunk: rounds run, frames scheduled on the nets (>= S*T; the excess is
@@ -98,7 +114,8 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
                                 float *nn_ms, int *launches);
 
 /* Last chunk: device time in ms of the shared front end (the log-Mel of every
- * frame of every stream, one launch). */
+ * frame of every stream, one launch; timed in the previous call when that call
+ * ran it ahead). */
 int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms);
 
 /* Last chunk, per round k < max_rounds and net i (NNSP_ID): the number of

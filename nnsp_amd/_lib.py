@@ -109,10 +109,12 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_reset": (I, [P, P]),
         "nnsp_cascade_exec": (I, [P, P, I, P, P, P]),
         "nnsp_cascade_exec_device": (I, [P, P, I, P, P, P]),
+        "nnsp_cascade_exec_device_ahead": (I, [P, P, I, P, I, P, P, P]),
         "nnsp_cascade_sync": (I, [P]),
         "nnsp_cascade_set_window": (I, [P, I]),
         "nnsp_cascade_set_timing": (I, [P, I]),
         "nnsp_cascade_set_serial": (I, [P, I]),
+        "nnsp_cascade_get_window": (I, [P, C.POINTER(I), C.POINTER(I), C.POINTER(I)]),
         "nnsp_cascade_stream": (P, [P]),
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),

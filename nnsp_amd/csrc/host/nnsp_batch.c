@@ -173,7 +173,7 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     b->nn_id = nn_id;
     b->out_linear = out_linear;
     b->norm_shift = 30 - net->qbit_input[0]; /* FeatureClass qbit_output, nn_speech.c:40-44 */
-    int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count);
+    int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count, 0);
     if (e) goto fail;
     b->nout = b->im.img.nout;
     if ((e = nnspk_stream_create(&b->stream))) goto fail;

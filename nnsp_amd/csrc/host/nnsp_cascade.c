@@ -36,7 +36,7 @@
 
 #define HIST_MAX 99   /* PcmBufClass keeps 100 frames: look-back 0..99 */
 #define MAX_TIMED 32  /* rounds per chunk with per-net device timing */
-#define ZERO_BYTES (3 * 8 + (18 + 1 + MAX_TIMED * 3) * 4)
+#define ZERO_BYTES (3 * 8 + (18 + 2 + MAX_TIMED * 3) * 4)
 
 struct nnsp_cascade {
     nnsp_batch *net[3];
@@ -51,8 +51,9 @@ struct nnsp_cascade {
     /* per round parity and net: the round's stream lists (round r reads
      * [r & 1] while its kernels append the next round's to [(r + 1) & 1]) */
     int32_t *d_list[2][3], *d_cold_list[2][3];
-    int16_t *d_hist[2];
-    int hist_cur;
+    int16_t *d_hist[3];             /* PCM history before chunk k: d_hist[k % 3] (the look-ahead
+                                       front end of chunk k+1 writes d_hist[(k + 2) % 3]) */
+    long long chunk;                /* chunks run since create */
     int32_t *d_lmel;                /* [S][ring][40] shared log-Mel */
     int ring, abs0;                 /* ring slots (>= H + Tmax); slot of chunk frame 0 */
     int16_t *d_stail;               /* [S][320] PCM tail of the shared front end */
@@ -62,6 +63,7 @@ struct nnsp_cascade {
     int16_t *d_pdef;                /* [3][40] FeatureClass_setDefault context value per net */
     int32_t *d_rcount;              /* [MAX_TIMED][3] list lengths each round ran with */
     int32_t *d_last_round;          /* last round a stream was listed for (+1) */
+    int32_t *d_cuts;                /* segments cut by a net switch in the chunk */
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation) */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
@@ -71,7 +73,14 @@ struct nnsp_cascade {
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
+    const int16_t *pre_pcm;         /* the chunk whose shared front end the last call ran ahead */
+    int pre_T;
+    void *ev_ahead[2];
+    float ahead_ms, prev_ahead_ms;  /* look-ahead front end: this call's, the previous call's */
+    int sfe_ahead;                  /* last chunk's shared front end ran in the previous call */
     int window;                     /* frames per stream and round (0: to the chunk end) */
+    int auto_window;                /* pick window per chunk from the last chunk's switch rate */
+    int last_cuts;                  /* last chunk: segments cut by a net switch */
     int serial;                     /* NNSP_CASCADE_SERIAL: the nets' work on the main stream (no fork/join) */
     int fused;                      /* controller fused into the nets' recur kernels (compiled shapes) */
     int timing;                     /* per-round, per-net device timing (set_timing; NNSP_CASCADE_TIMING) */
@@ -131,12 +140,13 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     /* PCM history: the look-back frame and, for the second frame after a
      * net's reset, the one before it (FE_MODE_COLD re-reads it) */
     c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
-    c->ring = c->H + c->Tmax;
+    c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
+    if ((e = nnspk_event_create(&c->ev_ahead[0])) || (e = nnspk_event_create(&c->ev_ahead[1]))) goto fail;
     for (int n = 0; n < 3; ++n) {
         if ((e = nnspk_stream_create(&c->ns[n])) || (e = nnspk_event_create(&c->ev_join[n])) ||
             (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
@@ -151,7 +161,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->d_frames = (unsigned long long *)c->d_zero;                 /* [3] */
     c->d_counts = (int32_t *)((char *)c->d_zero + 3 * 8);         /* [18] */
     c->d_last_round = c->d_counts + 18;                             /* [1] */
-    c->d_rcount = c->d_last_round + 1;                              /* [MAX_TIMED][3] */
+    c->d_cuts = c->d_last_round + 1;                                /* [1] */
+    c->d_rcount = c->d_cuts + 1;                                    /* [MAX_TIMED][3] */
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
@@ -167,7 +178,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         }
         if ((e = nnspk_memset(c->d_mask[i], 0, S, c->stream))) goto fail;
     }
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 3; ++i)
         if ((e = nnspk_malloc((void **)&c->d_hist[i], S * (size_t)c->H * 320))) goto fail;
     if ((e = nnspk_memset(c->d_st, 0, S * sizeof(CascState), c->stream))) goto fail; /* pos 0 */
     {
@@ -184,6 +195,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         a->frames = c->d_frames;
         a->fresh = c->d_fresh;
         a->last_round = c->d_last_round;
+        a->cuts = c->d_cuts;
         for (int i = 0; i < 3; ++i) {
             a->trig[i] = c->d_trig[i];
             a->feats[i] = nets[i]->d_feats;
@@ -220,7 +232,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         nnspk_free(tl);
         if (e) goto fail;
     }
-    c->window = 16; /* profiles/sweep_window.sh on MI355X: 14 ~ 16 > 12 at 32768 streams */
+    c->window = 16;      /* the first chunk's window; then chosen per chunk (auto_window) */
+    c->auto_window = 1;
     {
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
         /* the controller runs inside the nets' pipelined recur kernels when all
@@ -232,7 +245,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
         const char *w = getenv("NNSP_CASCADE_WINDOW");
-        if (w) c->window = atoi(w);
+        if (w && atoi(w) >= 0) {
+            c->window = atoi(w);
+            c->auto_window = 0;
+        }
     }
     if ((e = nnsp_cascade_reset(c, NULL))) goto fail;
     return 0;
@@ -248,7 +264,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     if (c->stream) nnspk_sync(c->stream);
     void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_zero,    c->d_trig[0], c->d_trig[1],
                     c->d_trig[2], c->d_mask[0],   c->d_mask[1],
-                    c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1],
+                    c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1], c->d_hist[2],
                     c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
                     c->d_ran,     c->d_pdef,      c->d_cold_list[0][0],
                     c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
@@ -259,6 +275,8 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         nnspk_event_destroy(c->ev_fe[i]);
     }
     nnspk_event_destroy(c->ev_fork);
+    nnspk_event_destroy(c->ev_ahead[0]);
+    nnspk_event_destroy(c->ev_ahead[1]);
     for (int n = 0; n < 3; ++n) {
         nnspk_event_destroy(c->ev_join[n]);
         nnspk_event_destroy(c->ev_rnd[0][n]);
@@ -281,7 +299,8 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
         TRY(nnspk_h2d(c->d_mask[0], mask, (size_t)c->S, c->stream));
         dm = c->d_mask[0];
     }
-    TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->hist_cur], c->H, c->d_stail, c->d_fresh, dm, c->S,
+    c->pre_pcm = NULL; /* a look-ahead front end ran on the old tail: recompute */
+    TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->chunk % 3], c->H, c->d_stail, c->d_fresh, dm, c->S,
                                 c->stream));
     /* PcmBufClass_reset: every look-back frame is silence */
     TRY(nnspk_launch_lmel_fill(c->d_lmel, c->ring, dm, c->S, c->stream));
@@ -391,10 +410,43 @@ static int join_rounds(nnsp_cascade *c, int r)
     return 0;
 }
 
+/* The shared front end of chunk k (log-Mel of every frame into ring slots
+ * abs0 .. abs0 + T - 1; the PCM history of chunk k + 1 into d_hist[(k+1) % 3]
+ * when T >= H) on the cascade's stream.  tail: the samples of the two frames
+ * before the chunk, tail_stride apart per stream. */
+static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *tail, int tail_stride, int abs0,
+                     long long k)
+{
+    FeArgs fa;
+    memset(&fa, 0, sizeof fa);
+    fa.pcm = pcm;
+    fa.tail = tail;
+    fa.tail_stride = tail_stride;
+    fa.S = c->S;
+    fa.T = T;
+    fa.mean = c->net[0]->d_mean; /* unused in FE_MODE_SHARED */
+    fa.stdR = c->net[0]->d_stdR;
+    fa.mode = FE_MODE_SHARED;
+    fa.ring = c->ring;
+    fa.abs0 = abs0;
+    fa.lmel = c->d_lmel;
+    if (T >= c->H) { /* the next chunk's look-back history, stored by the front end */
+        fa.hist_out = c->d_hist[(k + 1) % 3];
+        fa.hist_frames = c->H;
+    }
+    return nnspk_launch_fe(&fa, c->stream);
+}
+
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran, int16_t *detected,
                              int16_t *outputs3)
 {
-    if (!c || !pcm || T <= 0 || T > c->Tmax) {
+    return nnsp_cascade_exec_device_ahead(c, pcm, T, NULL, 0, net_ran, detected, outputs3);
+}
+
+int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *next_pcm, int next_T,
+                                   int8_t *net_ran, int16_t *detected, int16_t *outputs3)
+{
+    if (!c || !pcm || T <= 0 || T > c->Tmax || (next_pcm && (next_T <= 0 || next_T > c->Tmax))) {
         nnsp_set_error("nnsp_cascade_exec: T must be in 1..%d", c ? c->Tmax : 0);
         return NNSP_EINVAL;
     }
@@ -405,29 +457,16 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     a.detected = detected;
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
+    const long long k = c->chunk;
     TRY(nnspk_event_record(c->ev[0], c->stream));
-    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream)); /* counts, frames, last round, rcount */
-    {   /* 1. log-Mel of every frame (net-independent) */
-        FeArgs fa;
-        memset(&fa, 0, sizeof fa);
-        fa.pcm = pcm;
-        fa.tail = c->d_stail;
-        fa.S = c->S;
-        fa.T = T;
-        fa.mean = c->net[0]->d_mean; /* unused in FE_MODE_SHARED */
-        fa.stdR = c->net[0]->d_stdR;
-        fa.mode = FE_MODE_SHARED;
-        fa.ring = c->ring;
-        fa.abs0 = c->abs0;
-        fa.lmel = c->d_lmel;
-        if (T >= c->H) { /* the next chunk's look-back history, stored by the front end */
-            fa.hist_out = c->d_hist[c->hist_cur ^ 1];
-            fa.hist_frames = c->H;
-        }
-        TRY(nnspk_event_record(c->ev_fe[0], c->stream));
-        TRY(nnspk_launch_fe(&fa, c->stream));
-        TRY(nnspk_event_record(c->ev_fe[1], c->stream));
-    }
+    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream)); /* counts, frames, last round, cuts, rcount */
+    /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
+    const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
+    c->pre_pcm = NULL;
+    TRY(nnspk_event_record(c->ev_fe[0], c->stream));
+    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k));
+    TRY(nnspk_event_record(c->ev_fe[1], c->stream));
+    c->sfe_ahead = ahead_done;
     a.counts = c->d_counts; /* round 0's lists */
     for (int n = 0; n < 3; ++n) {
         a.list[n] = c->d_list[0][n];
@@ -435,9 +474,19 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     }
     TRY(nnspk_launch_casc_begin(&a, c->stream));
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
+    /* look-ahead: the next chunk's shared front end, queued on the cascade's
+     * stream behind the fork -- it runs while the nets' rounds of this chunk
+     * run on their streams (it writes ring slots and a history buffer this
+     * chunk does not read; its STFT tail is this chunk's last two frames) */
+    const int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
+    if (ahead) {
+        TRY(nnspk_event_record(c->ev_ahead[0], c->stream));
+        TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring, k + 1));
+        TRY(nnspk_event_record(c->ev_ahead[1], c->stream));
+    }
     /* rounds run without host round trips: launch as many as the last chunk
      * needed, then check the next round's list lengths (one read-back) */
-    const int16_t *hist = c->d_hist[c->hist_cur];
+    const int16_t *hist = c->d_hist[k % 3];
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
         for (; r < R; ++r) TRY(launch_round(c, &a, r, pcm, T, hist));
@@ -452,18 +501,37 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
     /* voice buffer: keep the last H frames for the next chunk's look-back;
      * the shared front end's STFT buffer keeps the last 2 frames */
     if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
-        TRY(nnspk_launch_hist_roll(c->d_hist[c->hist_cur ^ 1], hist, pcm, c->S, T, c->H, c->stream));
-    c->hist_cur ^= 1;
+        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
     TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     c->abs0 = (c->abs0 + T) % c->ring;
+    c->chunk = k + 1;
+    if (ahead) {
+        c->pre_pcm = next_pcm;
+        c->pre_T = next_T;
+    }
     TRY(nnspk_event_record(c->ev[1], c->stream));
     /* bookkeeping: rounds that had work, per-net device time of those rounds */
-    int32_t last = 0, rc[MAX_TIMED][3];
-    TRY(nnspk_d2h(&last, c->d_last_round, 4, c->stream));
+    int32_t last[2] = {0, 0}, rc[MAX_TIMED][3];
+    TRY(nnspk_d2h(last, c->d_last_round, 8, c->stream)); /* last_round, cuts */
     TRY(nnspk_d2h(rc, c->d_rcount, sizeof rc, c->stream));
     TRY(nnspk_sync(c->stream));
-    c->last_rounds = last + 1;
+    c->last_rounds = last[0] + 1;
+    c->last_cuts = last[1];
+    if (c->auto_window) {
+        /* window for the next chunk from this chunk's net switches per stream:
+         * few switches -> run each stream to the chunk end in one round (a
+         * switch then wastes the rest of the chunk's work on that stream, but
+         * rounds are few); frequent switches -> short windows bound the waste.
+         * Results do not depend on the window (tests/test_gpu_cascade.py). */
+        const double per = (double)c->last_cuts / (double)c->S;
+        c->window = per < 0.5 ? 0 : (per < 2.0 ? 32 : 16);
+    }
     TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
+    c->ahead_ms = 0.f;
+    if (ahead) TRY(nnspk_event_elapsed(&c->ahead_ms, c->ev_ahead[0], c->ev_ahead[1]));
+    /* the shared front end of this chunk: timed here, or by the previous call (ahead) */
+    if (ahead_done) c->sfe_ms = c->prev_ahead_ms;
+    c->prev_ahead_ms = c->ahead_ms;
     memcpy(c->rc, rc, sizeof rc);
     memset(c->rfe, 0, sizeof c->rfe);
     memset(c->rnn, 0, sizeof c->rnn);
@@ -513,8 +581,18 @@ int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ra
 
 int nnsp_cascade_set_window(nnsp_cascade *c, int frames)
 {
-    if (!c || frames < 0) return NNSP_EINVAL;
-    c->window = frames;
+    if (!c || frames < -1) return NNSP_EINVAL;
+    c->auto_window = frames < 0;
+    if (frames >= 0) c->window = frames;
+    return 0;
+}
+
+int nnsp_cascade_get_window(nnsp_cascade *c, int *frames, int *is_auto, int *last_cuts)
+{
+    if (!c) return NNSP_EINVAL;
+    if (frames) *frames = c->window;
+    if (is_auto) *is_auto = c->auto_window;
+    if (last_cuts) *last_cuts = c->last_cuts;
     return 0;
 }
 

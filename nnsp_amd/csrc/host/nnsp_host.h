@@ -36,7 +36,7 @@ typedef struct {
 
 int nnsp_describe_net(const NeuralNetClass *net, nnsp_layer_desc *L, int *nl, int *out_linear);
 int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id,
-                     int thresh_prob, int th_count);
+                     int thresh_prob, int th_count, int direct);
 int nnsp_image_upload(nnsp_image *im, void *stream);
 void nnsp_image_free(nnsp_image *im);
 

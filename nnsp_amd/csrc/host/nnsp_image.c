@@ -171,7 +171,7 @@ static void put_frags(uint8_t *A, const int8_t *nat, int K, int nrt, int nkt, in
 static int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
 int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id,
-                     int thresh_prob, int th_count)
+                     int thresh_prob, int th_count, int direct)
 {
     memset(im, 0, sizeof *im);
     NnImage *g = &im->img;
@@ -242,7 +242,15 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
             nnsp_set_error("mixed acc32 / acc64 layers are not supported");
             return NNSP_EUNSUPPORTED;
         }
-    if (L[nl - 1].type == NN_FC && g->nout > NN_MAX_OUT) {
+    /* streaming engines keep the last layer's row per stream (<= NN_MAX_OUT);
+     * a direct image (one NeuralNetClass_exe / fc_8x16 call) returns the raw
+     * activation row: 256 int16 or 128 int32 (linear) */
+    for (int i = 0; i < nl; ++i)
+        if (L[i].type == NN_FC && L[i].act == 3 && L[i].N > NN_MAX_K / 2) {
+            nnsp_set_error("layer %d: linear FC width %d > %d (int32 outputs)", i, L[i].N, NN_MAX_K / 2);
+            return NNSP_EUNSUPPORTED;
+        }
+    if (!direct && L[nl - 1].type == NN_FC && g->nout > NN_MAX_OUT) {
         nnsp_set_error("output width %d > %d", g->nout, NN_MAX_OUT);
         return NNSP_EUNSUPPORTED;
     }

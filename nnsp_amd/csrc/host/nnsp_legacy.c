@@ -188,7 +188,7 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
     n->key[0] = k0; n->key[1] = k1; n->key[2] = k2; n->key[3] = k3;
     memcpy(n->ikey, ik, sizeof n->ikey);
     n->bytes = bytes;
-    int e = nnsp_image_build(&n->im, L, nl, 0, 0, 0);
+    int e = nnsp_image_build(&n->im, L, nl, 0, 0, 0, 1);
     if (!e) e = nnsp_image_upload(&n->im, G.stream);
     if (e) {
         nnsp_image_free(&n->im);

@@ -92,6 +92,12 @@ __device__ __forceinline__ void post_reset(P& p) {
     p.outputs[0] = p.outputs[1] = p.outputs[2] = 0;
 }
 
+// segments cut by a net switch (one atomic per wave; whole wave calls)
+__device__ __forceinline__ void count_cuts(const CascArgs& a, bool cut) {
+    const unsigned long long m = __ballot(cut);
+    if (m && a.cuts && (threadIdx.x & 63) == 0) atomicAdd(a.cuts, (int)__popcll(m));
+}
+
 // frames the next round schedules for a stream that continues at b_next
 __device__ __forceinline__ unsigned long long next_frames(const CascArgs& a, int T, bool want, int b_next) {
     return want ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, T - b_next) : T - b_next) : 0ull;

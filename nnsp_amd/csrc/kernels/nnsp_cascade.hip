@@ -45,7 +45,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < 6 && a.counts_clear) a.counts_clear[s] = 0;
     const int T = a.T;
-    bool want = false;
+    bool want = false, was_cut = false;
     int n_next = 0, b_next = T, fr_next = 2;
     if (s < a.S && a.seg_begin[s] < T) {
         const int b = a.seg_begin[s];
@@ -102,6 +102,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
             for (int k = 0; k < NN_MAX_W / 4; ++k) cs[k] = z;
             nnsp::post_reset(*(reinterpret_cast<NnPost*>(a.post[n]) + s));
             b_next = cut + 1;
+            was_cut = true;
         }
         a.st[s] = st;
         a.seg_begin[s] = b_next;
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
     list_next(a, n_next, s, want, fr_next);
     if (a.last_round && __ballot(want) && (threadIdx.x & 63) == 0) atomicMax(a.last_round, a.round + 1);
     add_frames(a, n_next, nnsp::next_frames(a, T, want, b_next));
+    nnsp::count_cuts(a, was_cut);
 }
 
 // nnCntrlClass_reset's controller part + PcmBufClass_reset (nnCntrlClass.c:132-150,

@@ -1030,6 +1030,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
         nnsp::list_next(ca, n_next, s, want, fr_next);
         if (ca.last_round && __ballot(want) && lane == 0) atomicMax(ca.last_round, ca.round + 1);
         nnsp::add_frames(ca, n_next, nnsp::next_frames(ca, T, want, b_next));
+        nnsp::count_cuts(ca, lane < 16 && valid && cut >= 0);
     }
 }
 

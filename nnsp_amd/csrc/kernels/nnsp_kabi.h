@@ -59,6 +59,9 @@ typedef struct {
      * the look-back history of the next chunk, written while the samples are
      * in registers anyway (replaces a separate history roll) */
     int16_t *hist_out;
+    int32_t tail_stride;      /* samples between streams' tails (0: 320, a [S][320] buffer; a chunk's
+                                 last two frames: T * 160) */
+    int32_t pad_;
 } FeArgs;
 
 /* Cascade: where a net's segment features come from -- the shared log-Mel
@@ -257,6 +260,7 @@ typedef struct CascArgs_ {
     int16_t *outputs3;        /* [S][T][3] or NULL */
     int8_t *fresh;            /* [S] frames the current net ran since its reset (0..2) */
     FeatSrc fs[3];            /* per net id: segment feature source (slot 5 kept at a reset) */
+    int32_t *cuts;            /* segments cut by a net switch this chunk (window heuristic), or NULL */
 } CascArgs;
 
 int nnspk_launch_casc_begin(const CascArgs *a, void *stream);

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         if (cold) {
             if (fi < p.z) return nnsp_zero_pcm;
         } else if (fi < p.b) {
-            return a.tail + (size_t)p.s * 320 + (fi - p.b + 2) * 160;
+            return a.tail + (size_t)p.s * (a.tail_stride ? (unsigned)a.tail_stride : 320u) + (fi - p.b + 2) * 160;
         }
         const int x = fi - a.lookback;
         return x >= 0 ? a.pcm + ((size_t)p.s * a.T + x) * 160

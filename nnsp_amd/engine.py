@@ -26,7 +26,7 @@ class NNSPBatch:
         self.data = net
         self.handle = _lib.NetHandle(net, acc32=acc32)
         self.S, self.Tmax = n_streams, max_frames
-        self.nn_id = NN_ID[net.spec.name]
+        self.nn_id = net.spec.nn_id
         L = _lib.lib()
         h = C.c_void_p()
         _lib.check(L.nnsp_batch_create(C.byref(h), self.handle.addr, self.nn_id,
@@ -142,15 +142,25 @@ class NNSPCascade:
                                                 _lib.ptr(o3)), "nnsp_cascade_exec")
         return ran, det, o3
 
-    def exec_device(self, pcm_ptr: int, T: int, ran_ptr=None, det_ptr=None, o3_ptr=None) -> None:
-        _lib.check(_lib.lib().nnsp_cascade_exec_device(self.h, pcm_ptr, T, ran_ptr, det_ptr, o3_ptr),
-                   "nnsp_cascade_exec_device")
+    def exec_device(self, pcm_ptr: int, T: int, ran_ptr=None, det_ptr=None, o3_ptr=None,
+                    next_ptr: int | None = None, next_T: int = 0) -> None:
+        """Device buffers; next_ptr: the chunk the next call will get (its front
+        end then runs ahead, overlapped with this chunk's nets)."""
+        _lib.check(_lib.lib().nnsp_cascade_exec_device_ahead(self.h, pcm_ptr, T, next_ptr, next_T if next_ptr else 0,
+                                                             ran_ptr, det_ptr, o3_ptr), "nnsp_cascade_exec_device")
 
     def sync(self) -> None:
         _lib.check(_lib.lib().nnsp_cascade_sync(self.h), "nnsp_cascade_sync")
 
     def set_window(self, frames: int) -> None:
+        """Frames per stream and round (0: to the chunk end; -1: automatic)."""
         _lib.check(_lib.lib().nnsp_cascade_set_window(self.h, frames), "nnsp_cascade_set_window")
+
+    def window(self) -> tuple[int, bool, int]:
+        """(window of the next chunk, automatic?, net-switch cuts in the last chunk)"""
+        w, a, n = C.c_int(), C.c_int(), C.c_int()
+        _lib.check(_lib.lib().nnsp_cascade_get_window(self.h, C.byref(w), C.byref(a), C.byref(n)), "get_window")
+        return w.value, bool(a.value), n.value
 
     def set_serial(self, on: bool) -> None:
         """The nets' work of a round one after another on one stream (instrumentation)."""

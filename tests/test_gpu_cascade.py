@@ -116,3 +116,61 @@ def test_cascade_partial_reset():
     mask = np.zeros(S, np.uint8)
     mask[::3] = 1
     _check(oc, gc, _pcm(S, sum(chunks), 9), chunks, reset_at=2, reset_mask=mask)
+
+
+@pytest.mark.parametrize("weights", ["synth", "ref"])
+def test_cascade_lookahead_front_end(weights):
+    """nnsp_cascade_exec_device_ahead: the next chunk's shared front end runs
+    overlapped with this chunk's nets; results equal the oracle's, also when a
+    call receives a different chunk than the one announced (the look-ahead is
+    dropped and recomputed), after a partial reset, and with short chunks
+    (look-ahead off below look-back + 1 frames)."""
+    import torch
+
+    from nnsp_amd.nets import get_net
+    from oracle import load_wavs
+
+    torch.cuda.set_device(0)
+    S, Tm = 96, 100
+    chunks = [100, 100, 90, 100, 30, 100, 100]
+    announce = [1, 1, -1, 1, 1, 1, 1]   # -1: announce a different buffer than the next call gets
+    th = TH["lively"] if weights == "synth" else {n: (16383, 4) for n in ("vad", "kws", "s2i")}
+    onets, gnets = {}, {}
+    for name in ("vad", "kws", "s2i"):
+        data = get_net(name, weights)
+        onets[name] = OracleNet(data, thresh_prob=th[name][0], th_count=th[name][1])
+        gnets[name] = NNSPBatch(data, S, Tm, thresh_prob=th[name][0], th_count=th[name][1])
+    oc = OracleCascade(onets)
+    gc = NNSPCascade(gnets)
+    pcm = synthetic_pcm(S, sum(chunks), wavs=load_wavs(), every=1 if weights == "ref" else 4)
+    st = oc.new_states(S)
+    bufs, t0 = [], 0
+    for Tc in chunks:
+        bufs.append(torch.from_numpy(np.ascontiguousarray(pcm[:, t0:t0 + Tc])).to("cuda"))
+        t0 += Tc
+    decoy = torch.zeros_like(bufs[0])
+    ran = torch.empty((S, Tm), dtype=torch.int8, device="cuda")
+    det = torch.empty((S, Tm), dtype=torch.int16, device="cuda")
+    o3 = torch.empty((S, Tm, 3), dtype=torch.int16, device="cuda")
+    t0 = 0
+    for i, Tc in enumerate(chunks):
+        if i == 5:   # partial nnCntrlClass_reset: position kept
+            mask = (np.arange(S) % 4 == 1).astype(np.uint8)
+            gc.reset(mask)
+            for s in np.nonzero(mask)[0]:
+                pos = st[s, POS_OFF:POS_OFF + 2].copy()
+                lib().or_cascade_reset(C.c_void_p(st[s].ctypes.data), C.byref(oc.cfg))
+                st[s, POS_OFF:POS_OFF + 2] = pos
+        nxt = None
+        if i + 1 < len(chunks):
+            nxt = bufs[i + 1] if announce[i] > 0 else decoy
+        gc.exec_device(bufs[i].data_ptr(), Tc, ran.data_ptr(), det.data_ptr(), o3.data_ptr(),
+                       next_ptr=nxt.data_ptr() if nxt is not None else None,
+                       next_T=chunks[i + 1] if nxt is not None else 0)
+        gc.sync()
+        o_ran, o_det, o_o3, st = oc.run(pcm[:, t0:t0 + Tc], st)
+        np.testing.assert_array_equal(ran[:, :Tc].cpu().numpy(), o_ran, err_msg=f"net_ran chunk {i}")
+        np.testing.assert_array_equal(det[:, :Tc].cpu().numpy(), o_det, err_msg=f"detected chunk {i}")
+        np.testing.assert_array_equal(o3[:, :Tc].cpu().numpy(), o_o3, err_msg=f"outputs3 chunk {i}")
+        t0 += Tc
+    gc.close()
