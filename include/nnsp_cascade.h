@@ -42,7 +42,9 @@ typedef struct {
 /* nnCntrlClass_init: nets[NNSP_ID] (all with the same n_streams and a
  * max_frames the chunks will not exceed), seq = NNSP_ID per sequence position
  * (pt_seq_cntrl, len 1..8).  Every stream starts at position 0 with all nets
- * reset.  The nets stay owned by the caller and must outlive the cascade. */
+ * reset.  The nets stay owned by the caller and must outlive the cascade;
+ * their HIP streams (nnsp_batch_stream) carry the nets' rounds, so a batch of
+ * a cascade must not be run on its own while the cascade is in use. */
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq,
                         int len_seq, const nnsp_cascade_params *params);
 void nnsp_cascade_destroy(nnsp_cascade *c);
@@ -54,8 +56,8 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask);
 /* One chunk of T frames: pcm [S][T][160] int16.  Outputs per frame (NULL
  * skips): net_ran [S][T] int8 = NNSP_ID that ran, detected [S][T] int16 = its
  * NNSPClass_exec return, outputs3 [S][T][3] int16 = its NNSPClass.outputs.
- * _device: device pointers, work on nnsp_cascade_stream and the three net
- * streams forked from it.  The call returns once the chunk's rounds have
+ * _device: device pointers, work on nnsp_cascade_stream and the three nets'
+ * batch streams forked from it.  The call returns once the chunk's rounds have
  * finished on the device: the host reads back the list lengths of the round
  * after the last one it launched to decide whether more rounds are needed, so
  * it cannot queue the next chunk while this one runs. */

@@ -30,6 +30,9 @@ static int net_shape(const NnImage *g)
     if (L[0].K != 240 || L[0].act != 1 /* tanh */ || L[2].act != 0 /* relu6 */ || L[3].act != 0 ||
         L[4].act != 3 /* linear */)
         return NN_SHAPE_GENERIC;
+    /* the compiled recur adds the LSTM's input and recurrent halves in one
+     * accumulator: rc_Krows' shift of the input half must be 0 (qi_rec = qi) */
+    if (L[1].xs_sh != 0) return NN_SHAPE_GENERIC;
     const int N = L[1].N;
     if (L[0].N != N || L[1].K != N || L[2].K != N || L[2].N != N || L[3].K != N || L[3].N != N || L[4].K != N)
         return NN_SHAPE_GENERIC;
@@ -88,13 +91,19 @@ static void plan_fast(nnsp_batch *b)
         if (g->L[i].type == NN_LSTM) li = i;
     for (int i = li + 1; i < g->nl; ++i)
         if (g->L[i].N > 128 || g->L[i].K > 128) return;
-    const int a_proj = (int)g->L[li].ar_off;
-    const int a_rec = (int)(b->im.a_bytes - (size_t)g->L[li].ar_off);
-    /* epilogue rows: proj covers layers 0..li, recur li..nl-1 */
-    b->ep_proj = g->L[li].ep_off + 16 * g->L[li].nrt;
+    const int shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
+    /* compiled shapes: proj runs the layers before the LSTM and hands the
+     * LSTM's input x to recur, which stages the LSTM's input AND recurrent
+     * fragments; generic: proj also runs the input half (exact int32 gx) */
+    const int xmode = shape != NN_SHAPE_GENERIC;
+    const size_t rec_lo = xmode ? (size_t)g->L[li].a_off : (size_t)g->L[li].ar_off;
+    const int a_proj = xmode ? (int)g->L[li].a_off : (int)g->L[li].ar_off;
+    const int a_rec = (int)(b->im.a_bytes - rec_lo);
+    b->rec_a_off = (long long)rec_lo;
+    /* epilogue rows: proj covers layers 0..li (xmode: 0..li-1), recur li..nl-1 */
+    b->ep_proj = g->L[li].ep_off + (xmode ? 0 : 16 * g->L[li].nrt);
     b->ep_rec_lo = g->L[li].ep_off;
     b->ep_rec_n = b->im.rows_total - g->L[li].ep_off;
-    const int shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
     /* proj workgroups of 4 or 8 waves (they share the staged weights), whichever
      * keeps more waves per CU resident (LDS-bound) */
     int wpb = 4, per_cu = 0;
@@ -195,8 +204,13 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     b->ep32 = !b->im.img.acc32 && !getenv("NNSP_NO_EP32") && fits_int32(b, L, nl);
     if (b->fast) {
         if ((e = nnspk_set_lds_limit())) goto fail;
-        const size_t rows = (size_t)b->im.img.L[b->li].rows;
-        if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
+        if (b->shape != NN_SHAPE_GENERIC) { /* x rows: int16, 16 * ceil(N / 16) per (stream, step) */
+            const size_t xs = (size_t)(b->im.img.L[b->li].N + 15) / 16 * 16;
+            if ((e = nnspk_malloc((void **)&b->d_xg, S * (size_t)b->nstep_max * xs * 2))) goto fail;
+        } else {
+            const size_t rows = (size_t)b->im.img.L[b->li].rows;
+            if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
+        }
         if (getenv("NNSP_RECUR_CLOCKS")) { /* development probe of recur_kernel phases */
             if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 16 * 8))) goto fail;
             if ((e = nnspk_memset(b->d_clk, 0, 64 * 16 * 8, b->stream))) goto fail;
@@ -220,7 +234,7 @@ void nnsp_batch_destroy(nnsp_batch *b)
     if (b->stream) nnspk_sync(b->stream);
     nnsp_image_free(&b->im);
     void *bufs[] = {b->d_mean, b->d_stdR, b->d_tail, b->d_prev5, b->d_h, b->d_c, b->d_post,
-                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx, b->d_clk};
+                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx, b->d_xg, b->d_clk};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 3; ++i) nnspk_event_destroy(b->ev[i]);
     nnspk_stream_destroy(b->stream);
@@ -303,6 +317,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.prev5 = b->d_prev5;
         f.post = b->d_post;
         f.gx = b->d_gx;
+        f.xg = b->d_xg;
         f.h = b->d_h;
         f.c = b->d_c;
         f.trig = trig;
@@ -322,7 +337,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.ep32 = b->ep32;
         const NnLayer *LL = &b->im.img.L[b->li];
         f.a_off = 0;
-        f.a_lds_bytes = (int)LL->ar_off;
+        f.a_lds_bytes = (int)(b->shape != NN_SHAPE_GENERIC ? LL->a_off : LL->ar_off);
         f.ep_lo = 0;
         f.ep_n = b->ep_proj;
         f.n_list_dev = seg->n_list_dev;
@@ -340,8 +355,8 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             if (need < blocks) blocks = (int)need;
         }
         TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
-        f.a_off = LL->ar_off;
-        f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)LL->ar_off);
+        f.a_off = b->rec_a_off;
+        f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;
         f.ep_n = b->ep_rec_n;
         TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, seg->ctl, stream));

@@ -78,6 +78,9 @@ struct nnsp_cascade {
     void *ev_ahead[2];
     float ahead_ms, prev_ahead_ms;  /* look-ahead front end: this call's, the previous call's */
     int sfe_ahead;                  /* last chunk's shared front end ran in the previous call */
+    int ahead_blocks;               /* grid cap of the look-ahead front end (0: full) */
+    int ahead_fpw;                  /* its frames per wave (0: persistent grid) */
+    int ahead_after;                /* it starts after this many rounds of the nets */
     int window;                     /* frames per stream and round (0: to the chunk end) */
     int auto_window;                /* pick window per chunk from the last chunk's switch rate */
     int last_cuts;                  /* last chunk: segments cut by a net switch */
@@ -148,7 +151,12 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
     if ((e = nnspk_event_create(&c->ev_ahead[0])) || (e = nnspk_event_create(&c->ev_ahead[1]))) goto fail;
     for (int n = 0; n < 3; ++n) {
-        if ((e = nnspk_stream_create(&c->ns[n])) || (e = nnspk_event_create(&c->ev_join[n])) ||
+        /* each net's rounds run on its batch's own stream: the cascade adds
+         * one stream (c->stream) to the three, so on a device with four
+         * hardware queues (HIP's default) the look-ahead front end on
+         * c->stream never shares an in-order queue with a net's rounds */
+        c->ns[n] = nets[n]->stream;
+        if ((e = nnspk_event_create(&c->ev_join[n])) ||
             (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
             goto fail;
         for (int r = 0; r < MAX_TIMED; ++r)
@@ -244,6 +252,12 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         for (int i = 0; i < 3; ++i)
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
+        const char *ab = getenv("NNSP_AHEAD_FE_BLOCKS");
+        c->ahead_blocks = ab ? atoi(ab) : 0;
+        const char *af = getenv("NNSP_AHEAD_FE_FPW");
+        c->ahead_fpw = af ? atoi(af) : 0;
+        const char *aa = getenv("NNSP_AHEAD_AFTER_ROUND");
+        c->ahead_after = aa ? atoi(aa) : 1;
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
             c->window = atoi(w);
@@ -283,7 +297,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         nnspk_event_destroy(c->ev_rnd[1][n]);
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
-        nnspk_stream_destroy(c->ns[n]);
+        c->ns[n] = NULL; /* the batch's stream, owned by the batch */
     }
     nnspk_stream_destroy(c->stream);
     free(c);
@@ -415,10 +429,14 @@ static int join_rounds(nnsp_cascade *c, int r)
  * when T >= H) on the cascade's stream.  tail: the samples of the two frames
  * before the chunk, tail_stride apart per stream. */
 static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *tail, int tail_stride, int abs0,
-                     long long k)
+                     long long k, int ahead)
 {
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
+    if (ahead) {
+        fa.max_blocks = c->ahead_blocks;
+        fa.wave_frames = c->ahead_fpw;
+    }
     fa.pcm = pcm;
     fa.tail = tail;
     fa.tail_stride = tail_stride;
@@ -464,7 +482,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
     TRY(nnspk_event_record(c->ev_fe[0], c->stream));
-    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k));
+    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0));
     TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     c->sfe_ahead = ahead_done;
     a.counts = c->d_counts; /* round 0's lists */
@@ -478,18 +496,32 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
      * stream behind the fork -- it runs while the nets' rounds of this chunk
      * run on their streams (it writes ring slots and a history buffer this
      * chunk does not read; its STFT tail is this chunk's last two frames) */
-    const int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
-    if (ahead) {
-        TRY(nnspk_event_record(c->ev_ahead[0], c->stream));
-        TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring, k + 1));
-        TRY(nnspk_event_record(c->ev_ahead[1], c->stream));
-    }
+    int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
+    int ahead_launched = 0;
+    /* the look-ahead front end starts once the nets' first ahead_after rounds
+     * (the bulk of the chunk's NN work) are queued behind: running beside
+     * them from the start it slowed them more than it gained */
+#define LAUNCH_AHEAD()                                                                                         \
+    do {                                                                                                       \
+        TRY(nnspk_event_record(c->ev_ahead[0], c->stream));                                                    \
+        TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring,     \
+                      k + 1, 1));                                                                              \
+        TRY(nnspk_event_record(c->ev_ahead[1], c->stream));                                                    \
+        ahead_launched = 1;                                                                                    \
+    } while (0)
+    if (ahead && c->ahead_after <= 0) LAUNCH_AHEAD();
     /* rounds run without host round trips: launch as many as the last chunk
      * needed, then check the next round's list lengths (one read-back) */
     const int16_t *hist = c->d_hist[k % 3];
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
-        for (; r < R; ++r) TRY(launch_round(c, &a, r, pcm, T, hist));
+        for (; r < R; ++r) {
+            TRY(launch_round(c, &a, r, pcm, T, hist));
+            if (ahead && !ahead_launched && r + 1 >= c->ahead_after) {
+                for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[r & 1][n]));
+                LAUNCH_AHEAD();
+            }
+        }
         TRY(join_rounds(c, r));
         int32_t cnt[3];
         TRY(nnspk_d2h(cnt, c->d_counts + 6 * (r % 3), 12, c->stream));
@@ -505,6 +537,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     c->abs0 = (c->abs0 + T) % c->ring;
     c->chunk = k + 1;
+    ahead = ahead_launched;
     if (ahead) {
         c->pre_pcm = next_pcm;
         c->pre_T = next_T;

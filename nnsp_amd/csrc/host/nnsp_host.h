@@ -63,7 +63,9 @@ struct nnsp_batch {
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int shape;                        /* NN_SHAPE_* compiled split-path shape */
     int ep32;                         /* acc64 net that provably fits int32 accumulators */
-    int32_t *d_gx;
+    int32_t *d_gx;                    /* generic shape: proj -> recur exact Wx.x sums */
+    int16_t *d_xg;                    /* compiled shapes: proj -> recur LSTM inputs x */
+    long long rec_a_off;              /* first byte of the image recur stages into LDS */
     long long *d_clk; /* NNSP_RECUR_CLOCKS development probe */
 };
 

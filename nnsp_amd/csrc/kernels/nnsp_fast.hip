@@ -50,6 +50,7 @@ struct Shape {
     static constexpr bool generic = NRT_ == 0;
     static constexpr int NKR = NKR_, NRT = NRT_, R0 = R0_, R1 = R1_, R2 = R2_, R3 = R3_, NW = NW_, NOUT = NOUT_;
     static constexpr int RPW = (NRT_ + 3) / 4;
+    static constexpr int XS = (NW_ + 15) / 16 * 16;   // int16 per x row (proj -> recur, compiled shapes)
 };
 using ShapeGen = Shape<0, 0, 0, 0, 0, 0, 0, 0>;
 using ShapeVad = Shape<1, 7, 2, 2, 2, 1, 28, 2>;      // def_nn1_vad.c
@@ -69,7 +70,9 @@ struct EpRow {
     int64_t cst;
 };
 
-__device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, int n, bool recur) {
+// recur: the LSTM rows' constant covers the recurrent half (and, xsum, the
+// input half too: the compiled shapes' recur computes Wx.x itself)
+__device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, int n, bool recur, bool xsum = false) {
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int row = lo + i;
         int li = 0;
@@ -84,7 +87,8 @@ __device__ __forceinline__ void stage_ep(EpRow* ep, const NnImage& img, int lo, 
             else
                 bt = Ly.bias_sh >= 0 ? (int64_t)((uint64_t)(int64_t)b << Ly.bias_sh) : ((int64_t)b >> -Ly.bias_sh);
         }
-        const int32_t w = lstm && recur ? img.wsum_r[row] : img.wsum[row];
+        const int32_t w = lstm && recur ? (xsum ? wadd(img.wsum_r[row], img.wsum[row]) : img.wsum_r[row])
+                                        : img.wsum[row];
         ep[i].cst = img.acc32 ? (int64_t)wadd(w, (int32_t)bt) : (int64_t)w + bt;
     }
 }
@@ -255,6 +259,9 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PW& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
+    if constexpr (!GEN)   // x rows carry zeros past the LSTM input width N (fc_layer writes 0..N-1)
+        for (int c = lane; c < 16 * (PW::AS - SH::NW); c += 64)
+            P.act[0][c / (PW::AS - SH::NW)][SH::NW + c % (PW::AS - SH::NW)] = 0;
     const NnLayer& LL = img.L[r.li];
     const int nrt = GEN ? LL.nrt : SH::NRT;
     const int nkt = GEN ? LL.nkt : SH::NKR;
@@ -337,14 +344,27 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
         //      the per-lane base makes in + sc * in_stride that row)
         const int16_t* in = P.uni + kr * FR * 40 + 80 * jr - 80 * sc;
         int in_stride = 80;
-        if (!GEN) {   // one tanh FC layer, K = 240
+        if constexpr (!GEN) {   // one tanh FC layer, K = 240
             const NnLayer& L0 = img.L[0];
             fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
                                                           in, in_stride, &P.act[0][0][0], PW::AS, tt, lane);
             wave_lds_sync();
             PCLK(2);
-            in = &P.act[0][0][0];
-            in_stride = PW::AS;
+            // ---- the LSTM's input x of every row to HBM (int16, xs per row;
+            //      columns N..xs-1 are the zeros set at kernel start)
+            constexpr int XC = SH::XS / 8;   // 16-byte chunks per row
+            for (int c = lane; c < 16 * XC; c += 64) {
+                const int row = c / XC, part = c - row * XC;
+                const int kx = row / SPT, jx = row - kx * SPT;
+                const Seg g = seg_k(kx);
+                const int j = j0 + jx;
+                if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L)
+                    *reinterpret_cast<int4*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS + 8 * part) =
+                        *reinterpret_cast<const int4*>(&P.act[0][row][8 * part]);
+            }
+            wave_lds_sync();
+            PCLK(3);
+            continue;
         } else {
             for (int i = 0; i < r.li; ++i) {
                 const NnLayer& Ly = img.L[i];
@@ -356,8 +376,8 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
                 in_stride = PW::AS;
             }
         }
-        // ---- LSTM input half: gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
-        {
+        // ---- LSTM input half (generic shape): gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
+        if constexpr (GEN) {
             v4i bh[2], bl[2];
             load_b<2>(in, in_stride, nkt, lane, bh, bl);
             const uint8_t* A = W + (LL.a_off - r.a_off);
@@ -696,7 +716,9 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
 // ---------------------------------------------------------------------------
 template <class SH>
 struct PipeCfg {
-    static constexpr int LW = SH::NRT <= 8 ? 4 : (SH::NRT + 1) / 2;   // LSTM waves: <= 2 row tiles each
+    // LSTM waves: <= 2 row tiles each (4 tiles each on 4 waves would let KWS's
+    // workgroups fit two per CU, but spills ~250 B per lane at 128 VGPRs)
+    static constexpr int LW = SH::NRT <= 8 ? 4 : (SH::NRT + 1) / 2;
     static constexpr int RPW = (SH::NRT + LW - 1) / LW;      // LSTM row tiles per wave
     // the last FC layer and the post-processing on waves of their own (a
     // 5-stage pipeline) for the 2-output nets; S2I keeps them on one wave: a
@@ -704,6 +726,9 @@ struct PipeCfg {
     // than the split gains (profiles/recur_clocks.py)
     static constexpr int SPLIT = SH::NOUT <= 2 ? 1 : 0;
     static constexpr int NWV = LW + 3 + SPLIT;               // waves per workgroup
+    // waves per SIMD the register budget must allow: two workgroups per CU
+    // when a workgroup has <= 8 waves (VAD: <= 128 VGPRs), else one
+    static constexpr int MINW = NWV <= 8 ? 2 * ((NWV + 3) / 4) : (NWV + 3) / 4;
     static_assert(NWV <= 12, "recur_pipe_kernel: at most 3 waves per SIMD");
 };
 
@@ -731,7 +756,8 @@ struct alignas(16) PipeTile {
 // (NNSPClass_reset) instead of the carried one, and the stream is listed for
 // its next net -- what casc_control_kernel does after the kernel otherwise.
 template <class SH, bool ACC32>
-__global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRun r, CascArgs ca) {
+__global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
+                                                                                            CascArgs ca) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CF = PipeCfg<SH>;
     using PT = PipeTile<SH>;
@@ -749,7 +775,7 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
     PT& R = *reinterpret_cast<PT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
-    stage_ep(ep, img, r.ep_lo, r.ep_n, true);
+    stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     const int lane = threadIdx.x & 63;
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // < RGP: LSTM wave; then stages 1..3
@@ -758,8 +784,9 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
     const bool valid = i0 + sc < nrow;
     const int s = valid ? sid(i0 + sc) : 0;
     const NnLayer& LL = img.L[r.li];
-    constexpr int rows = 16 * nrt;
-    const int xs_sh = LL.xs_sh, rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
+    // compiled shapes have xs_sh == 0 (net_shape): the input and recurrent
+    // halves of a gate share one MFMA accumulator
+    const int rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
     for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
         const int st = idx / N, u = idx - st * N;
         const bool ok = i0 + st < nrow;
@@ -795,19 +822,52 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
         put_frame(r, s, T, b, ps);
         if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
     }
-    const uint8_t* Ar = W;   // LSTM recurrent fragments lead the staged region
+    // staged region: the LSTM's input fragments, then its recurrent ones, then the FC tail
+    const uint8_t* Ax = W;
+    const uint8_t* Ar = W + (LL.ar_off - LL.a_off);
     const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
-    v4i gxv[RPW];
-    auto load_gx = [&](int jj) {
+    // the input half Wx.x of the NEXT step is computed at the end of each
+    // step (off the recurrence's critical path) into the accumulators the
+    // recurrent half then starts from; its x rows come from proj through HBM
+    constexpr int XS = SH::XS;
+    v4i axh[RPW], axl[RPW];
+    int4 xr[nkt_r][2];
+    auto load_x = [&](int jj) {   // raw x of step jj for the lane's stream (B-fragment layout)
         const bool ok = valid && b + 2 * jj + phase < e;
-        const int32_t* gsrc = r.gx + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * rows + 4 * q;
+        const int16_t* src = r.xg + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * XS;
 #pragma unroll
-        for (int k = 0; k < RPW; ++k) {
-            const int rt = g + RGP * k;
-            if (rt < nrt) gxv[k] = *reinterpret_cast<const v4i*>(gsrc + 16 * rt);
+        for (int kt = 0; kt < nkt_r; ++kt) {   // branch-free: lanes past the row load column 0, then zero
+            const int k0 = 64 * kt + 16 * q;
+            const bool in = k0 < XS;
+            const int16_t* p = src + (in ? k0 : 0);
+            const int4 lo = *reinterpret_cast<const int4*>(p), hi = *reinterpret_cast<const int4*>(p + 8);
+            const int4 z = make_int4(0, 0, 0, 0);
+            xr[kt][0] = in ? lo : z;
+            xr[kt][1] = in ? hi : z;
         }
     };
-    if (g < RGP) load_gx(0);
+    auto x_half = [&]() {   // axh/axl := Wx . x (hi / lo planes) from xr
+        v4i bxh[nkt_r], bxl[nkt_r];
+#pragma unroll
+        for (int kt = 0; kt < nkt_r; ++kt) split_hilo_r(xr[kt][0], xr[kt][1], bxh[kt], bxl[kt]);
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {   // one row tile's fragments at a time (no LDS stores here)
+            axh[k] = v4i{0, 0, 0, 0};
+            axl[k] = v4i{0, 0, 0, 0};
+            if (g + RGP * k < nrt)
+#pragma unroll
+                for (int kt = 0; kt < nkt_r; ++kt) {
+                    const v4i wx = *reinterpret_cast<const v4i*>(Ax + (size_t)((g + RGP * k) * nkt_r + kt) * 1024 + 16 * lane);
+                    axh[k] = mfma8(wx, bxh[kt], axh[k]);
+                    axl[k] = mfma8(wx, bxl[kt], axl[k]);
+                }
+        }
+    };
+    if (g < RGP && nsteps > 0) {
+        load_x(0);
+        x_half();
+        if (nsteps > 1) load_x(1);
+    }
     const NnLayer& L2 = img.L[r.li + 1];
     const NnLayer& L3 = img.L[r.li + 2];
     const NnLayer& L4 = img.L[r.li + 3];
@@ -854,8 +914,8 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                 v4i hh[RPW], hl[RPW];
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
-                    hh[k] = v4i{0, 0, 0, 0};
-                    hl[k] = v4i{0, 0, 0, 0};
+                    hh[k] = axh[k];   // the input half, computed at the end of the previous step
+                    hl[k] = axl[k];
                     if (g + RGP * k < nrt)
 #pragma unroll
                         for (int kt = 0; kt < nkt_r; ++kt) {
@@ -874,16 +934,13 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                         int16_t gt[4];
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {
-                            const int32_t sx = gxv[k][i];
+                            // exact Wx.x + Wh.h (|.| < 2^31 for N <= 128: int32)
                             const int32_t hx = (hh[k][i] << 8) + hl[k][i];
                             int32_t v;
                             if (ACC32) {
-                                const int32_t x = __builtin_expect(xs_sh != 0, 0) ? shift32(sx, xs_sh) : sx;
-                                v = ep_out<true>(wadd(x, hx), cst[k][i], rsh, lsh);
+                                v = ep_out<true>(hx, cst[k][i], rsh, lsh);
                             } else {
-                                const int64_t x = __builtin_expect(xs_sh != 0, 0) ? shift64((int64_t)sx, xs_sh)
-                                                                                  : (int64_t)sx;
-                                const int64_t pre = x + hx + cst[k][i];
+                                const int64_t pre = (int64_t)hx + cst[k][i];
                                 v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                             }
                             gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
@@ -901,7 +958,10 @@ __global__ __launch_bounds__(64 * 12) void recur_pipe_kernel(NnImage img, FastRu
                         R.h[cur ^ 1][sc][u] = active ? hv[k] : h_old[k];   // h after all groups (T6)
                     }
                 }
-                if (j + 1 < nsteps) load_gx(j + 1);
+                if (j + 1 < nsteps) {   // the next step's input half, then its successor's x
+                    x_half();
+                    if (j + 2 < nsteps) load_x(j + 2);
+                }
             }
         } else if (g == RGP) {   // stage 1: step j-1
             if (j >= 1 && j - 1 < nsteps)

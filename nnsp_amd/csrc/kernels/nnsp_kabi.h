@@ -61,7 +61,10 @@ typedef struct {
     int16_t *hist_out;
     int32_t tail_stride;      /* samples between streams' tails (0: 320, a [S][320] buffer; a chunk's
                                  last two frames: T * 160) */
-    int32_t pad_;
+    int32_t max_blocks;       /* > 0: cap on the grid */
+    int32_t wave_frames;      /* > 0: frames per wave (short-lived workgroups: a look-ahead front end
+                                 yields CU slots to the nets' kernels as it goes); 0: persistent grid */
+    int32_t pad2_;
 } FeArgs;
 
 /* Cascade: where a net's segment features come from -- the shared log-Mel
@@ -146,6 +149,10 @@ typedef struct {
     int32_t *n_list_rec;      /* non-NULL: proj records the list length it ran with (stats) */
     FeatSrc fs;               /* cascade feature source (fs.lmel NULL: feats) */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
+    /* compiled shapes: proj writes the LSTM's input x (the prefix layers'
+     * int16 output, [S][nstep_max][xs] with xs = 16 * ceil(N / 16)) instead of
+     * the int32 gate sums gx; recur computes Wx.x itself on MFMA */
+    int16_t *xg;
 } FastRun;
 
 /* Legacy row-block primitives (affine_Krows_8x16*, rc_Krows_8x16*, rc_8x16*):
@@ -218,6 +225,9 @@ int nnspk_set_device(int d);
 int nnspk_get_device(int *d);
 const char *nnspk_error_string(int e);
 int nnspk_stream_create(void **s);
+/* high != 0: the device's greatest stream priority (its kernels' workgroups
+ * are dispatched ahead of normal-priority streams' when both wait) */
+int nnspk_stream_create_prio(void **s, int high);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);

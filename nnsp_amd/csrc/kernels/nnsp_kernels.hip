@@ -920,6 +920,8 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
         return e && atoll(e) > 0 ? atoll(e) : 256LL * 6 * 4;
     }();
     if (blocks > cap) blocks = cap;
+    if (a->wave_frames > 0) blocks = (nfr + 4LL * a->wave_frames - 1) / (4LL * a->wave_frames);
+    if (a->max_blocks > 0 && blocks > a->max_blocks) blocks = a->max_blocks;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
@@ -1052,6 +1054,12 @@ int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
 const char* nnspk_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 int nnspk_stream_create(void** s) { return ok(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); }
+int nnspk_stream_create_prio(void** s, int high) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return (int)e;
+    return ok(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
+}
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }

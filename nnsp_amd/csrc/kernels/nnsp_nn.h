@@ -24,6 +24,19 @@ __device__ __forceinline__ void split_hilo(const int16_t* p, v4i& hi, v4i& lo) {
     lo.w = (int)(__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, LS) ^ 0x80808080u);
 }
 
+// the same from 16 int16 already in registers (a: elements 0..7, b: 8..15)
+__device__ __forceinline__ void split_hilo_r(int4 a, int4 b, v4i& hi, v4i& lo) {
+    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
+    hi.x = (int)__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, HS);
+    hi.y = (int)__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, HS);
+    hi.z = (int)__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, HS);
+    hi.w = (int)__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, HS);
+    lo.x = (int)(__builtin_amdgcn_perm((uint32_t)a.y, (uint32_t)a.x, LS) ^ 0x80808080u);
+    lo.y = (int)(__builtin_amdgcn_perm((uint32_t)a.w, (uint32_t)a.z, LS) ^ 0x80808080u);
+    lo.z = (int)(__builtin_amdgcn_perm((uint32_t)b.y, (uint32_t)b.x, LS) ^ 0x80808080u);
+    lo.w = (int)(__builtin_amdgcn_perm((uint32_t)b.w, (uint32_t)b.z, LS) ^ 0x80808080u);
+}
+
 __device__ __forceinline__ v4i mfma8(v4i a, v4i b, v4i c) {
     return __builtin_amdgcn_mfma_i32_16x16x64_i8(a, b, c, 0, 0, 0);
 }

@@ -169,8 +169,12 @@ def test_cascade_lookahead_front_end(weights):
                        next_T=chunks[i + 1] if nxt is not None else 0)
         gc.sync()
         o_ran, o_det, o_o3, st = oc.run(pcm[:, t0:t0 + Tc], st)
-        np.testing.assert_array_equal(ran[:, :Tc].cpu().numpy(), o_ran, err_msg=f"net_ran chunk {i}")
-        np.testing.assert_array_equal(det[:, :Tc].cpu().numpy(), o_det, err_msg=f"detected chunk {i}")
-        np.testing.assert_array_equal(o3[:, :Tc].cpu().numpy(), o_o3, err_msg=f"outputs3 chunk {i}")
+        # outputs are [S][T] of this call's T (the buffers hold Tm frames per stream)
+        g_ran = ran.view(-1)[:S * Tc].view(S, Tc).cpu().numpy()
+        g_det = det.view(-1)[:S * Tc].view(S, Tc).cpu().numpy()
+        g_o3 = o3.view(-1)[:S * Tc * 3].view(S, Tc, 3).cpu().numpy()
+        np.testing.assert_array_equal(g_ran, o_ran, err_msg=f"net_ran chunk {i}")
+        np.testing.assert_array_equal(g_det, o_det, err_msg=f"detected chunk {i}")
+        np.testing.assert_array_equal(g_o3, o_o3, err_msg=f"outputs3 chunk {i}")
         t0 += Tc
     gc.close()
