@@ -22,11 +22,20 @@
  *      the look-back and the cold frames read was stored by step 1).
  * The host reads back three list lengths per batch of rounds and nothing else.
  */
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "../../../include/nnsp_cascade.h"
 #include "nnsp_host.h"
+
+/* NNSP_CASCADE_DEBUG: after each launch, wait for the stream and report
+ * which launch failed (asynchronous faults otherwise surface at a later sync) */
+static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n, int r);
+#define DBG(st, what, n, r)                                  \
+    do {                                                     \
+        if (c->debug) TRY(dbg_step(c, (st), (what), (n), (r))); \
+    } while (0)
 
 #define TRY(x)                 \
     do {                       \
@@ -54,7 +63,8 @@ struct nnsp_cascade {
     int16_t *d_hist[3];             /* PCM history before chunk k: d_hist[k % 3] (the look-ahead
                                        front end of chunk k+1 writes d_hist[(k + 2) % 3]) */
     long long chunk;                /* chunks run since create */
-    int32_t *d_lmel;                /* [S][ring][40] shared log-Mel */
+    int debug;                      /* NNSP_CASCADE_DEBUG: synchronise after every launch, name the failing one */
+    int16_t *d_nring[3];            /* per net id: [S][ring][40] normalised shared front-end output */
     int ring, abs0;                 /* ring slots (>= H + Tmax); slot of chunk frame 0 */
     int16_t *d_stail;               /* [S][320] PCM tail of the shared front end */
     int8_t *d_fresh;                /* [S] frames the current net ran since its reset */
@@ -174,7 +184,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_lmel, S * (size_t)c->ring * 40 * 4))) goto fail;
+    for (int i = 0; i < 3; ++i)
+        if ((e = nnspk_malloc((void **)&c->d_nring[i], S * (size_t)c->ring * 40 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_fresh, S))) goto fail;
     for (int i = 0; i < 3; ++i) {
@@ -215,13 +226,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             a->list[i] = c->d_list[0][i]; /* round 0 (casc_begin); set per round */
             a->cold_list[i] = c->d_cold_list[0][i];
             FeatSrc *fs = &a->fs[i];
-            fs->lmel = c->d_lmel;
+            fs->nring = c->d_nring[i];
             fs->fresh = c->d_fresh;
-            fs->mean = nets[i]->d_mean;
-            fs->stdR = nets[i]->d_stdR;
             fs->ring = c->ring;
             fs->lookback = c->lookback[i];
-            fs->norm_shift = nets[i]->norm_shift;
         }
     }
     {   /* the reset context value of each net: FeatureClass_setDefault on a scratch stream */
@@ -252,6 +260,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         for (int i = 0; i < 3; ++i)
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
+        c->debug = getenv("NNSP_CASCADE_DEBUG") != NULL;
         const char *ab = getenv("NNSP_AHEAD_FE_BLOCKS");
         c->ahead_blocks = ab ? atoi(ab) : 0;
         const char *af = getenv("NNSP_AHEAD_FE_FPW");
@@ -279,7 +288,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_zero,    c->d_trig[0], c->d_trig[1],
                     c->d_trig[2], c->d_mask[0],   c->d_mask[1],
                     c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1], c->d_hist[2],
-                    c->d_lmel,    c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
+                    c->d_nring[0], c->d_nring[1], c->d_nring[2], c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
                     c->d_ran,     c->d_pdef,      c->d_cold_list[0][0],
                     c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
                     c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2]};
@@ -317,7 +326,16 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
     TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->chunk % 3], c->H, c->d_stail, c->d_fresh, dm, c->S,
                                 c->stream));
     /* PcmBufClass_reset: every look-back frame is silence */
-    TRY(nnspk_launch_lmel_fill(c->d_lmel, c->ring, dm, c->S, c->stream));
+    {
+        const int32_t *mn[3], *sd[3];
+        int32_t sh[3];
+        for (int n = 0; n < 3; ++n) {
+            mn[n] = c->net[n]->d_mean;
+            sd[n] = c->net[n]->d_stdR;
+            sh[n] = c->net[n]->norm_shift;
+        }
+        TRY(nnspk_launch_nring_fill(c->d_nring, mn, sd, sh, c->ring, dm, c->S, c->stream));
+    }
     if (mask) TRY(nnspk_memset(c->d_mask[0], 0, (size_t)c->S, c->stream));
     return nnspk_sync(c->stream);
 }
@@ -325,6 +343,17 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 /* features of net n for this round's segments: the full front end for the
  * frames right after the net's reset (the others are normalised from the
  * shared log-Mel by the kernels that read them, FeatSrc) */
+static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n, int r)
+{
+    (void)c;
+    const int e = nnspk_sync(stream);
+    if (e) {
+        fprintf(stderr, "nnsp_cascade: %s (net %d, round %d) failed: %s\n", what, n, r, nnspk_error_string(e));
+        nnsp_set_error("nnsp_cascade: %s (net %d, round %d) failed", what, n, r);
+    }
+    return e;
+}
+
 static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, int T, const int32_t *cnt,
                             const int16_t *hist, void *stream)
 {
@@ -347,7 +376,6 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     fa.seg_len = c->window;
     fa.ring = c->ring;
     fa.abs0 = c->abs0;
-    fa.lmel = c->d_lmel;
     fa.fresh = c->d_fresh;
     fa.mode = FE_MODE_COLD;
     fa.list = c->d_cold_list[r & 1][n];
@@ -386,6 +414,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         }
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
         TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
+        DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
         nnsp_segment seg;
         memset(&seg, 0, sizeof seg);
@@ -404,6 +433,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
         seg.ctl = c->fused ? a : NULL;
         TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
+        DBG(st, "proj + recur", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
         if (c->fused) {
             TRY(nnspk_event_record(c->ev_rnd[r & 1][n], st));
@@ -447,7 +477,12 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     fa.mode = FE_MODE_SHARED;
     fa.ring = c->ring;
     fa.abs0 = abs0;
-    fa.lmel = c->d_lmel;
+    for (int n = 0; n < 3; ++n) {
+        fa.nring[n] = c->d_nring[n];
+        fa.nmean[n] = c->net[n]->d_mean;
+        fa.nstdR[n] = c->net[n]->d_stdR;
+        fa.nshift[n] = c->net[n]->norm_shift;
+    }
     if (T >= c->H) { /* the next chunk's look-back history, stored by the front end */
         fa.hist_out = c->d_hist[(k + 1) % 3];
         fa.hist_frames = c->H;
@@ -483,6 +518,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     c->pre_pcm = NULL;
     TRY(nnspk_event_record(c->ev_fe[0], c->stream));
     if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0));
+    DBG(c->stream, "shared front end", -1, -1);
     TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     c->sfe_ahead = ahead_done;
     a.counts = c->d_counts; /* round 0's lists */
@@ -491,6 +527,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         a.cold_list[n] = c->d_cold_list[0][n];
     }
     TRY(nnspk_launch_casc_begin(&a, c->stream));
+    DBG(c->stream, "casc_begin", -1, -1);
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
     /* look-ahead: the next chunk's shared front end, queued on the cascade's
      * stream behind the fork -- it runs while the nets' rounds of this chunk

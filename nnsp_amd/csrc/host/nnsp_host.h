@@ -81,7 +81,7 @@ typedef struct {
     int seg_len;              /* > 0: segments end at min(T, seg_begin + seg_len) */
     const int32_t *n_list_dev; /* non-NULL: list length on the device (overrides n_list) */
     int32_t *n_list_rec;       /* non-NULL: the list length proj ran with is recorded there */
-    FeatSrc fs;                /* cascade feature source (fs.lmel NULL: the batch's feats) */
+    FeatSrc fs;                /* cascade feature source (fs.nring NULL: the batch's feats) */
     int8_t *net_ran;           /* cascade: the caller's per-frame outputs (NULL skips) */
     int16_t *detected, *outputs3;
     int net_id;

@@ -43,15 +43,19 @@ typedef struct {
     const int16_t *hist;
     int32_t n_list, lookback, hist_frames;
     int32_t seg_len;          /* > 0: a segment ends at min(T, seg_begin + seg_len) */
-    /* cascade modes (FE_MODE_*): SHARED writes the log-Mel of every frame of
-     * every stream (no normalisation) into the ring lmel [S][ring][40], chunk
-     * frame t at slot (abs0 + t) % ring; COLD runs only the frames of a listed
-     * segment that come less than 2 frames after the net's reset (fresh[s] =
-     * frames the net ran since its reset, 0..2): input frames before the reset
-     * point are zero (stftModule_setDefault), the rest come from pcm/hist */
+    /* cascade modes (FE_MODE_*): SHARED computes the log-Mel of every frame of
+     * every stream once and writes it normalised with each net's mean / stdR
+     * (feature_module.c:67-73) into that net's ring nring[n] [S][ring][40]
+     * int16, chunk frame t at slot (abs0 + t) % ring; COLD runs only the
+     * frames of a listed segment that come less than 2 frames after the net's
+     * reset (fresh[s] = frames the net ran since its reset, 0..2): input frames
+     * before the reset point are zero (stftModule_setDefault), the rest come
+     * from pcm/hist */
     int32_t mode;
     int32_t ring, abs0;
-    int32_t *lmel;
+    int16_t *nring[3];
+    const int32_t *nmean[3], *nstdR[3];
+    int32_t nshift[3];
     const int8_t *fresh;
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device */
     /* FE_MODE_SHARED, non-NULL: the PCM of the chunk's last hist_frames frames
@@ -67,15 +71,14 @@ typedef struct {
     int32_t pad2_;
 } FeArgs;
 
-/* Cascade: where a net's segment features come from -- the shared log-Mel
- * ring normalised on the fly with the net's mean / stdR (feature_module.c:
- * 67-73), except the frames within 2 frames of the net's reset, which the
- * cold front end (FE_MODE_COLD) wrote to the net's feats buffer. */
+/* Cascade: where a net's segment features come from -- its ring of the shared
+ * front end's normalised output, except the frames within 2 frames of the
+ * net's reset, which the cold front end (FE_MODE_COLD) wrote to the net's
+ * feats buffer. */
 typedef struct {
-    const int32_t *lmel;      /* [S][ring][40]; NULL: every frame from feats */
+    const int16_t *nring;     /* the net's normalised ring [S][ring][40]; NULL: every frame from feats */
     const int8_t *fresh;      /* [S] frames the net ran since its reset, at the segment start */
-    const int32_t *mean, *stdR;
-    int32_t ring, abs0, lookback, norm_shift;
+    int32_t ring, abs0, lookback, pad;
 } FeatSrc;
 
 #define FE_MODE_BATCH 0
@@ -147,7 +150,7 @@ typedef struct {
     int32_t net_id;
     int32_t gpt;              /* proj: streams per 16-row tile (1, 2 or 4; compiled shapes) */
     int32_t *n_list_rec;      /* non-NULL: proj records the list length it ran with (stats) */
-    FeatSrc fs;               /* cascade feature source (fs.lmel NULL: feats) */
+    FeatSrc fs;               /* cascade feature source (fs.nring NULL: feats) */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
     /* compiled shapes: proj writes the LSTM's input x (the prefix layers'
      * int16 output, [S][nstep_max][xs] with xs = 16 * ceil(N / 16)) instead of
@@ -183,8 +186,10 @@ typedef struct {
 
 /* launch layer (nnsp_kernels.hip) */
 int nnspk_launch_fe(const FeArgs *a, void *stream);
-/* cascade reset: ring slots of the masked streams := log-Mel of silence */
-int nnspk_launch_lmel_fill(int32_t *lmel, int ring, const uint8_t *mask, int S, void *stream);
+/* cascade reset: ring slots of the masked streams := each net's normalised
+ * log-Mel of silence */
+int nnspk_launch_nring_fill(int16_t *const nring[3], const int32_t *const nmean[3], const int32_t *const nstdR[3],
+                            const int32_t nshift[3], int ring, const uint8_t *mask, int S, void *stream);
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
 int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
                           int n_list, const int32_t *seg_begin, int seg_len, void *stream);

@@ -47,21 +47,32 @@ struct FeLane {
 // Block-shared constant tables (LDS).
 struct FeTables {
     int2 tw[3][3][64];    // per stage, twiddle (k, 2k, 3k) of each lane's butterfly: (cos, sin)
-    int4 split[256];      // per bin k: (A_re, A_im, B_re, 0) of realCoefA/BQ31 at 16k
+    int4 split[256];      // per bin k: (A_re, A_im, B_re, nv) of realCoefA/BQ31 at 16k; nv: in
+                          // FE_MODE_SHARED, k < 120 net k/40's mean of Mel bank k%40,
+                          // 120 <= k < 240 its stdR (fe_norm_word); otherwise 0
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
     uint4 win[64];        // per lane: window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
     uint2 mc[3][64];      // per lane: Mel segment coefficients as int16 pairs (LDS, not VGPRs:
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
-};
+};   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
 
-__device__ __forceinline__ void fe_tables_init(FeTables& T) {
+// the per-net normalisation constants ride in split[].w: a separate table
+// would push fe_kernel's LDS past 160 KB / 6 and cost a workgroup per CU
+__device__ __forceinline__ int32_t fe_norm_word(const FeArgs& a, int k) {
+    if (a.mode != FE_MODE_SHARED || k >= 240) return 0;
+    const int n = (k % 120) / 40, b = k % 40;
+    if (!a.nring[n]) return 0;
+    return k < 120 ? a.nmean[n][b] : a.nstdR[n][b];
+}
+
+__device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
     for (int i = threadIdx.x; i < 576; i += blockDim.x) {
         const int s = i / 192, j = (i / 64) % 3, l = i % 64;
         const int k = s == 0 ? l : (s == 1 ? 4 * (l & 15) : 16 * (l >> 4));
         T.tw[s][j][l] = make_int2(nnsp_tbl_tw256[2 * (j + 1) * k], nnsp_tbl_tw256[2 * (j + 1) * k + 1]);
     }
     for (int k = threadIdx.x; k < 256; k += blockDim.x)
-        T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
+        T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], fe_norm_word(a, k));
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
     if (threadIdx.x < 64) {
@@ -187,6 +198,9 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // runs a contiguous range of frames (consecutive frames of a stream re-read
 // two thirds of their window from L1/L2) and prefetches the next frame's PCM.
 // (256, 6): at most 80 VGPRs, six waves per SIMD (window and Mel coefficients in LDS)
+// One instantiation per mode (FE_MODE_*): the batch and cold modes keep the
+// 80-VGPR budget of six waves per SIMD without the shared mode's ring writes.
+template <int MODE>
 __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
@@ -194,13 +208,14 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) FeTables TB;
     const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
     const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
-    const bool cold = a.mode == FE_MODE_COLD;
+    constexpr bool cold = MODE == FE_MODE_COLD;
+    constexpr bool shared = MODE == FE_MODE_SHARED;
     const unsigned W = cold ? (segW < 2u ? segW : 2u) : segW;
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
     const unsigned nw = gridDim.x * 4u;
     const unsigned per = (nfr + nw - 1) / nw;
     if (blockIdx.x * 4u * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
-    fe_tables_init(TB);
+    fe_tables_init(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = Xs[wv];
@@ -269,7 +284,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(p2 + 64 + o) : 0u;
     };
     if (fbeg >= fend) return;
-    const unsigned ring0 = a.mode == FE_MODE_SHARED ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
+    const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
     Pos nx;
     nx.i = fbeg / W;
     nx.k = fbeg - nx.i * W;
@@ -361,11 +376,19 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 if (k < L.mcnt) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
             if (a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
-            if (a.mode == FE_MODE_SHARED) {
+            if constexpr (shared) {
                 // (abs0 + t) % ring with t < T <= ring: one conditional subtract
                 unsigned slot = ring0 + (unsigned)t;
                 if (slot >= (unsigned)a.ring) slot -= (unsigned)a.ring;
-                a.lmel[((size_t)s * a.ring + slot) * 40 + lane] = lg;
+                const unsigned o = ((unsigned)s * (unsigned)a.ring + slot) * 40u + (unsigned)lane;   // < 2^31 (host)
+                // keep the (mean, stdR) LDS reads here: hoisted out of the frame
+                // loop they would pin 6 VGPRs and cost a wave per SIMD
+                __asm__ volatile("" ::: "memory");
+#pragma unroll
+                for (int n = 0; n < 3; ++n) {   // each net's normalisation (feature_module.c:67-73)
+                    const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
+                    a.nring[n][o] = sat16(mad_i64_i32(wsub(lg, mn), sr, 0) >> a.nshift[n]);
+                }
             } else {
                 const int64_t d = (int64_t)lg - mean;
                 a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
@@ -641,12 +664,25 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
     for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
 }
 
-// log-Mel of silence: mel 0 -> log10_vec's x == 0 -> 1 (fixlog10.c:56)
-__global__ __launch_bounds__(256) void lmel_fill_kernel(int32_t* lmel, int ring, const uint8_t* mask, int S) {
+// each net's normalised log-Mel of silence: mel 0 -> log10_vec's x == 0 -> 1
+// (fixlog10.c:56), then feature_module.c:67-73
+struct NringFill {
+    int16_t* nring[3];
+    const int32_t* nmean[3];
+    const int32_t* nstdR[3];
+    int32_t nshift[3];
+};
+__global__ __launch_bounds__(256) void nring_fill_kernel(NringFill f, int ring, const uint8_t* mask, int S) {
     const int s = blockIdx.x;
     if (s >= S || (mask && !mask[s])) return;
-    const int32_t v = log10_q15(0);
-    for (int i = threadIdx.x; i < ring * 40; i += blockDim.x) lmel[(size_t)s * ring * 40 + i] = v;
+    const int32_t lg = log10_q15(0);
+    for (int n = 0; n < 3; ++n) {
+        if (!f.nring[n]) continue;
+        for (int i = threadIdx.x; i < ring * 40; i += blockDim.x) {
+            const int b = i % 40;
+            f.nring[n][(size_t)s * ring * 40 + i] = sat16((((int64_t)lg - f.nmean[n][b]) * f.nstdR[n][b]) >> f.nshift[n]);
+        }
+    }
 }
 
 // ============================================================================
@@ -655,7 +691,9 @@ __global__ __launch_bounds__(256) void lmel_fill_kernel(int32_t* lmel, int ring,
 __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
     __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW];
     __shared__ __attribute__((aligned(16))) FeTables TB;
-    fe_tables_init(TB);
+    FeArgs none{};
+    none.mode = FE_MODE_BATCH;
+    fe_tables_init(TB, none);
     const int lane = threadIdx.x;
     __syncthreads();
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
@@ -925,7 +963,12 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
-    hipLaunchKernelGGL(fe_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    if (a->mode == FE_MODE_SHARED)
+        hipLaunchKernelGGL(fe_kernel<FE_MODE_SHARED>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    else if (a->mode == FE_MODE_COLD)
+        hipLaunchKernelGGL(fe_kernel<FE_MODE_COLD>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    else
+        hipLaunchKernelGGL(fe_kernel<FE_MODE_BATCH>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
     return ok(hipGetLastError());
 }
 
@@ -941,9 +984,17 @@ int nnspk_launch_shift(void* x, int shift, int n, int acc32, void* stream) {
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_lmel_fill(int32_t* lmel, int ring, const uint8_t* mask, int S, void* stream) {
+int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[3], const int32_t* const nstdR[3],
+                            const int32_t nshift[3], int ring, const uint8_t* mask, int S, void* stream) {
     if (S <= 0) return 0;
-    hipLaunchKernelGGL(lmel_fill_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, lmel, ring, mask, S);
+    NringFill f;
+    for (int n = 0; n < 3; ++n) {
+        f.nring[n] = nring[n];
+        f.nmean[n] = nmean[n];
+        f.nstdR[n] = nstdR[n];
+        f.nshift[n] = nshift[n];
+    }
+    hipLaunchKernelGGL(nring_fill_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, f, ring, mask, S);
     return ok(hipGetLastError());
 }
 

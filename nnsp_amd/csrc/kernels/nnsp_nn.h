@@ -63,24 +63,25 @@ __device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) 
 }
 
 // 8 features [8*part, 8*part + 8) of stream s at chunk frame t of a segment
-// starting at b: from the net's feats buffer, or the shared log-Mel ring
-// normalised on the fly (cascade; the 2 frames after a reset come from feats)
+// starting at b: from the net's feats buffer, or (cascade) from the net's
+// ring of the shared front end's normalised output, except the 2 frames after
+// a reset, which the cold front end wrote to feats
+//
+// The per-lane choice is a select of one address, not two branches with a
+// load each: from the branchy form hipcc (ROCm 7.2) merged the two loads (and
+// the caller's prev5 load) into one load whose base pointer it kept in an
+// SGPR across the divergent branches, so the cold lanes of a wave read
+// through another branch's base -- out of bounds, a memory fault in
+// recur_pipe_kernel.  With the select the base is a VGPR per lane.
+// fs.nring is wave-uniform.
 __device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
                                       int part) {
-    if (!fs.lmel || t - b + fs.fresh[s] < 2)
-        return *reinterpret_cast<const int4*>(feats + ((size_t)s * T + t) * 40 + 8 * part);
+    if (!fs.nring) return *reinterpret_cast<const int4*>(feats + ((size_t)s * T + t) * 40 + 8 * part);
+    const bool cold = t - b + fs.fresh[s] < 2;
     const unsigned slot = (unsigned)(fs.abs0 + t - fs.lookback + fs.ring) % (unsigned)fs.ring;
-    const int4* src = reinterpret_cast<const int4*>(fs.lmel + ((size_t)s * fs.ring + slot) * 40 + 8 * part);
-    const int4 l0 = src[0], l1 = src[1];
-    const int32_t lg[8] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z, l1.w};
-    uint32_t o[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int64_t d = (int64_t)lg[j] - fs.mean[8 * part + j];
-        o[j] = (uint16_t)sat16((d * fs.stdR[8 * part + j]) >> fs.norm_shift);
-    }
-    return make_int4((int)(o[0] | o[1] << 16), (int)(o[2] | o[3] << 16), (int)(o[4] | o[5] << 16),
-                     (int)(o[6] | o[7] << 16));
+    const size_t row = cold ? (size_t)s * T + t : (size_t)s * fs.ring + slot;
+    const uintptr_t base = cold ? (uintptr_t)feats : (uintptr_t)fs.nring;
+    return *reinterpret_cast<const int4*>(base + (row * 40 + 8 * part) * sizeof(int16_t));
 }
 
 // Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
