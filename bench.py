@@ -49,7 +49,17 @@ from nnsp_amd.shard import dist_env, reduce_run, shard_streams  # noqa: E402
 # algorithmic work per frame (denominators of roofline.achieved)
 FE_MULS_PER_FRAME = 5912           # integer multiplies of one front-end frame
 NN_MACS_PER_INFERENCE = {"vad": 14616, "kws": 56448, "s2i": 72072}
-FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out (cascade: + 80, int32 log-Mel out)
+FE_HBM_BYTES_PER_FRAME = 320 + 80  # PCM in + normalised features out (single net)
+# cascade shared front end: PCM in, each of the three nets' normalised ring
+# (3 x 80 B) out, and the look-back history of the next chunk (the chunk's
+# last H = max look-back + 1 = 81 frames of PCM, stored once per chunk)
+CASCADE_HIST_FRAMES = 81
+
+
+def fe_bytes_per_frame(cascade: bool, T: int) -> float:
+    if not cascade:
+        return FE_HBM_BYTES_PER_FRAME
+    return 320 + 3 * 80 + 320 * min(CASCADE_HIST_FRAMES, T) / T
 # NN per inference (one per 2 frames): the 2 new context frames in (cascade:
 # int32 log-Mel, 2 x 160 B) + per-frame outputs of its 2 frames (net, trigger,
 # outputs[3]: 2 x 9 B)
@@ -284,8 +294,8 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
     fe_ms = res["fe_ms"]
     fe_frames = S * T
     fe_ach = fe_frames * FE_MULS_PER_FRAME / (fe_ms / 1e3) / 1e12
-    fe_traffic = kern.get("fe_kernel", {}).get("hbm_bytes_per_launch")
-    fe_alg = fe_frames * (FE_HBM_BYTES_PER_FRAME + (80 if cascade else 0))
+    fe_traffic = kern.get("fe_kernel[shared]" if cascade else "fe_kernel[batch]", {}).get("hbm_bytes_per_launch")
+    fe_alg = fe_frames * fe_bytes_per_frame(cascade, T)
     fe = {"kernel": "fe_kernel", "bound": "valu", "achieved": fe_ach, "peak": mul_peak, "unit": "Tops/s",
           "frac": fe_ach / mul_peak, "traffic": fe_traffic,
           "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, profiles/pmc_latest.json)",

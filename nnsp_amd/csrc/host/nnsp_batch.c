@@ -185,7 +185,19 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count, 0);
     if (e) goto fail;
     b->nout = b->im.img.nout;
-    if ((e = nnspk_stream_create(&b->stream))) goto fail;
+    /* NNSP_NET_STREAM_PRIO=1: the batch's stream at the device's highest
+     * priority (cascade experiments: the nets' rounds ahead of the look-ahead
+     * front end) */
+    int hi = getenv("NNSP_NET_STREAM_PRIO") != NULL;
+    {   /* NNSP_PRIO_NETS="0,2": only the batches of these NNSP_IDs at high priority */
+        const char *pn = getenv("NNSP_PRIO_NETS");
+        if (pn) {
+            hi = 0;
+            for (const char *q = pn; *q; ++q)
+                if (*q >= '0' && *q <= '9' && *q - '0' == nn_id) hi = 1;
+        }
+    }
+    if ((e = hi ? nnspk_stream_create_prio(&b->stream, 1) : nnspk_stream_create(&b->stream))) goto fail;
     for (int i = 0; i < 3; ++i)
         if ((e = nnspk_event_create(&b->ev[i]))) goto fail;
     if ((e = nnsp_image_upload(&b->im, b->stream))) goto fail;

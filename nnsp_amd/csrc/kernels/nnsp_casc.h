@@ -50,13 +50,17 @@ __device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned lo
 // controller state; returns true when the frame resets net n (the stream's
 // segment ends here and the next frame runs the net at st.pos from its reset).
 // A move without a reset keeps the same net and state running.
+// The counters and the position stay in range (0 <= cnt < timeout, 0 <= pos <
+// len_seq: reset to 0, then only advanced here), so each "% m" of the
+// reference is a compare-and-wrap: no integer division on the post wave.
+__device__ __forceinline__ int wrap_inc(int x, int m) { return x + 1 == m ? 0 : x + 1; }
 __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int n, int16_t det) {
     bool move = false, rst = false;
     int np = st.pos;
     if (n == 0) {   // s2i (nnCntrlClass.c:173-200)
-        st.cnt_s2i = (uint16_t)((st.cnt_s2i + 1) % a.timeout_s2i);
+        st.cnt_s2i = (uint16_t)wrap_inc(st.cnt_s2i, a.timeout_s2i);
         if (det || st.cnt_s2i == a.timeout_s2i - 1) {
-            np = (st.pos + 1) % a.len_seq;
+            np = wrap_inc(st.pos, a.len_seq);
             move = true;
             if (det || n != a.seq[np]) {
                 st.cnt_s2i = 0;
@@ -64,10 +68,9 @@ __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int 
             }
         }
     } else if (n == 2) {   // kws (nnCntrlClass.c:203-236)
-        st.cnt_kws = (uint16_t)((st.cnt_kws + 1) % a.timeout_kws);
+        st.cnt_kws = (uint16_t)wrap_inc(st.cnt_kws, a.timeout_kws);
         if (det || st.cnt_kws == a.timeout_kws - 1) {
-            np = det ? (st.pos + 1) % a.len_seq : (st.pos - 1) % a.len_seq;
-            if (np < 0) np += a.len_seq;
+            np = det ? wrap_inc(st.pos, a.len_seq) : (st.pos == 0 ? a.len_seq - 1 : st.pos - 1);
             move = true;
             if (det || n != a.seq[np]) {
                 st.cnt_kws = 0;
@@ -75,7 +78,7 @@ __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int 
             }
         }
     } else if (det) {   // vad (nnCntrlClass.c:238-262)
-        np = (st.pos + 1) % a.len_seq;
+        np = wrap_inc(st.pos, a.len_seq);
         move = rst = true;
     }
     if (move) st.pos = (int16_t)np;

@@ -725,11 +725,18 @@ struct PipeCfg {
     // 13th wave would cap the kernel at 128 VGPRs, and the spills cost more
     // than the split gains (profiles/recur_clocks.py)
     static constexpr int SPLIT = SH::NOUT <= 2 ? 1 : 0;
-    static constexpr int NWV = LW + 3 + SPLIT;               // waves per workgroup
+    static constexpr int NWV = LW + 3 + SPLIT;               // waves per tile
+    // tiles per workgroup (the kernel supports several, sharing the staged
+    // weights): one.  Two VAD tiles per workgroup (16 waves, so that every
+    // net's recur workgroup fills one CU in a cascade round) measured slower:
+    // VAD iteration 2960 -> 4572 cycles with one barrier over both tiles, and
+    // no cascade gain (profiles/r02/casc_clocks.py).
+    static constexpr int TPW = 1;
+    static constexpr int WPG = NWV * TPW;                    // waves per workgroup
     // waves per SIMD the register budget must allow: two workgroups per CU
     // when a workgroup has <= 8 waves (VAD: <= 128 VGPRs), else one
-    static constexpr int MINW = NWV <= 8 ? 2 * ((NWV + 3) / 4) : (NWV + 3) / 4;
-    static_assert(NWV <= 12, "recur_pipe_kernel: at most 3 waves per SIMD");
+    static constexpr int MINW = WPG <= 8 ? 2 * ((WPG + 3) / 4) : (WPG + 3) / 4;
+    static_assert(WPG <= 16, "recur_pipe_kernel: at most 4 waves per SIMD");
 };
 
 template <class SH>
@@ -756,7 +763,7 @@ struct alignas(16) PipeTile {
 // (NNSPClass_reset) instead of the carried one, and the stream is listed for
 // its next net -- what casc_control_kernel does after the kernel otherwise.
 template <class SH, bool ACC32>
-__global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
+__global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
                                                                                             CascArgs ca) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CF = PipeCfg<SH>;
@@ -768,17 +775,23 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     // does; nothing reads or appends to it during this round)
     if (ctl && blockIdx.x == 0 && threadIdx.x < 6) ca.counts_clear[threadIdx.x] = 0;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
-    const int i0 = blockIdx.x * 16;   // tile = 16 consecutive entries of the stream list
-    if (i0 >= nrow) return;
+    constexpr int TPW = CF::TPW, TD = 64 * CF::NWV;   // tiles per workgroup, threads per tile
+    if ((int)blockIdx.x * TPW * 16 >= nrow) return;
+    // the workgroup's tiles share the staged weights and tables; everything
+    // else below is per tile (tid / TD instead of threadIdx / blockDim)
+    const int sub = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / CF::NWV;
+    const int tid = (int)threadIdx.x - sub * TD;
+    const int i0 = ((int)blockIdx.x * TPW + sub) * 16;   // tile = 16 consecutive entries of the stream list
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
-    PT& R = *reinterpret_cast<PT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    PT* RT = reinterpret_cast<PT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    PT& R = RT[sub];
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     const int lane = threadIdx.x & 63;
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));   // < RGP: LSTM wave; then stages 1..3
+    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - sub * CF::NWV;   // < RGP: LSTM wave; then stages
     const int sc = lane & 15, q = lane >> 4;
     auto sid = [&](int i) { return r.list ? r.list[i] : i; };
     const bool valid = i0 + sc < nrow;
@@ -787,7 +800,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     // compiled shapes have xs_sh == 0 (net_shape): the input and recurrent
     // halves of a gate share one MFMA accumulator
     const int rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
-    for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
+    for (int idx = tid; idx < 16 * N; idx += TD) {
         const int st = idx / N, u = idx - st * N;
         const bool ok = i0 + st < nrow;
         const int gs = ok ? sid(i0 + st) : 0;
@@ -815,9 +828,13 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     const int phase = R.phase[sc];
     const int b = R.beg[sc];
     const int e = R.end[sc];   // segment: frames b..e-1
-    int nsteps = 0;
+    int nsteps = 0, nloop = 0;   // this tile's NN steps; the workgroup's (the barriers' trip count)
 #pragma unroll
     for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
+#pragma unroll
+    for (int k = 0; k < TPW; ++k)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) nloop = max(nloop, RT[k].nst[i]);
     if (post_w && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
         put_frame(r, s, T, b, ps);
         if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
@@ -873,7 +890,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     const NnLayer& L4 = img.L[r.li + 3];
     // development probe (NNSP_RECUR_CLOCKS): s_memtime at the start and end of each
     // iteration's work of LSTM wave 0 and the three stage waves, tile 0
-    long long* clk = (r.dbg_clk && blockIdx.x == 0 && lane == 0 && (g == 0 || g >= RGP))
+    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && sub == 0 && lane == 0 && (g == 0 || g >= RGP))
                          ? r.dbg_clk + 2 * (g == 0 ? 0 : g - RGP + 1)
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the
@@ -1013,9 +1030,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
         __syncthreads();
     };
-    for (int j = 0; j < nsteps + 3 + SPL; j += 2) {
+    for (int j = 0; j < nloop + 3 + SPL; j += 2) {
         iteration(j, std::integral_constant<int, 0>{});
-        if (j + 1 < nsteps + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
+        if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
     }
     if (ctl) {
         if (post_w && lane < 16) R.cut[lane] = valid ? cut : -1;
@@ -1024,7 +1041,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     // ---- state out: LSTM step nsteps-1 wrote h[nsteps & 1]; a stream whose
     //      net was reset gets the zero state (NeuralNetClass_setDefault)
     const int hb = nsteps & 1;
-    for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
+    for (int idx = tid; idx < 16 * N; idx += TD) {
         const int st = idx / N, u = idx - st * N;
         if (i0 + st < nrow) {
             const int gs = sid(i0 + st);
@@ -1048,7 +1065,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::NWV, PipeCfg<SH>::MINW) void recu
     int ci[2];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
-        const int idx = threadIdx.x + (int)blockDim.x * k;   // (stream in tile, 16-byte chunk of 5x40)
+        const int idx = tid + TD * k;   // (stream in tile, 16-byte chunk of 5x40)
         ci[k] = -1;
         if (idx < 16 * 25 && i0 + idx / 25 < nrow) {
             const int st = idx / 25, c = idx - st * 25, m = c / 5, part = c - 5 * m;
@@ -1126,9 +1143,9 @@ const void* pipe_fn(bool acc32) {
 // compiled shapes: the pipelined recurrence (one tile per workgroup)
 const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes) {
     switch (shape) {
-        case NN_SHAPE_VAD: *waves = PipeCfg<ShapeVad>::NWV; *tile_bytes = sizeof(PipeTile<ShapeVad>); return pipe_fn<ShapeVad>(acc32);
-        case NN_SHAPE_KWS: *waves = PipeCfg<ShapeKws>::NWV; *tile_bytes = sizeof(PipeTile<ShapeKws>); return pipe_fn<ShapeKws>(acc32);
-        case NN_SHAPE_S2I: *waves = PipeCfg<ShapeS2i>::NWV; *tile_bytes = sizeof(PipeTile<ShapeS2i>); return pipe_fn<ShapeS2i>(acc32);
+        case NN_SHAPE_VAD: *waves = PipeCfg<ShapeVad>::WPG; *tile_bytes = sizeof(PipeTile<ShapeVad>); return pipe_fn<ShapeVad>(acc32);
+        case NN_SHAPE_KWS: *waves = PipeCfg<ShapeKws>::WPG; *tile_bytes = sizeof(PipeTile<ShapeKws>); return pipe_fn<ShapeKws>(acc32);
+        case NN_SHAPE_S2I: *waves = PipeCfg<ShapeS2i>::WPG; *tile_bytes = sizeof(PipeTile<ShapeS2i>); return pipe_fn<ShapeS2i>(acc32);
         default: return nullptr;
     }
 }
@@ -1163,9 +1180,9 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int 
     const size_t base = (size_t)a_bytes + 768 + ep_bytes(ep_rows);
     size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
     switch (shape) {   // compiled shapes: recur runs one pipelined tile per workgroup
-        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(PipeTile<ShapeVad>); units = which ? 1 : units; break;
-        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(PipeTile<ShapeKws>); units = which ? 1 : units; break;
-        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(PipeTile<ShapeS2i>); units = which ? 1 : units; break;
+        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(PipeTile<ShapeVad>); units = which ? PipeCfg<ShapeVad>::TPW : units; break;
+        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(PipeTile<ShapeKws>); units = which ? PipeCfg<ShapeKws>::TPW : units; break;
+        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(PipeTile<ShapeS2i>); units = which ? PipeCfg<ShapeS2i>::TPW : units; break;
         default: break;
     }
     return base + (size_t)units * (which == 0 ? pw : rt);
@@ -1185,7 +1202,10 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const Casc
     if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb)) {
         CascArgs none;
         memset(&none, 0, sizeof none);
-        return launch(fn, dim3((nrow + 15) / 16), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
+        const int tpw = r->shape == NN_SHAPE_VAD ? PipeCfg<ShapeVad>::TPW
+                                                 : (r->shape == NN_SHAPE_KWS ? PipeCfg<ShapeKws>::TPW : PipeCfg<ShapeS2i>::TPW);
+        const int tiles = (nrow + 15) / 16;
+        return launch(fn, dim3((tiles + tpw - 1) / tpw), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
     }
     if (ctl) return (int)hipErrorInvalidValue;   // fused control needs the pipelined kernel
     const int tiles = (nrow + 15) / 16;

@@ -88,6 +88,13 @@ def main():
         if avg.get("SQ_WAVE_CYCLES"):
             e["wait_frac"] = avg.get("SQ_WAIT_ANY", 0) / avg["SQ_WAVE_CYCLES"]
         res["kernels"][k] = e
+    # steps (chunks) profiled: one shared front end (cascade) or one batch
+    # front end (single net) per step; per-step HBM bytes of every kernel
+    nsteps = (res["kernels"].get("fe_kernel[shared]") or res["kernels"].get("fe_kernel[batch]") or {}).get("launches", 0)
+    res["steps"] = nsteps
+    for e in res["kernels"].values():
+        if nsteps and "hbm_bytes_all_launches" in e:
+            e["hbm_bytes_per_step"] = e["hbm_bytes_all_launches"] / nsteps
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
     for k, v in res["kernels"].items():
