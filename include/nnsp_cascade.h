@@ -58,9 +58,13 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask);
  * NNSPClass_exec return, outputs3 [S][T][3] int16 = its NNSPClass.outputs.
  * _device: device pointers, work on nnsp_cascade_stream and the three nets'
  * batch streams forked from it.  The call returns once the chunk's rounds have
- * finished on the device: the host reads back the list lengths of the round
- * after the last one it launched to decide whether more rounds are needed, so
- * it cannot queue the next chunk while this one runs. */
+ * finished on the device (its outputs are final): the host reads back the list
+ * lengths of the round after the last one it launched to decide whether more
+ * rounds are needed, so it cannot queue the next chunk while this one runs.
+ * The chunk's bookkeeping (counter copy, the next chunk's STFT tail and
+ * look-back history, a look-ahead front end) may still run on
+ * nnsp_cascade_stream when it returns; the next call, the statistics getters,
+ * nnsp_cascade_sync and nnsp_cascade_reset order themselves after it. */
 int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,
                       int16_t *detected, int16_t *outputs3);
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,

@@ -32,6 +32,7 @@
 /* NNSP_CASCADE_DEBUG: after each launch, wait for the stream and report
  * which launch failed (asynchronous faults otherwise surface at a later sync) */
 static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n, int r);
+static int book_take(nnsp_cascade *c);
 #define DBG(st, what, n, r)                                  \
     do {                                                     \
         if (c->debug) TRY(dbg_step(c, (st), (what), (n), (r))); \
@@ -102,6 +103,15 @@ struct nnsp_cascade {
     int runs[3];                    /* last chunk, per net id: segment runs */
     int rc[MAX_TIMED][3];           /* last chunk: list length of each round and net */
     float rfe[MAX_TIMED][3], rnn[MAX_TIMED][3]; /* last chunk, timing on: per round and net ms */
+    /* end-of-chunk bookkeeping, asynchronous: the chunk's counters (d_zero) are
+     * copied to pinned host memory and cleared for the next chunk on the
+     * stream; the host reads the copy (book_take) when it next needs it */
+    void *h_book;                   /* pinned copy of d_zero */
+    void *ev_book;                  /* recorded after the copy */
+    int book_pending;               /* a copy is in flight */
+    int book_rounds;                /* rounds launched in that chunk */
+    int book_ahead, book_ahead_done; /* its look-ahead front end ran; its own front end ran ahead */
+    unsigned long long book_frames[3];
 };
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
@@ -155,7 +165,14 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
     c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
-    if ((e = nnspk_stream_create(&c->stream))) goto fail;
+    {   /* NNSP_FE_FREE_CUS=N: the cascade's stream (shared front end, look-ahead
+         * included) leaves N CUs to the nets' rounds (experiment) */
+        const char *fc = getenv("NNSP_FE_FREE_CUS");
+        const char *fs = getenv("NNSP_FE_FREE_SPREAD");
+        if ((e = fc ? nnspk_stream_create_cumask(&c->stream, atoi(fc), fs ? atoi(fs) : 1)
+                    : nnspk_stream_create(&c->stream)))
+            goto fail;
+    }
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
@@ -176,6 +193,9 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_st, S * sizeof(CascState)))) goto fail;
     /* the per-chunk counters, one allocation zeroed by one memset per chunk */
     if ((e = nnspk_malloc((void **)&c->d_zero, ZERO_BYTES))) goto fail;
+    if ((e = nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream))) goto fail;
+    if ((e = nnspk_host_alloc(&c->h_book, ZERO_BYTES))) goto fail;
+    if ((e = nnspk_event_create(&c->ev_book))) goto fail;
     c->d_frames = (unsigned long long *)c->d_zero;                 /* [3] */
     c->d_counts = (int32_t *)((char *)c->d_zero + 3 * 8);         /* [18] */
     c->d_last_round = c->d_counts + 18;                             /* [1] */
@@ -207,7 +227,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         a->len_seq = len_seq;
         a->timeout_kws = p->thresh_timeout_kws;
         a->timeout_s2i = p->thresh_timeout_s2i;
-        for (int i = 0; i < len_seq; ++i) a->seq[i] = seq[i];
+        for (int i = 0; i < len_seq; ++i) {
+            a->seq[i] = seq[i];
+            a->seq_bits |= (int32_t)seq[i] << (2 * i);
+        }
         a->st = c->d_st;
         a->seg_begin = c->d_seg_begin;
         a->counts = c->d_counts;
@@ -309,6 +332,8 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         c->ns[n] = NULL; /* the batch's stream, owned by the batch */
     }
     nnspk_stream_destroy(c->stream);
+    nnspk_event_destroy(c->ev_book);
+    nnspk_host_free(c->h_book);
     free(c);
 }
 
@@ -316,6 +341,7 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
+    TRY(book_take(c));
     for (int i = 0; i < 3; ++i) TRY(nnsp_batch_reset(c->net[i], mask)); /* synchronous */
     const uint8_t *dm = NULL;
     if (mask) {
@@ -490,6 +516,59 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     return nnspk_launch_fe(&fa, c->stream);
 }
 
+/* The last chunk's bookkeeping: wait for the pinned copy of its counters
+ * (long done by the time the host comes back) and derive the host-side
+ * statistics and the next chunk's window. */
+static int book_take(nnsp_cascade *c)
+{
+    if (!c->book_pending) return 0;
+    TRY(nnspk_event_sync(c->ev_book));
+    c->book_pending = 0;
+    const char *h = (const char *)c->h_book;   /* d_zero: frames[3], counts[18], last_round, cuts, rcount */
+    memcpy(c->book_frames, h, sizeof c->book_frames);
+    const int32_t *cnt = (const int32_t *)(h + 3 * 8);
+    const int32_t(*rc)[3] = (const int32_t(*)[3])(cnt + 20);
+    const int r = c->book_rounds, ahead = c->book_ahead;
+    c->last_rounds = cnt[18] + 1;
+    c->last_cuts = cnt[19];
+    if (c->auto_window) {
+        /* window for the next chunk from this chunk's net switches per stream:
+         * few switches -> run each stream to the chunk end in one round (a
+         * switch then wastes the rest of the chunk's work on that stream, but
+         * rounds are few); frequent switches -> short windows bound the waste.
+         * Results do not depend on the window (tests/test_gpu_cascade.py). */
+        const double per = (double)c->last_cuts / (double)c->S;
+        c->window = per < 0.5 ? 0 : (per < 2.0 ? 32 : 16);
+    }
+    TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
+    c->ahead_ms = 0.f;
+    if (ahead) TRY(nnspk_event_elapsed(&c->ahead_ms, c->ev_ahead[0], c->ev_ahead[1]));
+    /* the shared front end of this chunk: timed here, or by the previous call (ahead) */
+    if (c->book_ahead_done) c->sfe_ms = c->prev_ahead_ms;
+    c->prev_ahead_ms = c->ahead_ms;
+    memcpy(c->rc, rc, sizeof c->rc);
+    memset(c->rfe, 0, sizeof c->rfe);
+    memset(c->rnn, 0, sizeof c->rnn);
+    for (int k = r; k < MAX_TIMED; ++k) c->rc[k][0] = c->rc[k][1] = c->rc[k][2] = 0;
+    for (int n = 0; n < 3; ++n) {
+        c->fe_ms[n] = c->nn_ms[n] = 0.f;
+        c->runs[n] = 0;
+        for (int k = 0; k < r && k < MAX_TIMED; ++k) {
+            if (!c->rc[k][n]) continue;
+            c->runs[n]++;
+            if (!c->timing) continue;
+            float fe = 0.f, nn = 0.f;
+            TRY(nnspk_event_elapsed(&fe, c->ev_t[k][n][0], c->ev_t[k][n][1]));
+            TRY(nnspk_event_elapsed(&nn, c->ev_t[k][n][1], c->ev_t[k][n][2]));
+            c->fe_ms[n] += fe;
+            c->nn_ms[n] += nn;
+            c->rfe[k][n] = fe;
+            c->rnn[k][n] = nn;
+        }
+    }
+    return 0;
+}
+
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran, int16_t *detected,
                              int16_t *outputs3)
 {
@@ -503,6 +582,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         nnsp_set_error("nnsp_cascade_exec: T must be in 1..%d", c ? c->Tmax : 0);
         return NNSP_EINVAL;
     }
+    TRY(book_take(c)); /* the last chunk's counters: rounds, switches (this chunk's window) */
     CascArgs a = c->a;
     a.T = T;
     a.seg_len = c->window;
@@ -511,8 +591,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
     const long long k = c->chunk;
-    TRY(nnspk_event_record(c->ev[0], c->stream));
-    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream)); /* counts, frames, last round, cuts, rcount */
+    TRY(nnspk_event_record(c->ev[0], c->stream)); /* the counters (d_zero) were cleared by the last chunk */
     /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
@@ -521,6 +600,14 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     DBG(c->stream, "shared front end", -1, -1);
     TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     c->sfe_ahead = ahead_done;
+    /* the next chunk's voice buffer (its look-back history) and STFT tail:
+     * they read this chunk's PCM, and nothing in this chunk reads what they
+     * write (cold frames read d_hist[k % 3]; the look-ahead front end takes
+     * its tail from pcm) -- queued now, off the chunk's tail */
+    const int16_t *hist = c->d_hist[k % 3];
+    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
+        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
+    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     a.counts = c->d_counts; /* round 0's lists */
     for (int n = 0; n < 3; ++n) {
         a.list[n] = c->d_list[0][n];
@@ -549,7 +636,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     if (ahead && c->ahead_after <= 0) LAUNCH_AHEAD();
     /* rounds run without host round trips: launch as many as the last chunk
      * needed, then check the next round's list lengths (one read-back) */
-    const int16_t *hist = c->d_hist[k % 3];
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
         for (; r < R; ++r) {
@@ -567,61 +653,22 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         R = r + 2;
     }
     c->launched = r;
-    /* voice buffer: keep the last H frames for the next chunk's look-back;
-     * the shared front end's STFT buffer keeps the last 2 frames */
-    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
-        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
-    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     c->abs0 = (c->abs0 + T) % c->ring;
     c->chunk = k + 1;
-    ahead = ahead_launched;
-    if (ahead) {
+    if (ahead_launched) {
         c->pre_pcm = next_pcm;
         c->pre_T = next_T;
     }
     TRY(nnspk_event_record(c->ev[1], c->stream));
-    /* bookkeeping: rounds that had work, per-net device time of those rounds */
-    int32_t last[2] = {0, 0}, rc[MAX_TIMED][3];
-    TRY(nnspk_d2h(last, c->d_last_round, 8, c->stream)); /* last_round, cuts */
-    TRY(nnspk_d2h(rc, c->d_rcount, sizeof rc, c->stream));
-    TRY(nnspk_sync(c->stream));
-    c->last_rounds = last[0] + 1;
-    c->last_cuts = last[1];
-    if (c->auto_window) {
-        /* window for the next chunk from this chunk's net switches per stream:
-         * few switches -> run each stream to the chunk end in one round (a
-         * switch then wastes the rest of the chunk's work on that stream, but
-         * rounds are few); frequent switches -> short windows bound the waste.
-         * Results do not depend on the window (tests/test_gpu_cascade.py). */
-        const double per = (double)c->last_cuts / (double)c->S;
-        c->window = per < 0.5 ? 0 : (per < 2.0 ? 32 : 16);
-    }
-    TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
-    c->ahead_ms = 0.f;
-    if (ahead) TRY(nnspk_event_elapsed(&c->ahead_ms, c->ev_ahead[0], c->ev_ahead[1]));
-    /* the shared front end of this chunk: timed here, or by the previous call (ahead) */
-    if (ahead_done) c->sfe_ms = c->prev_ahead_ms;
-    c->prev_ahead_ms = c->ahead_ms;
-    memcpy(c->rc, rc, sizeof rc);
-    memset(c->rfe, 0, sizeof c->rfe);
-    memset(c->rnn, 0, sizeof c->rnn);
-    for (int k = r; k < MAX_TIMED; ++k) c->rc[k][0] = c->rc[k][1] = c->rc[k][2] = 0;
-    for (int n = 0; n < 3; ++n) {
-        c->fe_ms[n] = c->nn_ms[n] = 0.f;
-        c->runs[n] = 0;
-        for (int k = 0; k < r && k < MAX_TIMED; ++k) {
-            if (!rc[k][n]) continue;
-            c->runs[n]++;
-            if (!c->timing) continue;
-            float fe = 0.f, nn = 0.f;
-            TRY(nnspk_event_elapsed(&fe, c->ev_t[k][n][0], c->ev_t[k][n][1]));
-            TRY(nnspk_event_elapsed(&nn, c->ev_t[k][n][1], c->ev_t[k][n][2]));
-            c->fe_ms[n] += fe;
-            c->nn_ms[n] += nn;
-            c->rfe[k][n] = fe;
-            c->rnn[k][n] = nn;
-        }
-    }
+    /* bookkeeping without a host wait: the counters to pinned memory, then
+     * cleared for the next chunk (book_take reads the copy) */
+    TRY(nnspk_d2h(c->h_book, c->d_zero, ZERO_BYTES, c->stream));
+    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream));
+    TRY(nnspk_event_record(c->ev_book, c->stream));
+    c->book_pending = 1;
+    c->book_rounds = r;
+    c->book_ahead = ahead_launched;
+    c->book_ahead_done = ahead_done;
     return 0;
 }
 
@@ -660,6 +707,7 @@ int nnsp_cascade_set_window(nnsp_cascade *c, int frames)
 int nnsp_cascade_get_window(nnsp_cascade *c, int *frames, int *is_auto, int *last_cuts)
 {
     if (!c) return NNSP_EINVAL;
+    TRY(book_take(c));
     if (frames) *frames = c->window;
     if (is_auto) *is_auto = c->auto_window;
     if (last_cuts) *last_cuts = c->last_cuts;
@@ -681,20 +729,20 @@ int nnsp_cascade_set_serial(nnsp_cascade *c, int on)
     return 0;
 }
 
-int nnsp_cascade_sync(nnsp_cascade *c) { return c ? nnspk_sync(c->stream) : NNSP_EINVAL; }
+int nnsp_cascade_sync(nnsp_cascade *c)
+{
+    if (!c) return NNSP_EINVAL;
+    TRY(nnspk_sync(c->stream));
+    return book_take(c);
+}
 void *nnsp_cascade_stream(nnsp_cascade *c) { return c ? c->stream : NULL; }
 
 int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run, float *ms)
 {
     if (!c) return NNSP_EINVAL;
-    TRY(nnspk_sync(c->stream));
+    TRY(book_take(c));
     if (rounds) *rounds = c->last_rounds;
-    if (frames_run) {
-        unsigned long long f[3] = {0, 0, 0};
-        TRY(nnspk_d2h(f, c->d_frames, 3 * 8, c->stream));
-        TRY(nnspk_sync(c->stream));
-        *frames_run = (long long)(f[0] + f[1] + f[2]);
-    }
+    if (frames_run) *frames_run = (long long)(c->book_frames[0] + c->book_frames[1] + c->book_frames[2]);
     if (ms) TRY(nnspk_event_elapsed(ms, c->ev[0], c->ev[1]));
     return 0;
 }
@@ -702,7 +750,7 @@ int nnsp_cascade_last_stats(nnsp_cascade *c, int *rounds, long long *frames_run,
 int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms)
 {
     if (!c) return NNSP_EINVAL;
-    TRY(nnspk_sync(c->stream));
+    TRY(book_take(c));
     if (ms) *ms = c->sfe_ms;
     return 0;
 }
@@ -711,13 +759,8 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
                                 int *launches)
 {
     if (!c || nn_id < 0 || nn_id > 2) return NNSP_EINVAL;
-    TRY(nnspk_sync(c->stream));
-    if (frames_run) {
-        unsigned long long f[3] = {0, 0, 0};
-        TRY(nnspk_d2h(f, c->d_frames, 3 * 8, c->stream));
-        TRY(nnspk_sync(c->stream));
-        *frames_run = (long long)f[nn_id];
-    }
+    TRY(book_take(c));
+    if (frames_run) *frames_run = (long long)c->book_frames[nn_id];
     if (fe_ms) *fe_ms = c->fe_ms[nn_id];
     if (nn_ms) *nn_ms = c->nn_ms[nn_id];
     if (launches) *launches = c->runs[nn_id];
@@ -727,7 +770,7 @@ int nnsp_cascade_last_net_stats(nnsp_cascade *c, int nn_id, long long *frames_ru
 int nnsp_cascade_last_rounds(nnsp_cascade *c, int max_rounds, int32_t *lists, float *fe_ms, float *nn_ms)
 {
     if (!c || max_rounds < 0) return NNSP_EINVAL;
-    TRY(nnspk_sync(c->stream));
+    TRY(book_take(c));
     const int n = c->launched < MAX_TIMED ? c->launched : MAX_TIMED;
     for (int k = 0; k < max_rounds && k < n; ++k)
         for (int i = 0; i < 3; ++i) {

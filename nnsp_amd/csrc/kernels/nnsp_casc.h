@@ -54,6 +54,10 @@ __device__ __forceinline__ void add_frames(const CascArgs& a, int n, unsigned lo
 // len_seq: reset to 0, then only advanced here), so each "% m" of the
 // reference is a compare-and-wrap: no integer division on the post wave.
 __device__ __forceinline__ int wrap_inc(int x, int m) { return x + 1 == m ? 0 : x + 1; }
+// a.seq[i] for a per-lane i, from the 2-bit packed copy (host, seq_bits).  A
+// dynamic index into the kernel argument is a vector memory load, and its wait
+// (vmcnt) also waited for the post wave's output stores issued just before.
+__device__ __forceinline__ int seq_at(const CascArgs& a, int i) { return (a.seq_bits >> (2 * i)) & 3; }
 __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int n, int16_t det) {
     bool move = false, rst = false;
     int np = st.pos;
@@ -62,7 +66,7 @@ __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int 
         if (det || st.cnt_s2i == a.timeout_s2i - 1) {
             np = wrap_inc(st.pos, a.len_seq);
             move = true;
-            if (det || n != a.seq[np]) {
+            if (det || n != seq_at(a, np)) {
                 st.cnt_s2i = 0;
                 rst = true;
             }
@@ -72,7 +76,7 @@ __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int 
         if (det || st.cnt_kws == a.timeout_kws - 1) {
             np = det ? wrap_inc(st.pos, a.len_seq) : (st.pos == 0 ? a.len_seq - 1 : st.pos - 1);
             move = true;
-            if (det || n != a.seq[np]) {
+            if (det || n != seq_at(a, np)) {
                 st.cnt_kws = 0;
                 rst = true;
             }

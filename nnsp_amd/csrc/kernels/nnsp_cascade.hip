@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
     int n = 0, fr = 2;
     if (ok_s) {
         a.seg_begin[s] = 0;
-        n = a.seq[a.st[s].pos];
+        n = nnsp::seq_at(a, a.st[s].pos);
         fr = a.fresh[s];
     }
     list_next(a, n, s, ok_s, fr);
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
         a.seg_begin[s] = b_next;
         if (b_next < T) {
             want = true;
-            n_next = a.seq[st.pos];
+            n_next = nnsp::seq_at(a, st.pos);
         }
     }
     list_next(a, n_next, s, want, fr_next);

@@ -223,15 +223,25 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 // per-frame results of stream s at frame f (NNSPClass_exec's return value and
 // NNSPClass.outputs after the frame): per-net buffers for the controller and,
 // in a cascade, the caller's outputs
-__device__ __forceinline__ void put_frame(const FastRun& r, int s, int T, int f, const PostState& ps) {
+__device__ __forceinline__ void put_out(const FastRun& r, int s, int T, int f, int16_t trig, int16_t o0, int16_t o1,
+                                        int16_t o2) {
     const size_t i = (size_t)s * T + f;
-    if (r.trig) r.trig[i] = ps.trigger;
-    if (r.out3)
-        for (int o = 0; o < 3; ++o) r.out3[i * 3 + o] = ps.outputs[o];
-    if (r.detected) r.detected[i] = ps.trigger;
+    if (r.trig) r.trig[i] = trig;
+    if (r.out3) {
+        r.out3[i * 3] = o0;
+        r.out3[i * 3 + 1] = o1;
+        r.out3[i * 3 + 2] = o2;
+    }
+    if (r.detected) r.detected[i] = trig;
     if (r.net_ran) r.net_ran[i] = (int8_t)r.net_id;
-    if (r.outputs3)
-        for (int o = 0; o < 3; ++o) r.outputs3[i * 3 + o] = ps.outputs[o];
+    if (r.outputs3) {
+        r.outputs3[i * 3] = o0;
+        r.outputs3[i * 3 + 1] = o1;
+        r.outputs3[i * 3 + 2] = o2;
+    }
+}
+__device__ __forceinline__ void put_frame(const FastRun& r, int s, int T, int f, const PostState& ps) {
+    put_out(r, s, T, f, ps.trigger, ps.outputs[0], ps.outputs[1], ps.outputs[2]);
 }
 // ---------------------------------------------------------------------------
 // proj_kernel
@@ -753,6 +763,12 @@ struct alignas(16) PipeTile {
     int32_t beg[16];          // segment start frame
     int32_t end[16];          // segment end frame (exclusive)
     int32_t cut[16];          // fused control: frame that reset the net (-1: none)
+    // the post wave's frame outputs of one step, stored to HBM by another wave
+    // one iteration later (double-buffered by iteration parity): frame t,
+    // which of t / t + 1 to write (bits 0 / 1), trigger, outputs[3]
+    int32_t pt[2][16];
+    int32_t pw[2][16];
+    int16_t po[2][16][4];
 };
 
 //
@@ -810,6 +826,11 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     const int T = r.T;
     constexpr int SPL = CF::SPLIT;
     const bool post_w = g == RGP + 2 + SPL;   // the post-processing wave
+    // the waves that store the post wave's frame outputs one iteration later:
+    // the stage with the most slack (FC linear); S2I, whose FC stages are as
+    // long as its LSTM step, splits them over its two FC waves (frame t / t + 1)
+    const bool store_w = SPL ? g == RGP + 2 : (g == RGP || g == RGP + 1);
+    const int store_bits = SPL ? 3 : (g == RGP ? 1 : 2);
     PostState ps = {};
     CascState cst = {};   // fused control: the stream's controller state
     int cut = -1;
@@ -823,6 +844,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         R.beg[lane] = b;
         R.end[lane] = e;
         R.nst[lane] = valid && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
+        R.pw[0][lane] = R.pw[1][lane] = 0;
     }
     __syncthreads();
     const int phase = R.phase[sc];
@@ -885,6 +907,19 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         x_half();
         if (nsteps > 1) load_x(1);
     }
+    // store the frame outputs the post wave left in slot p (lanes 0..15: the
+    // tile's streams)
+    auto flush = [&](int p) {   // this wave's share: frame t (store_bits 1), t + 1 (2)
+        if (lane < 16) {
+            const int fl = R.pw[p][lane] & store_bits;
+            if (fl) {
+                const int ft = R.pt[p][lane];
+                const int16_t* o = R.po[p][lane];
+                if (fl & 1) put_out(r, s, T, ft, o[0], o[1], o[2], o[3]);
+                if (fl & 2) put_out(r, s, T, ft + 1, o[0], o[1], o[2], o[3]);
+            }
+        }
+    };
     const NnLayer& L2 = img.L[r.li + 1];
     const NnLayer& L3 = img.L[r.li + 2];
     const NnLayer& L4 = img.L[r.li + 3];
@@ -985,19 +1020,25 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
                     RS, tt, lane);
+            if (!SPL) flush(cur ^ 1);
         } else if (g == RGP + 1) {   // stage 2: step j-2
             if (j >= 2 && j - 2 < nsteps)
                 fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                     &R.a3[cur][0][0], RS, tt, lane);
+            if (!SPL) flush(cur ^ 1);
         } else if (SPL && g == RGP + 2) {   // stage 3 (split): step j-3
             if (j >= 3 && j - 3 < nsteps)
                 fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
                     L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                     &R.a4[cur][0][0], RS, tt, lane);
-        } else if (post_w && j >= 3 + SPL && j - 3 - SPL < nsteps) {   // post: step j-3-SPL
+            flush(cur ^ 1);   // the post wave's outputs of the previous iteration
+        } else if (post_w) {   // post: step j-3-SPL
+          int wfl = 0;   // frames of this step to store (bits: t, t + 1)
+          int t = 0;
+          if (j >= 3 + SPL && j - 3 - SPL < nsteps) {
             const int jj = j - 3 - SPL;
-            const int t = b + 2 * jj + phase;
+            t = b + 2 * jj + phase;
             const bool active = valid && t < e;
             if (!SPL) {   // the last FC layer on this wave too
                 fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
@@ -1011,6 +1052,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 int32_t* dst = r.logits + ((size_t)s * T + t) * SH::NOUT;
                 for (int o = q; o < SH::NOUT; o += 4) dst[o] = f32[o];
             }
+            if (clk && j < 64) clk[j * 16 + 2] = (long long)__builtin_amdgcn_s_memtime();
             if (lane < 16 && active && cut < 0) {
                 // logits read from LDS where the post-processing uses them
                 // (s2i: 7, and 2 x 17 only on a detection) -- no register copy
@@ -1018,14 +1060,32 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                     post_proc_s2i_lds(ps, img, f32);
                 else
                     post_proc(ps, img, LdsLogits{f32});
-                put_frame(r, s, T, t, ps);
+            }
+            if (clk && j < 64) clk[j * 16 + 3] = (long long)__builtin_amdgcn_s_memtime();
+            if (lane < 16 && active && cut < 0) {
+                // the controller for frames t and t + 1; their outputs go to
+                // the slot, and another wave stores them next iteration (the
+                // stores and their address arithmetic off this wave, the
+                // pipeline's slowest)
+                wfl = 1;
                 if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) {
                     cut = t;
                 } else if (t + 1 < e) {
-                    put_frame(r, s, T, t + 1, ps);
+                    wfl = 3;
                     if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = t + 1;
                 }
             }
+            if (clk && j < 64) clk[j * 16 + 4] = (long long)__builtin_amdgcn_s_memtime();
+          }
+          if (lane < 16) {
+              R.pw[cur][lane] = wfl;
+              if (wfl) {
+                  R.pt[cur][lane] = t;
+                  *reinterpret_cast<int2*>(R.po[cur][lane]) =
+                      make_int2((int)((uint32_t)(uint16_t)ps.trigger | ((uint32_t)(uint16_t)ps.outputs[0] << 16)),
+                                (int)((uint32_t)(uint16_t)ps.outputs[1] | ((uint32_t)(uint16_t)ps.outputs[2] << 16)));
+              }
+          }
         }
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
         __syncthreads();
@@ -1034,6 +1094,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         iteration(j, std::integral_constant<int, 0>{});
         if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
     }
+    // the last iteration's post outputs (each iteration ends with a barrier)
+    if (store_w) flush((nloop + 2 + SPL) & 1);
     if (ctl) {
         if (post_w && lane < 16) R.cut[lane] = valid ? cut : -1;
         __syncthreads();
@@ -1101,7 +1163,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             ca.seg_begin[s] = b_next;
             if (b_next < T) {
                 want = true;
-                n_next = ca.seq[cst.pos];
+                n_next = nnsp::seq_at(ca, cst.pos);
             }
         }
         nnsp::list_next(ca, n_next, s, want, fr_next);

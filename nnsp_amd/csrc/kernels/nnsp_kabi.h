@@ -223,6 +223,9 @@ int nnspk_free(void *p);
 int nnspk_memset(void *p, int v, size_t n, void *stream);
 int nnspk_h2d(void *d, const void *h, size_t n, void *stream);
 int nnspk_d2h(void *h, const void *d, size_t n, void *stream);
+int nnspk_host_alloc(void **p, size_t n);   /* pinned host memory (asynchronous copies) */
+int nnspk_host_free(void *p);
+int nnspk_event_sync(void *e);
 int nnspk_d2d(void *d, const void *s, size_t n, void *stream);
 int nnspk_sync(void *stream);
 int nnspk_device_count(int *n);
@@ -233,6 +236,7 @@ int nnspk_stream_create(void **s);
 /* high != 0: the device's greatest stream priority (its kernels' workgroups
  * are dispatched ahead of normal-priority streams' when both wait) */
 int nnspk_stream_create_prio(void **s, int high);
+int nnspk_stream_create_cumask(void **s, int free_cus, int spread);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);
@@ -276,6 +280,8 @@ typedef struct CascArgs_ {
     int8_t *fresh;            /* [S] frames the current net ran since its reset (0..2) */
     FeatSrc fs[3];            /* per net id: segment feature source (slot 5 kept at a reset) */
     int32_t *cuts;            /* segments cut by a net switch this chunk (window heuristic), or NULL */
+    int32_t seq_bits;         /* seq[k] in bits 2k..2k+1 (per-lane lookups without a memory load) */
+    int32_t pad_;
 } CascArgs;
 
 int nnspk_launch_casc_begin(const CascArgs *a, void *stream);

@@ -1100,6 +1100,9 @@ int nnspk_d2d(void* d, const void* s, size_t n, void* stream) {
     return ok(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)stream));
 }
 int nnspk_sync(void* stream) { return ok(hipStreamSynchronize((hipStream_t)stream)); }
+int nnspk_host_alloc(void** p, size_t n) { return ok(hipHostMalloc(p, n ? n : 16, hipHostMallocDefault)); }
+int nnspk_host_free(void* p) { return p ? ok(hipHostFree(p)) : 0; }
+int nnspk_event_sync(void* e) { return ok(hipEventSynchronize((hipEvent_t)e)); }
 int nnspk_device_count(int* n) { return ok(hipGetDeviceCount(n)); }
 int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
@@ -1110,6 +1113,21 @@ int nnspk_stream_create_prio(void** s, int high) {
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e != hipSuccess) return (int)e;
     return ok(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
+}
+int nnspk_stream_create_cumask(void** s, int free_cus, int spread) {
+    // a stream whose kernels leave free_cus CUs to the others: the top ones
+    // (spread 0) or every (n / free_cus)-th (spread 1)
+    int n = 0;
+    hipError_t e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
+    if (e != hipSuccess) return (int)e;
+    if (n <= 0 || n > 1024 || free_cus <= 0 || free_cus >= n) return nnspk_stream_create(s);
+    uint32_t m[32] = {0};
+    const int step = n / free_cus;
+    for (int i = 0; i < n; ++i) {
+        const bool off = spread ? (i % step == 0 && i / step < free_cus) : (i >= n - free_cus);
+        if (!off) m[i / 32] |= 1u << (i % 32);
+    }
+    return ok(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)((n + 31) / 32), m));
 }
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }

@@ -51,3 +51,8 @@ for n, b in nets.items():
     for k, nm in enumerate(names):
         d = st[3:valid - 2, 2 * k + 1] - st[3:valid - 2, 2 * k]
         print(f"  {nm:16s} work median {np.median(d):7.0f}")
+    pw = 2 * (len(names) - 1)   # the post wave's slots: start, end, then +2.. its sub-phases
+    sub = st[3:valid - 2, pw:pw + 5]
+    if sub[:, 2].any():
+        print(f"  post: fc/logits {np.median(sub[:, 2] - sub[:, 0]):6.0f}  post_proc {np.median(sub[:, 3] - sub[:, 2]):6.0f}"
+              f"  stores+controller {np.median(sub[:, 4] - sub[:, 3]):6.0f}  to end {np.median(sub[:, 1] - sub[:, 4]):6.0f}")

@@ -11,12 +11,14 @@ one() {  # name env... [-- bench args]
   python3 -c "import json,sys; d=json.loads(open('$O/$n.json').read().strip().splitlines()[-1]); print('$n', round(d['value']/1e6,1), round(d['ms_per_step'],3))"
 }
 one base X=1
-one vad X=1 -- --net vad
-one kws X=1 -- --net kws
-one s2i X=1 -- --net s2i
-one synth X=1 -- --weights synth
-one after0 NNSP_AHEAD_AFTER_ROUND=0
-one prio_after0_blk2048 NNSP_NET_STREAM_PRIO=1 NNSP_AHEAD_AFTER_ROUND=0 NNSP_AHEAD_FE_BLOCKS=2048
-one prio_after0_blk3072 NNSP_NET_STREAM_PRIO=1 NNSP_AHEAD_AFTER_ROUND=0 NNSP_AHEAD_FE_BLOCKS=3072
-one noahead X=1 -- --no-lookahead
+one free16s NNSP_FE_FREE_CUS=16
+one free32s NNSP_FE_FREE_CUS=32
+one free64s NNSP_FE_FREE_CUS=64
+one free32t NNSP_FE_FREE_CUS=32 NNSP_FE_FREE_SPREAD=0
+one free32s_prio NNSP_FE_FREE_CUS=32 NNSP_NET_STREAM_PRIO=1
+one free32s_after0 NNSP_FE_FREE_CUS=32 NNSP_AHEAD_AFTER_ROUND=0
+one free64s_after0 NNSP_FE_FREE_CUS=64 NNSP_AHEAD_AFTER_ROUND=0
+one free32s_after2 NNSP_FE_FREE_CUS=32 NNSP_AHEAD_AFTER_ROUND=2
+one after2 NNSP_AHEAD_AFTER_ROUND=2
+one after3 NNSP_AHEAD_AFTER_ROUND=3
 echo done
