@@ -224,8 +224,8 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
             if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
         }
         if (getenv("NNSP_RECUR_CLOCKS")) { /* development probe of recur_kernel phases */
-            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 16 * 8))) goto fail;
-            if ((e = nnspk_memset(b->d_clk, 0, 64 * 16 * 8, b->stream))) goto fail;
+            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 32 * 8))) goto fail;
+            if ((e = nnspk_memset(b->d_clk, 0, 64 * 32 * 8, b->stream))) goto fail;
         }
     }
     if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
@@ -293,6 +293,7 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     fa.T = T;
     fa.mean = b->d_mean;
     fa.stdR = b->d_stdR;
+    fa.dbg_clk = b->d_clk;
     fa.norm_shift = b->norm_shift;
     fa.feats = b->d_feats;
     fa.list = seg->list;
@@ -494,7 +495,7 @@ int nnsp_batch_set_state(nnsp_batch *b, const void *host, int first, int count)
 int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
 {
     if (!b || !out || !b->d_clk) return NNSP_EINVAL;
-    TRY(nnspk_d2h(out, b->d_clk, 64 * 16 * 8, b->stream));
+    TRY(nnspk_d2h(out, b->d_clk, 64 * 32 * 8, b->stream));
     return nnspk_sync(b->stream);
 }
 

@@ -92,6 +92,7 @@ struct nnsp_cascade {
     int ahead_blocks;               /* grid cap of the look-ahead front end (0: full) */
     int ahead_fpw;                  /* its frames per wave (0: persistent grid) */
     int ahead_after;                /* it starts after this many rounds of the nets */
+    int cold_first;                 /* all nets' cold front ends of a round before their NN kernels */
     int window;                     /* frames per stream and round (0: to the chunk end) */
     int auto_window;                /* pick window per chunk from the last chunk's switch rate */
     int last_cuts;                  /* last chunk: segments cut by a net switch */
@@ -290,6 +291,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->ahead_fpw = af ? atoi(af) : 0;
         const char *aa = getenv("NNSP_AHEAD_AFTER_ROUND");
         c->ahead_after = aa ? atoi(aa) : 1;
+        const char *cf = getenv("NNSP_COLD_FIRST");
+        c->cold_first = cf ? atoi(cf) != 0 : 0;   /* measured: +1 % reference nets, -5 % synthetic */
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
             c->window = atoi(w);
@@ -409,6 +412,43 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     return nnspk_launch_fe(&fa, stream);
 }
 
+/* net n's NN kernels of round r on stream st (after its cold front end);
+ * wait_cold: first wait for the other nets' cold front ends (ev_join) */
+static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
+                    int wait_cold)
+{
+    const int timed = c->timing && r < MAX_TIMED;
+    if (wait_cold)
+        for (int m = 0; m < 3; ++m)
+            if (m != n) TRY(nnspk_stream_wait(st, c->ev_join[m]));
+    nnsp_segment seg;
+    memset(&seg, 0, sizeof seg);
+    seg.list = c->d_list[r & 1][n];
+    seg.n_list_dev = cur + n;
+    seg.seg_begin = c->d_seg_begin;
+    seg.lookback = c->lookback[n];
+    seg.hist = hist;
+    seg.hist_frames = c->H;
+    seg.seg_len = c->window;
+    seg.net_ran = a->net_ran;
+    seg.detected = a->detected;
+    seg.outputs3 = a->outputs3;
+    seg.net_id = n;
+    seg.fs = a->fs[n];
+    seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
+    seg.ctl = c->fused ? a : NULL;
+    TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
+    DBG(st, "proj + recur", n, r);
+    if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
+    if (c->fused) {
+        TRY(nnspk_event_record(c->ev_rnd[r & 1][n], st));
+    } else if (!c->serial) {
+        TRY(nnspk_event_record(c->ev_join[n], st));
+        TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
+    }
+    return 0;
+}
+
 /* One round, asynchronous: the three nets' segments on their own streams
  * (empty lists exit on the device).  Fused control: each net's recur kernel
  * runs the controller for its streams and lists them for the next round, so
@@ -425,6 +465,10 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         a->cold_list[n] = c->d_cold_list[(r + 1) & 1][n];
     }
     if (!c->serial && !c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
+    /* cold frames first: every net's cold front end is queued before any
+     * net's NN kernels may start (ev_join as the cold-done event), so the tiny
+     * cold launches do not wait behind the other nets' proj workgroups */
+    const int cold_first = c->fused && !c->serial && c->cold_first;
     for (int n = 0; n < 3; ++n) {
         void *st = c->serial ? c->stream : c->ns[n];
         const int timed = c->timing && r < MAX_TIMED;
@@ -442,32 +486,11 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
-        nnsp_segment seg;
-        memset(&seg, 0, sizeof seg);
-        seg.list = c->d_list[r & 1][n];
-        seg.n_list_dev = cur + n;
-        seg.seg_begin = c->d_seg_begin;
-        seg.lookback = c->lookback[n];
-        seg.hist = hist;
-        seg.hist_frames = c->H;
-        seg.seg_len = c->window;
-        seg.net_ran = a->net_ran;
-        seg.detected = a->detected;
-        seg.outputs3 = a->outputs3;
-        seg.net_id = n;
-        seg.fs = a->fs[n];
-        seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
-        seg.ctl = c->fused ? a : NULL;
-        TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
-        DBG(st, "proj + recur", n, r);
-        if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
-        if (c->fused) {
-            TRY(nnspk_event_record(c->ev_rnd[r & 1][n], st));
-        } else if (!c->serial) {
-            TRY(nnspk_event_record(c->ev_join[n], st));
-            TRY(nnspk_stream_wait(c->stream, c->ev_join[n]));
-        }
+        if (cold_first) TRY(nnspk_event_record(c->ev_join[n], st));
+        else TRY(round_nn(c, a, r, n, T, cur, hist, st, 0));
     }
+    if (cold_first)
+        for (int n = 0; n < 3; ++n) TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1));
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
 }

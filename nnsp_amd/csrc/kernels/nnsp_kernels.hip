@@ -292,7 +292,11 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     nx.t = nx.b + (int)nx.k;
     uint32_t nxt[4] = {0u, 0u, 0u, 0u};
     if (nx.t < nx.lim) load_frame(nx, nxt);
+    long long* fclk = (a.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? a.dbg_clk + 1024 : nullptr;
+#define FCLK(k) \
+    if (fclk && f - fbeg < 64u) fclk[8 * (f - fbeg) + (k)] = (long long)__builtin_amdgcn_s_memtime()
     for (unsigned f = fbeg; f < fend; ++f) {
+        FCLK(0);
         const Pos cur = nx;
         const uint32_t raw[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
         if (f + 1 < fend) {   // prefetch the next frame's window
@@ -321,7 +325,9 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 v[2 * m + 1] = (int32_t)(int16_t)(wn[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
             }
         }
+        FCLK(1);
         wave_cfft256(v, X, TB, lane);
+        FCLK(2);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
@@ -348,6 +354,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             }
         }
         wave_lds_sync();
+        FCLK(3);
         // ---- Mel (melSpecProc.c:6-27): lane segments of <= 12 MACs (zero-padded), then per bank
         {
             int64_t mac = 0;
@@ -366,6 +373,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             Mp[lane] = mac;
         }
         wave_lds_sync();
+        FCLK(4);
         // ---- log10 (fixlog10.c:53-61), normalise (feature_module.c:67-73)
         if (lane < 40) {
             int64_t mac = 0;
@@ -395,7 +403,9 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             }
         }
         wave_lds_sync();
+        FCLK(5);
     }
+#undef FCLK
 }
 // ============================================================================
 // NN: generic fc / lstm stack on int8 MFMA

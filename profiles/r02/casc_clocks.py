@@ -36,8 +36,9 @@ for c in range(3):
     eng.exec_device(pcm.data_ptr(), T, ran.data_ptr(), det.data_ptr(), o3.data_ptr())
 eng.sync()
 for n, b in nets.items():
-    clk = np.zeros((64, 16), np.int64)
-    _lib.check(L.nnsp_batch_debug_clocks(b.h, C.c_void_p(clk.ctypes.data)), "clocks")
+    raw = np.zeros(2048, np.int64)
+    _lib.check(L.nnsp_batch_debug_clocks(b.h, C.c_void_p(raw.ctypes.data)), "clocks")
+    clk = raw[:1024].reshape(64, 16)
     valid = (clk[:, 0] > 0).sum()
     st = clk[:valid]
     if valid < 8:

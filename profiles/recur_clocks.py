@@ -26,8 +26,10 @@ L.nnsp_synth_pcm(C.c_void_p(pcm.data_ptr()), S, T, C.c_uint64(1), 0, C.c_int64(0
 for _ in range(3):
     eng.exec_device(pcm.data_ptr(), T, trig.data_ptr())
 fe, nn = eng.last_timing()
-clk = np.zeros((64, 16), np.int64)
-_lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clocks")
+raw = np.zeros(2048, np.int64)
+_lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(raw.ctypes.data)), "clocks")
+clk = raw[:1024].reshape(64, 16)
+fclk = raw[1024:].reshape(128, 8)[:64]
 st = clk[:53]
 step = np.diff(st[:, 0])
 print(f"{net} S={S}: fe {fe:.3f} ms nn {nn:.3f} ms; iteration cycles median {np.median(step[3:48]):.0f}")
@@ -38,3 +40,19 @@ for k, nm in enumerate(names):
     d = st[3:50, 2 * k + 1] - st[3:50, 2 * k]
     lag = st[3:50, 2 * k] - st[3:50, 0]
     print(f"  {nm:16s} work median {np.median(d):7.0f}  start lag {np.median(lag):6.0f}")
+# proj_kernel wave 0 of workgroup 0 (slots 12-15 per tile: start, union loaded, FC done, x stored)
+pj = clk[:, 12:16]
+nt = int((pj[:, 0] > 0).sum())
+if nt > 2:
+    d = np.diff(pj[:nt], axis=1)
+    tile = np.diff(pj[:nt, 0])
+    print(f"  proj tiles {nt}: per tile median {np.median(tile):.0f} cycles; union {np.median(d[:, 0]):.0f}"
+          f"  fc {np.median(d[:, 1]):.0f}  x store {np.median(d[:, 2]):.0f}")
+# fe_kernel wave 0 of workgroup 0, per frame: start, window, cFFT, split+power, Mel, log+normalise
+nf = int((fclk[:, 0] > 0).sum())
+if nf > 2:
+    d = np.diff(fclk[:nf, :6], axis=1)
+    fr = np.diff(fclk[:nf, 0])
+    print(f"  fe frames {nf}: per frame median {np.median(fr):.0f} cycles; window {np.median(d[:, 0]):.0f}"
+          f"  cfft {np.median(d[:, 1]):.0f}  split+pspec {np.median(d[:, 2]):.0f}  mel {np.median(d[:, 3]):.0f}"
+          f"  log+norm {np.median(d[:, 4]):.0f}")
