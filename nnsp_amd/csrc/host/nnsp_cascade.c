@@ -33,6 +33,7 @@
  * which launch failed (asynchronous faults otherwise surface at a later sync) */
 static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n, int r);
 static int book_take(nnsp_cascade *c);
+static int ahead_read(nnsp_cascade *c, int q, int wait);
 #define DBG(st, what, n, r)                                  \
     do {                                                     \
         if (c->debug) TRY(dbg_step(c, (st), (what), (n), (r))); \
@@ -78,6 +79,14 @@ struct nnsp_cascade {
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation) */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
+    /* XCD partition for chunks with a look-ahead front end: it runs on the
+     * CUs [0, part) of fe_stream while the nets' rounds run on the other
+     * CUs (own_ns); other chunks use the unmasked streams */
+    int part;                       /* CUs of the front end's partition (0: off) */
+    void *fe_stream;                /* look-ahead front end, CU-masked */
+    void *own_ns[3];                /* the nets' CU-masked streams */
+    void *ev_fe_dep;                /* fe_stream waits for the cascade's stream there */
+    int ahead_on_fe;                /* the last look-ahead ran on fe_stream */
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
@@ -86,8 +95,11 @@ struct nnsp_cascade {
     int last_rounds, launched;
     const int16_t *pre_pcm;         /* the chunk whose shared front end the last call ran ahead */
     int pre_T;
-    void *ev_ahead[2];
-    float ahead_ms, prev_ahead_ms;  /* look-ahead front end: this call's, the previous call's */
+    /* look-ahead front end of chunk q (events by chunk parity q & 1: around
+     * the launch; read without waiting once it has finished, or by sync) */
+    void *ev_ahead[2][2];
+    int ahead_pending[2];
+    float ahead_ms[2];
     int sfe_ahead;                  /* last chunk's shared front end ran in the previous call */
     int ahead_blocks;               /* grid cap of the look-ahead front end (0: full) */
     int ahead_fpw;                  /* its frames per wave (0: persistent grid) */
@@ -166,24 +178,44 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
     c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
-    {   /* NNSP_FE_FREE_CUS=N: the cascade's stream (shared front end, look-ahead
-         * included) leaves N CUs to the nets' rounds (experiment) */
+    {   /* experiment: NNSP_FE_FREE_CUS=N: the cascade's stream leaves N CUs to the nets */
         const char *fc = getenv("NNSP_FE_FREE_CUS");
         const char *fs = getenv("NNSP_FE_FREE_SPREAD");
-        if ((e = fc ? nnspk_stream_create_cumask(&c->stream, atoi(fc), fs ? atoi(fs) : 1)
-                    : nnspk_stream_create(&c->stream)))
-            goto fail;
+        e = fc ? nnspk_stream_create_cumask(&c->stream, atoi(fc), fs ? atoi(fs) : 1) : nnspk_stream_create(&c->stream);
+        if (e) goto fail;
+    }
+    {   /* experiment (off unless NNSP_PART_FE=F): the XCD partition of
+         * look-ahead chunks -- the look-ahead front end on F CUs (MI355X: 256
+         * CUs in 8 XCDs of 32, CU i on XCD i % 8; F = 192: 6 XCDs), the nets'
+         * rounds on the others.  With the cascade's own stream masked as well it
+         * measured +2.4 % (paired A/B); in this form, with the front end on a
+         * stream of its own so that the call returns before it ends, -7 %
+         * (profiles/r02/sched).  A partition that splits an XCD: -15 %. */
+        int cus = 0, clk = 0;
+        char arch[64];
+        if (nnspk_device_info(&cus, &clk, arch, (int)sizeof arch)) cus = 0;
+        const char *pf = getenv("NNSP_PART_FE");
+        c->part = pf ? atoi(pf) : 0;
+        if (c->part > 0 && c->part < cus) {
+            if ((e = nnspk_stream_create_cupart(&c->fe_stream, 0, c->part, 1))) goto fail;
+            for (int n = 0; n < 3; ++n)
+                if ((e = nnspk_stream_create_cupart(&c->own_ns[n], c->part, cus, 1))) goto fail;
+            if ((e = nnspk_event_create(&c->ev_fe_dep))) goto fail;
+        } else {
+            c->part = 0;
+        }
     }
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
-    if ((e = nnspk_event_create(&c->ev_ahead[0])) || (e = nnspk_event_create(&c->ev_ahead[1]))) goto fail;
+    for (int q = 0; q < 2; ++q)
+        if ((e = nnspk_event_create(&c->ev_ahead[q][0])) || (e = nnspk_event_create(&c->ev_ahead[q][1]))) goto fail;
     for (int n = 0; n < 3; ++n) {
         /* each net's rounds run on its batch's own stream: the cascade adds
          * one stream (c->stream) to the three, so on a device with four
          * hardware queues (HIP's default) the look-ahead front end on
          * c->stream never shares an in-order queue with a net's rounds */
-        c->ns[n] = nets[n]->stream;
+        c->ns[n] = nets[n]->stream;   /* per chunk: own_ns[n] when partitioned */
         if ((e = nnspk_event_create(&c->ev_join[n])) ||
             (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
             goto fail;
@@ -290,7 +322,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         const char *af = getenv("NNSP_AHEAD_FE_FPW");
         c->ahead_fpw = af ? atoi(af) : 0;
         const char *aa = getenv("NNSP_AHEAD_AFTER_ROUND");
-        c->ahead_after = aa ? atoi(aa) : 1;
+        c->ahead_after = aa ? atoi(aa) : (c->part ? 0 : 1);
         const char *cf = getenv("NNSP_COLD_FIRST");
         c->cold_first = cf ? atoi(cf) != 0 : 0;   /* measured: +1 % reference nets, -5 % synthetic */
         const char *w = getenv("NNSP_CASCADE_WINDOW");
@@ -324,8 +356,10 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         nnspk_event_destroy(c->ev_fe[i]);
     }
     nnspk_event_destroy(c->ev_fork);
-    nnspk_event_destroy(c->ev_ahead[0]);
-    nnspk_event_destroy(c->ev_ahead[1]);
+    for (int q = 0; q < 2; ++q) {
+        nnspk_event_destroy(c->ev_ahead[q][0]);
+        nnspk_event_destroy(c->ev_ahead[q][1]);
+    }
     for (int n = 0; n < 3; ++n) {
         nnspk_event_destroy(c->ev_join[n]);
         nnspk_event_destroy(c->ev_rnd[0][n]);
@@ -333,7 +367,12 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
         c->ns[n] = NULL; /* the batch's stream, owned by the batch */
+        nnspk_stream_destroy(c->own_ns[n]);
+        c->own_ns[n] = NULL;
     }
+    if (c->fe_stream) nnspk_sync(c->fe_stream);
+    nnspk_stream_destroy(c->fe_stream);
+    nnspk_event_destroy(c->ev_fe_dep);
     nnspk_stream_destroy(c->stream);
     nnspk_event_destroy(c->ev_book);
     nnspk_host_free(c->h_book);
@@ -344,6 +383,8 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
+    if (c->fe_stream) TRY(nnspk_sync(c->fe_stream)); /* a look-ahead front end writes ring slots */
+    c->ahead_on_fe = 0;
     TRY(book_take(c));
     for (int i = 0; i < 3; ++i) TRY(nnsp_batch_reset(c->net[i], mask)); /* synchronous */
     const uint8_t *dm = NULL;
@@ -508,7 +549,7 @@ static int join_rounds(nnsp_cascade *c, int r)
  * when T >= H) on the cascade's stream.  tail: the samples of the two frames
  * before the chunk, tail_stride apart per stream. */
 static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *tail, int tail_stride, int abs0,
-                     long long k, int ahead)
+                     long long k, int ahead, void *stream)
 {
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
@@ -536,12 +577,24 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
         fa.hist_out = c->d_hist[(k + 1) % 3];
         fa.hist_frames = c->H;
     }
-    return nnspk_launch_fe(&fa, c->stream);
+    return nnspk_launch_fe(&fa, stream);
 }
 
 /* The last chunk's bookkeeping: wait for the pinned copy of its counters
  * (long done by the time the host comes back) and derive the host-side
  * statistics and the next chunk's window. */
+/* the duration of look-ahead slot q, once its front end has finished (wait:
+ * block until it has) */
+static int ahead_read(nnsp_cascade *c, int q, int wait)
+{
+    if (!c->ahead_pending[q]) return 0;
+    if (!wait && !nnspk_event_done(c->ev_ahead[q][1])) return 0;
+    TRY(nnspk_event_sync(c->ev_ahead[q][1]));
+    TRY(nnspk_event_elapsed(&c->ahead_ms[q], c->ev_ahead[q][0], c->ev_ahead[q][1]));
+    c->ahead_pending[q] = 0;
+    return 0;
+}
+
 static int book_take(nnsp_cascade *c)
 {
     if (!c->book_pending) return 0;
@@ -563,12 +616,15 @@ static int book_take(nnsp_cascade *c)
         const double per = (double)c->last_cuts / (double)c->S;
         c->window = per < 0.5 ? 0 : (per < 2.0 ? 32 : 16);
     }
-    TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
-    c->ahead_ms = 0.f;
-    if (ahead) TRY(nnspk_event_elapsed(&c->ahead_ms, c->ev_ahead[0], c->ev_ahead[1]));
-    /* the shared front end of this chunk: timed here, or by the previous call (ahead) */
-    if (c->book_ahead_done) c->sfe_ms = c->prev_ahead_ms;
-    c->prev_ahead_ms = c->ahead_ms;
+    (void)ahead;
+    /* the shared front end of that chunk: run in the call (ev_fe), or ahead by
+     * the previous call (its slot, once finished; else the last known value) */
+    if (!c->book_ahead_done) {
+        TRY(nnspk_event_elapsed(&c->sfe_ms, c->ev_fe[0], c->ev_fe[1]));
+    } else {
+        TRY(ahead_read(c, (int)((c->chunk - 1) & 1), 0));
+        c->sfe_ms = c->ahead_ms[(c->chunk - 1) & 1];
+    }
     memcpy(c->rc, rc, sizeof c->rc);
     memset(c->rfe, 0, sizeof c->rfe);
     memset(c->rnn, 0, sizeof c->rnn);
@@ -606,6 +662,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         return NNSP_EINVAL;
     }
     TRY(book_take(c)); /* the last chunk's counters: rounds, switches (this chunk's window) */
+    const long long k = c->chunk;
     CascArgs a = c->a;
     a.T = T;
     a.seg_len = c->window;
@@ -613,13 +670,25 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     a.detected = detected;
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
-    const long long k = c->chunk;
     TRY(nnspk_event_record(c->ev[0], c->stream)); /* the counters (d_zero) were cleared by the last chunk */
+    /* a look-ahead front end of the last call on fe_stream: this chunk's work
+     * (its features, or, if it was not used, its ring slots) comes after it */
+    if (c->ahead_on_fe) {
+        TRY(nnspk_stream_wait(c->stream, c->ev_ahead[k & 1][1]));
+        c->ahead_on_fe = 0;
+    }
+    /* look-ahead: the next chunk's shared front end runs while this chunk's
+     * rounds run (it writes ring slots and a history buffer this chunk does not
+     * read; its STFT tail is this chunk's last two frames).  With the XCD
+     * partition it runs on fe_stream's CUs and the nets on theirs. */
+    const int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
+    const int part = ahead && c->part > 0;
+    for (int n = 0; n < 3; ++n) c->ns[n] = part ? c->own_ns[n] : c->net[n]->stream;
     /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
     TRY(nnspk_event_record(c->ev_fe[0], c->stream));
-    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0));
+    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0, c->stream));
     DBG(c->stream, "shared front end", -1, -1);
     TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     c->sfe_ahead = ahead_done;
@@ -639,21 +708,25 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     TRY(nnspk_launch_casc_begin(&a, c->stream));
     DBG(c->stream, "casc_begin", -1, -1);
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
-    /* look-ahead: the next chunk's shared front end, queued on the cascade's
-     * stream behind the fork -- it runs while the nets' rounds of this chunk
-     * run on their streams (it writes ring slots and a history buffer this
-     * chunk does not read; its STFT tail is this chunk's last two frames) */
-    int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
     int ahead_launched = 0;
     /* the look-ahead front end starts once the nets' first ahead_after rounds
      * (the bulk of the chunk's NN work) are queued behind: running beside
      * them from the start it slowed them more than it gained */
 #define LAUNCH_AHEAD()                                                                                         \
     do {                                                                                                       \
-        TRY(nnspk_event_record(c->ev_ahead[0], c->stream));                                                    \
+        const int q_ = (int)((k + 1) & 1);                                                                     \
+        TRY(ahead_read(c, q_, 1)); /* slot q_'s last front end (two chunks ago) is long done */               \
+        void *fs_ = part ? c->fe_stream : c->stream;                                                           \
+        if (part) {                                                                                            \
+            TRY(nnspk_event_record(c->ev_fe_dep, c->stream));                                                  \
+            TRY(nnspk_stream_wait(fs_, c->ev_fe_dep));                                                         \
+        }                                                                                                      \
+        TRY(nnspk_event_record(c->ev_ahead[q_][0], fs_));                                                      \
         TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring,     \
-                      k + 1, 1));                                                                              \
-        TRY(nnspk_event_record(c->ev_ahead[1], c->stream));                                                    \
+                      k + 1, 1, fs_));                                                                         \
+        TRY(nnspk_event_record(c->ev_ahead[q_][1], fs_));                                                      \
+        c->ahead_pending[q_] = 1;                                                                              \
+        c->ahead_on_fe = part;                                                                                 \
         ahead_launched = 1;                                                                                    \
     } while (0)
     if (ahead && c->ahead_after <= 0) LAUNCH_AHEAD();
@@ -756,7 +829,10 @@ int nnsp_cascade_sync(nnsp_cascade *c)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
-    return book_take(c);
+    if (c->fe_stream) TRY(nnspk_sync(c->fe_stream));
+    TRY(book_take(c));
+    for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
+    return 0;
 }
 void *nnsp_cascade_stream(nnsp_cascade *c) { return c ? c->stream : NULL; }
 

@@ -228,6 +228,7 @@ int nnspk_d2h(void *h, const void *d, size_t n, void *stream);
 int nnspk_host_alloc(void **p, size_t n);   /* pinned host memory (asynchronous copies) */
 int nnspk_host_free(void *p);
 int nnspk_event_sync(void *e);
+int nnspk_event_done(void *e);              /* 1: the event has completed (no wait) */
 int nnspk_d2d(void *d, const void *s, size_t n, void *stream);
 int nnspk_sync(void *stream);
 int nnspk_device_count(int *n);
@@ -239,6 +240,7 @@ int nnspk_stream_create(void **s);
  * are dispatched ahead of normal-priority streams' when both wait) */
 int nnspk_stream_create_prio(void **s, int high);
 int nnspk_stream_create_cumask(void **s, int free_cus, int spread);
+int nnspk_stream_create_cupart(void **s, int lo, int hi, int spread);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);

@@ -1113,6 +1113,7 @@ int nnspk_sync(void* stream) { return ok(hipStreamSynchronize((hipStream_t)strea
 int nnspk_host_alloc(void** p, size_t n) { return ok(hipHostMalloc(p, n ? n : 16, hipHostMallocDefault)); }
 int nnspk_host_free(void* p) { return p ? ok(hipHostFree(p)) : 0; }
 int nnspk_event_sync(void* e) { return ok(hipEventSynchronize((hipEvent_t)e)); }
+int nnspk_event_done(void* e) { return hipEventQuery((hipEvent_t)e) == hipSuccess; }
 int nnspk_device_count(int* n) { return ok(hipGetDeviceCount(n)); }
 int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
@@ -1123,6 +1124,21 @@ int nnspk_stream_create_prio(void** s, int high) {
     hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
     if (e != hipSuccess) return (int)e;
     return ok(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
+}
+// a stream on the CUs [lo, hi) of the device's n (spread 1: CU i counts as
+// i' = (i % 8) * (n / 8) + i / 8, i.e. the partition takes the same share of
+// every 8th CU)
+int nnspk_stream_create_cupart(void** s, int lo, int hi, int spread) {
+    int n = 0;
+    hipError_t e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
+    if (e != hipSuccess) return (int)e;
+    if (n <= 0 || n > 1024 || lo < 0 || hi > n || lo >= hi) return nnspk_stream_create(s);
+    uint32_t m[32] = {0};
+    for (int i = 0; i < n; ++i) {
+        const int ip = spread ? (i % 8) * (n / 8) + i / 8 : i;
+        if (ip >= lo && ip < hi) m[i / 32] |= 1u << (i % 32);
+    }
+    return ok(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)((n + 31) / 32), m));
 }
 int nnspk_stream_create_cumask(void** s, int free_cus, int spread) {
     // a stream whose kernels leave free_cus CUs to the others: the top ones
