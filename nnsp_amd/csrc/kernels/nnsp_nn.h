@@ -77,7 +77,9 @@ __device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) 
 __device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
                                       int part) {
     if (!fs.nring) return *reinterpret_cast<const int4*>(feats + ((size_t)s * T + t) * 40 + 8 * part);
-    const bool cold = t - b + fs.fresh[s] < 2;
+    // only the first two frames of a segment can be cold: the fresh[] load
+    // (and the dependent-load latency) only for those
+    const bool cold = t - b < 2 && t - b + fs.fresh[s] < 2;
     const unsigned slot = (unsigned)(fs.abs0 + t - fs.lookback + fs.ring) % (unsigned)fs.ring;
     const size_t row = cold ? (size_t)s * T + t : (size_t)s * fs.ring + slot;
     const uintptr_t base = cold ? (uintptr_t)feats : (uintptr_t)fs.nring;
