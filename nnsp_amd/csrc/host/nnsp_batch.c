@@ -368,6 +368,8 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             if (need < blocks) blocks = (int)need;
         }
         TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
+        for (int i = 0; i < 2; ++i)
+            if (seg->recur_wait[i]) TRY(nnspk_stream_wait(stream, seg->recur_wait[i]));
         f.a_off = b->rec_a_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;

@@ -105,6 +105,7 @@ struct nnsp_cascade {
     int ahead_fpw;                  /* its frames per wave (0: persistent grid) */
     int ahead_after;                /* it starts after this many rounds of the nets */
     int cold_first;                 /* all nets' cold front ends of a round before their NN kernels */
+    int vad_last;                   /* VAD's recurrence after S2I's and KWS's in each round */
     int window;                     /* frames per stream and round (0: to the chunk end) */
     int auto_window;                /* pick window per chunk from the last chunk's switch rate */
     int last_cuts;                  /* last chunk: segments cut by a net switch */
@@ -325,6 +326,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->ahead_after = aa ? atoi(aa) : (c->part ? 0 : 1);
         const char *cf = getenv("NNSP_COLD_FIRST");
         c->cold_first = cf ? atoi(cf) != 0 : 0;   /* measured: +1 % reference nets, -5 % synthetic */
+        const char *vl = getenv("NNSP_VAD_LAST");
+        c->vad_last = vl ? atoi(vl) != 0 : 0;   /* measured: -2 % reference nets, -7 % synthetic */
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
             c->window = atoi(w);
@@ -456,7 +459,7 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
 static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
-                    int wait_cold)
+                    int wait_cold, void *const recur_wait[2])
 {
     const int timed = c->timing && r < MAX_TIMED;
     if (wait_cold)
@@ -478,6 +481,10 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
     seg.fs = a->fs[n];
     seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
     seg.ctl = c->fused ? a : NULL;
+    if (recur_wait) {
+        seg.recur_wait[0] = recur_wait[0];
+        seg.recur_wait[1] = recur_wait[1];
+    }
     TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
     DBG(st, "proj + recur", n, r);
     if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
@@ -510,7 +517,15 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
      * net's NN kernels may start (ev_join as the cold-done event), so the tiny
      * cold launches do not wait behind the other nets' proj workgroups */
     const int cold_first = c->fused && !c->serial && c->cold_first;
-    for (int n = 0; n < 3; ++n) {
+    /* VAD last (experiment, NNSP_VAD_LAST=1): its recurrence waits for the
+     * S2I and KWS recurrences of the round, so that their 12-wave workgroups
+     * find whole CUs.  Measured slower: S2I and KWS alone still take 0.4-0.5 ms
+     * in round 0 (396 whole-CU workgroups on 256 CUs), and VAD's then follows. */
+    const int vad_last = c->fused && !c->serial && c->vad_last;
+    static const int order_vad_last[3] = {0, 2, 1}, order_plain[3] = {0, 1, 2};
+    const int *order = vad_last ? order_vad_last : order_plain;
+    for (int i = 0; i < 3; ++i) {
+        const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];
         const int timed = c->timing && r < MAX_TIMED;
         if (c->fused) {
@@ -528,10 +543,25 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
         if (cold_first) TRY(nnspk_event_record(c->ev_join[n], st));
-        else TRY(round_nn(c, a, r, n, T, cur, hist, st, 0));
+        else {
+            void *w[2] = {NULL, NULL};
+            if (vad_last && n == 1) {
+                w[0] = c->ev_rnd[r & 1][0];
+                w[1] = c->ev_rnd[r & 1][2];
+            }
+            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w));
+        }
     }
     if (cold_first)
-        for (int n = 0; n < 3; ++n) TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1));
+        for (int i = 0; i < 3; ++i) {
+            const int n = order[i];
+            void *w[2] = {NULL, NULL};
+            if (vad_last && n == 1) {
+                w[0] = c->ev_rnd[r & 1][0];
+                w[1] = c->ev_rnd[r & 1][2];
+            }
+            TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1, w));
+        }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
 }

@@ -86,6 +86,7 @@ typedef struct {
     int16_t *detected, *outputs3;
     int net_id;
     const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
+    void *recur_wait[2];       /* events the stream waits for between proj and recur (NULL: none) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

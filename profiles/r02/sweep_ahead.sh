@@ -10,16 +10,14 @@ one() {  # name env... [-- bench args]
   env "${E[@]}" timeout -k 10 150 python -u bench.py --no-cpu-baseline --no-stress --steps 10 --warmup 2 "$@" > $O/$n.json 2>> $O/err.log || { echo "$n failed"; exit 4; }
   python3 -c "import json,sys; d=json.loads(open('$O/$n.json').read().strip().splitlines()[-1]); print('$n', round(d['value']/1e6,1), round(d['ms_per_step'],3))"
 }
-one p0 X=1
-one q0 GPU_MAX_HW_QUEUES=8
-one b0 NNSP_PART_FE=0
-one c0 NNSP_PART_FE=0 GPU_MAX_HW_QUEUES=8
-one p1 X=1
-one q1 GPU_MAX_HW_QUEUES=8
-one b1 NNSP_PART_FE=0
-one c1 NNSP_PART_FE=0 GPU_MAX_HW_QUEUES=8
-one p2 X=1
-one q2 GPU_MAX_HW_QUEUES=8
-one b2 NNSP_PART_FE=0
-one c2 NNSP_PART_FE=0 GPU_MAX_HW_QUEUES=8
+one v0 X=1
+one n0 NNSP_VAD_LAST=0
+one v1 X=1
+one n1 NNSP_VAD_LAST=0
+one v2 X=1
+one n2 NNSP_VAD_LAST=0
+one vs X=1 -- --weights synth
+one ns NNSP_VAD_LAST=0 -- --weights synth
+one vs2 X=1 -- --weights synth
+one ns2 NNSP_VAD_LAST=0 -- --weights synth
 echo done
