@@ -871,24 +871,28 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     constexpr int XS = SH::XS;
     v4i axh[RPW], axl[RPW];
     int4 xr[nkt_r][2];
+    // The loads land in xr untouched (lanes past the row read column 0 of it)
+    // and x_half zeroes those lanes: any use of a load result right after it
+    // (a select, a copy) made the wave wait the full load latency every step.
     auto load_x = [&](int jj) {   // raw x of step jj for the lane's stream (B-fragment layout)
         const bool ok = valid && b + 2 * jj + phase < e;
         const int16_t* src = r.xg + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * XS;
 #pragma unroll
-        for (int kt = 0; kt < nkt_r; ++kt) {   // branch-free: lanes past the row load column 0, then zero
+        for (int kt = 0; kt < nkt_r; ++kt) {
             const int k0 = 64 * kt + 16 * q;
-            const bool in = k0 < XS;
-            const int16_t* p = src + (in ? k0 : 0);
-            const int4 lo = *reinterpret_cast<const int4*>(p), hi = *reinterpret_cast<const int4*>(p + 8);
-            const int4 z = make_int4(0, 0, 0, 0);
-            xr[kt][0] = in ? lo : z;
-            xr[kt][1] = in ? hi : z;
+            const int16_t* p = src + (k0 < XS ? k0 : 0);
+            xr[kt][0] = *reinterpret_cast<const int4*>(p);
+            xr[kt][1] = *reinterpret_cast<const int4*>(p + 8);
         }
     };
     auto x_half = [&]() {   // axh/axl := Wx . x (hi / lo planes) from xr
         v4i bxh[nkt_r], bxl[nkt_r];
 #pragma unroll
-        for (int kt = 0; kt < nkt_r; ++kt) split_hilo_r(xr[kt][0], xr[kt][1], bxh[kt], bxl[kt]);
+        for (int kt = 0; kt < nkt_r; ++kt) {
+            const bool in = 64 * kt + 16 * q < XS;
+            const int4 z = make_int4(0, 0, 0, 0);
+            split_hilo_r(in ? xr[kt][0] : z, in ? xr[kt][1] : z, bxh[kt], bxl[kt]);
+        }
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {   // one row tile's fragments at a time (no LDS stores here)
             axh[k] = v4i{0, 0, 0, 0};
@@ -902,10 +906,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 }
         }
     };
-    if (g < RGP && nsteps > 0) {
+    if (g < RGP) {   // (past the segment: row 0 of xg, unused)
         load_x(0);
         x_half();
-        if (nsteps > 1) load_x(1);
+        load_x(1);
     }
     // store the frame outputs the post wave left in slot p (lanes 0..15: the
     // tile's streams)
@@ -932,6 +936,11 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // loop runs two iterations per trip), so every LDS access of the stages
     // has a constant offset -- indexing the double buffers with a run-time
     // parity cost the S2I post wave ~1100 of its ~6000 cycles per step
+    // LSTM wave 0's sub-phases (dbg_clk[1536 + 8 j + k]): loads + MFMA, gates, stores, x_half, load_x
+    // (in time order 0, 3, 4, 1, 2)
+    long long* lclk = (clk && g == 0) ? r.dbg_clk + 1536 : nullptr;
+#define LCLK(k) \
+    if (lclk && j < 64) lclk[8 * j + (k)] = (long long)__builtin_amdgcn_s_memtime()
     auto iteration = [&](const int j, auto CUR) {
         constexpr int cur = decltype(CUR)::value;
         if (clk && j < 64) clk[j * 16] = (long long)__builtin_amdgcn_s_memtime();
@@ -975,6 +984,17 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                             hl[k] = mfma8(w[k][kt], bl[kt], hl[k]);
                         }
                 }
+                LCLK(0);
+                // the input half of step j + 1 (axh/axl are free now: consumed
+                // above) and the prefetch of x for step j + 2, ahead of the
+                // gates: the x_half MFMAs run beside the gates' VALU work and
+                // the loads have the gates and stores to land in -- issued at
+                // the end of the step, the copy into the loop-carried xr at the
+                // loop latch waited out their latency every step
+                x_half();
+                LCLK(3);
+                load_x(j + 2);
+                LCLK(4);
                 int32_t c_new[RPW];
                 int16_t hv[RPW];
 #pragma unroll
@@ -1001,6 +1021,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                         hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
                     }
                 }
+                LCLK(1);
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
                     const int rt = g + RGP * k;
@@ -1010,10 +1031,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                         R.h[cur ^ 1][sc][u] = active ? hv[k] : h_old[k];   // h after all groups (T6)
                     }
                 }
-                if (j + 1 < nsteps) {   // the next step's input half, then its successor's x
-                    x_half();
-                    if (j + 2 < nsteps) load_x(j + 2);
-                }
+                LCLK(2);
             }
         } else if (g == RGP) {   // stage 1: step j-1
             if (j >= 1 && j - 1 < nsteps)
@@ -1094,6 +1112,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         iteration(j, std::integral_constant<int, 0>{});
         if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
     }
+#undef LCLK
     // the last iteration's post outputs (each iteration ends with a barrier)
     if (store_w) flush((nloop + 2 + SPL) & 1);
     if (ctl) {

@@ -52,6 +52,13 @@ for n, b in nets.items():
     for k, nm in enumerate(names):
         d = st[3:valid - 2, 2 * k + 1] - st[3:valid - 2, 2 * k]
         print(f"  {nm:16s} work median {np.median(d):7.0f}")
+    lw = raw[1536:2048].reshape(64, 8)[:valid]
+    if lw[3:valid - 6, 4].any():
+        d = lw[3:valid - 6]
+        # probe order in time: 0 (loads + MFMA), 3 (x_half), 4 (load_x), 1 (gates), 2 (stores)
+        print(f"  lstm: loads+mfma {np.median(d[:, 0] - st[3:valid - 6, 0]):6.0f}  x_half {np.median(d[:, 3] - d[:, 0]):6.0f}"
+              f"  load_x {np.median(d[:, 4] - d[:, 3]):6.0f}  gates {np.median(d[:, 1] - d[:, 4]):6.0f}"
+              f"  h/c stores {np.median(d[:, 2] - d[:, 1]):6.0f}  rest {np.median(st[4:valid - 5, 0] - d[:, 2]):6.0f}")
     pw = 2 * (len(names) - 1)   # the post wave's slots: start, end, then +2.. its sub-phases
     sub = st[3:valid - 2, pw:pw + 5]
     if sub[:, 2].any():
