@@ -137,6 +137,10 @@ static void plan_fast(nnsp_batch *b)
     b->fast = 1;
 }
 
+/* NNSP_RECUR_CLOCKS probe buffer: 2048 longs of phase clocks, then
+ * fe_kernel's per-wave records (4 longs per wave, 32768 waves) */
+#define DCLK_LONGS (2048 + 4 * 32768)
+
 #define TRY(x)                 \
     do {                       \
         int _e = (x);          \
@@ -224,8 +228,8 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
             if ((e = nnspk_malloc((void **)&b->d_gx, S * (size_t)b->nstep_max * rows * 4))) goto fail;
         }
         if (getenv("NNSP_RECUR_CLOCKS")) { /* development probe of recur_kernel phases */
-            if ((e = nnspk_malloc((void **)&b->d_clk, 64 * 32 * 8))) goto fail;
-            if ((e = nnspk_memset(b->d_clk, 0, 64 * 32 * 8, b->stream))) goto fail;
+            if ((e = nnspk_malloc((void **)&b->d_clk, DCLK_LONGS * 8))) goto fail;
+            if ((e = nnspk_memset(b->d_clk, 0, DCLK_LONGS * 8, b->stream))) goto fail;
         }
     }
     if ((e = nnspk_h2d(b->d_mean, mean, 40 * 4, b->stream))) goto fail;
@@ -498,6 +502,15 @@ int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
 {
     if (!b || !out || !b->d_clk) return NNSP_EINVAL;
     TRY(nnspk_d2h(out, b->d_clk, 64 * 32 * 8, b->stream));
+    return nnspk_sync(b->stream);
+}
+
+/* development probe: the first n longs of the clock buffer (past the 2048 of
+ * nnsp_batch_debug_clocks: fe_kernel's per-wave records, 4 longs per wave) */
+int nnsp_batch_debug_clocks_n(nnsp_batch *b, long long *out, int n)
+{
+    if (!b || !out || !b->d_clk || n <= 0 || n > DCLK_LONGS) return NNSP_EINVAL;
+    TRY(nnspk_d2h(out, b->d_clk, (size_t)n * 8, b->stream));
     return nnspk_sync(b->stream);
 }
 

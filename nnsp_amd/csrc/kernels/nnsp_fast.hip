@@ -941,10 +941,11 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     long long* lclk = (clk && g == 0) ? r.dbg_clk + 1536 : nullptr;
 #define LCLK(k) \
     if (lclk && j < 64) lclk[8 * j + (k)] = (long long)__builtin_amdgcn_s_memtime()
-    auto iteration = [&](const int j, auto CUR) {
+    auto iteration = [&](const int j, auto CUR, auto RL) {
         constexpr int cur = decltype(CUR)::value;
+        constexpr int role = decltype(RL)::value;   // 0 LSTM, 1-3 FC stages 1-3, 4 post
         if (clk && j < 64) clk[j * 16] = (long long)__builtin_amdgcn_s_memtime();
-        if (g < RGP) {
+        if constexpr (role == 0) {
             if (j < nsteps) {
                 // ---- LSTM step j: row tile = 4 units x gates i, j, f, o
                 const int t = b + 2 * j + phase;
@@ -1033,25 +1034,25 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 }
                 LCLK(2);
             }
-        } else if (g == RGP) {   // stage 1: step j-1
+        } else if constexpr (role == 1) {   // stage 1: step j-1
             if (j >= 1 && j - 1 < nsteps)
                 fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
                     RS, tt, lane);
             if (!SPL) flush(cur ^ 1);
-        } else if (g == RGP + 1) {   // stage 2: step j-2
+        } else if constexpr (role == 2) {   // stage 2: step j-2
             if (j >= 2 && j - 2 < nsteps)
                 fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
                     L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                     &R.a3[cur][0][0], RS, tt, lane);
             if (!SPL) flush(cur ^ 1);
-        } else if (SPL && g == RGP + 2) {   // stage 3 (split): step j-3
+        } else if constexpr (role == 3) {   // stage 3 (split): step j-3
             if (j >= 3 && j - 3 < nsteps)
                 fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
                     L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                     &R.a4[cur][0][0], RS, tt, lane);
             flush(cur ^ 1);   // the post wave's outputs of the previous iteration
-        } else if (post_w) {   // post: step j-3-SPL
+        } else {   // post: step j-3-SPL
           int wfl = 0;   // frames of this step to store (bits: t, t + 1)
           int t = 0;
           if (j >= 3 + SPL && j - 3 - SPL < nsteps) {
@@ -1108,10 +1109,26 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
         __syncthreads();
     };
-    for (int j = 0; j < nloop + 3 + SPL; j += 2) {
-        iteration(j, std::integral_constant<int, 0>{});
-        if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{});
-    }
+    // one loop per wave role (the same trip count, so the same barriers):
+    // in one loop over all roles the compiler kept every role's uniform
+    // values live across it, spilled ~170 SGPRs to VGPR lanes and paid a
+    // v_readlane (a VALU issue) per use -- 15-20 % of the kernel's VALU code
+    auto run = [&](auto RL) {
+        for (int j = 0; j < nloop + 3 + SPL; j += 2) {
+            iteration(j, std::integral_constant<int, 0>{}, RL);
+            if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{}, RL);
+        }
+    };
+    if (g < RGP)
+        run(std::integral_constant<int, 0>{});
+    else if (g == RGP)
+        run(std::integral_constant<int, 1>{});
+    else if (g == RGP + 1)
+        run(std::integral_constant<int, 2>{});
+    else if (SPL && g == RGP + 2)
+        run(std::integral_constant<int, 3>{});
+    else
+        run(std::integral_constant<int, 4>{});
 #undef LCLK
     // the last iteration's post outputs (each iteration ends with a barrier)
     if (store_w) flush((nloop + 2 + SPL) & 1);

@@ -215,6 +215,11 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const unsigned nw = gridDim.x * 4u;
     const unsigned per = (nfr + nw - 1) / nw;
     if (blockIdx.x * 4u * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
+    // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
+    // the start, after the tables, at the end, and the frames it ran
+    const unsigned wid0 = blockIdx.x * 4u + (threadIdx.x >> 6);
+    long long* wclk = (a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
+    if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
     fe_tables_init(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -229,6 +234,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const unsigned wid = blockIdx.x * 4u + (unsigned)wv;
     const unsigned fbeg = wid * per;
     const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
+    if (wclk) wclk[1] = (long long)__builtin_amdgcn_s_memrealtime();
     // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
     // T); walked incrementally (no per-frame division)
     // t >= lim: nothing to do (past the chunk; COLD: past the segment or not
@@ -272,7 +278,10 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             r[0] = *reinterpret_cast<const uint32_t*>(q);
             r[1] = *reinterpret_cast<const uint32_t*>(q + 128);
             r[2] = *reinterpret_cast<const uint32_t*>(q + 256);
-            r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(q + 384) : 0u;
+            // lanes 48..63 (taps 480..511, window coefficient 0) load a
+            // dummy in-frame word: a select of the value, not of the address,
+            // was a register write behind the frame's pending stores
+            r[3] = *reinterpret_cast<const uint32_t*>(q + (lane < 48 ? 384 : 0));
             return;
         }
         const int16_t* p0 = frame_ptr(p, p.t - 2);
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         r[0] = *reinterpret_cast<const uint32_t*>(p0 + o);
         r[1] = *reinterpret_cast<const uint32_t*>(lane < 16 ? p0 + 128 + o : p1 + o - 32);
         r[2] = *reinterpret_cast<const uint32_t*>(lane < 32 ? p1 + 96 + o : p2 + o - 64);
-        r[3] = lane < 48 ? *reinterpret_cast<const uint32_t*>(p2 + 64 + o) : 0u;
+        r[3] = *reinterpret_cast<const uint32_t*>(lane < 48 ? p2 + 64 + o : p2 + o - 96);
     };
     if (fbeg >= fend) return;
     const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
@@ -290,20 +299,45 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     nx.k = fbeg - nx.i * W;
     row_of(nx);
     nx.t = nx.b + (int)nx.k;
-    uint32_t nxt[4] = {0u, 0u, 0u, 0u};
-    if (nx.t < nx.lim) load_frame(nx, nxt);
+    uint32_t raw[4] = {0u, 0u, 0u, 0u};
+    if (nx.t < nx.lim) load_frame(nx, raw);
+    // The frame's features are stored one frame late, after the next frame's
+    // window multiply, and the next window's loads are issued only after that
+    // multiply (into the same registers).  On gfx9 vmcnt counts stores as well
+    // as loads, and the wait for the window samples cannot count past the
+    // frame's conditional stores and loads: issued at the end of a frame, the
+    // stores were waited for at the next frame's window (and, with the
+    // prefetch issued before the multiply, the prefetch too).  Now everything
+    // outstanding at that wait was issued a frame earlier.
+    bool pend = false;
+    unsigned po = 0;          // output row (shared: ring row s * ring + slot; batch: frame fo)
+    uint32_t pv01 = 0u;       // features of nets 0 and 1 (batch: the one feature), int16 pair
+    int32_t pv2 = 0;          // shared: net 2's feature
+    auto flush = [&]() {
+        if (pend && lane < 40) {
+            if constexpr (shared) {
+                const unsigned o = po * 40u + (unsigned)lane;   // < 2^31 (host)
+                a.nring[0][o] = (int16_t)(pv01 & 0xffff);
+                a.nring[1][o] = (int16_t)(pv01 >> 16);
+                a.nring[2][o] = (int16_t)pv2;
+            } else {
+                a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
+            }
+        }
+    };
     long long* fclk = (a.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? a.dbg_clk + 1024 : nullptr;
 #define FCLK(k) \
     if (fclk && f - fbeg < 64u) fclk[8 * (f - fbeg) + (k)] = (long long)__builtin_amdgcn_s_memtime()
     for (unsigned f = fbeg; f < fend; ++f) {
         FCLK(0);
         const Pos cur = nx;
-        const uint32_t raw[4] = {nxt[0], nxt[1], nxt[2], nxt[3]};
-        if (f + 1 < fend) {   // prefetch the next frame's window
-            advance(nx);
-            if (nx.t < nx.lim) load_frame(nx, nxt);
+        if (cur.t >= cur.lim) {   // wave-uniform: nothing to compute, only the next prefetch
+            if (f + 1 < fend) {
+                advance(nx);
+                if (nx.t < nx.lim) load_frame(nx, raw);
+            }
+            continue;
         }
-        if (cur.t >= cur.lim) continue;   // wave-uniform
         const int s = cur.s, t = cur.t;
         if (a.hist_out && t >= a.T - a.hist_frames) {
             // frame t's own 160 samples: raw[2] of lanes 32..63 (samples 0..63),
@@ -325,6 +359,18 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 v[2 * m + 1] = (int32_t)(int16_t)(wn[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
             }
         }
+        // pin the products here: sunk past the prefetch (next to their use)
+        // they kept the old samples live beside the new ones, and the copy
+        // between the two at the loop latch waited for the loads again
+        asm volatile("" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+        if (f + 1 < fend) {   // prefetch the next frame's window (raw is free now)
+            advance(nx);
+            if (nx.t < nx.lim) load_frame(nx, raw);
+        }
+        // the previous frame's features, after the loads: a wait the compiler
+        // puts into the prefetch code (path merges) must not cover them
+        flush();
+        pend = false;
         FCLK(1);
         wave_cfft256(v, X, TB, lane);
         FCLK(2);
@@ -388,22 +434,32 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 // (abs0 + t) % ring with t < T <= ring: one conditional subtract
                 unsigned slot = ring0 + (unsigned)t;
                 if (slot >= (unsigned)a.ring) slot -= (unsigned)a.ring;
-                const unsigned o = ((unsigned)s * (unsigned)a.ring + slot) * 40u + (unsigned)lane;   // < 2^31 (host)
+                po = (unsigned)s * (unsigned)a.ring + slot;
                 // keep the (mean, stdR) LDS reads here: hoisted out of the frame
                 // loop they would pin 6 VGPRs and cost a wave per SIMD
                 __asm__ volatile("" ::: "memory");
+                int16_t nv[3];
 #pragma unroll
                 for (int n = 0; n < 3; ++n) {   // each net's normalisation (feature_module.c:67-73)
                     const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
-                    a.nring[n][o] = sat16(mad_i64_i32(wsub(lg, mn), sr, 0) >> a.nshift[n]);
+                    nv[n] = sat16(mad_i64_i32(wsub(lg, mn), sr, 0) >> a.nshift[n]);
                 }
+                pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
+                pv2 = nv[2];
             } else {
                 const int64_t d = (int64_t)lg - mean;
-                a.feats[(size_t)fo * 40 + lane] = sat16((d * stdR) >> a.norm_shift);
+                po = fo;
+                pv01 = (uint32_t)(uint16_t)sat16((d * stdR) >> a.norm_shift);
             }
         }
+        pend = true;
         wave_lds_sync();
         FCLK(5);
+    }
+    flush();
+    if (wclk) {
+        wclk[2] = (long long)__builtin_amdgcn_s_memrealtime();
+        wclk[3] = (long long)(fend - fbeg);
     }
 #undef FCLK
 }
