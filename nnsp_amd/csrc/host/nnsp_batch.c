@@ -138,8 +138,9 @@ static void plan_fast(nnsp_batch *b)
 }
 
 /* NNSP_RECUR_CLOCKS probe buffer: 2048 longs of phase clocks, then
- * fe_kernel's per-wave records (4 longs per wave, 32768 waves) */
-#define DCLK_LONGS (2048 + 4 * 32768)
+ * fe_kernel's per-wave records (4 longs per wave, 32768 waves), then
+ * proj_kernel's (8192 waves) */
+#define DCLK_LONGS (2048 + 4 * 32768 + 4 * 8192)
 
 #define TRY(x)                 \
     do {                       \

@@ -257,8 +257,11 @@ struct alignas(16) ProjWave {
     int16_t act[NA][16][AS];
 };
 
+// 16 zero bytes: the source of union elements outside a segment (proj_kernel)
+__device__ __attribute__((aligned(16))) int4 nnsp_proj_zero16;
+
 template <class SH, bool ACC32>
-__global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
+__global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) {   // <= 128 VGPRs: 4 waves per SIMD
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
@@ -291,34 +294,56 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
     // device-sized lists (cascade rounds): workgroups with no tile exit
     // before staging anything
     if ((long long)blockIdx.x * (blockDim.x >> 6) >= ntiles) return;
+    // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
+    // the start, after staging, at the end, and the tiles it ran
+    const unsigned pwid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    long long* pwc = (r.dbg_clk && lane == 0 && pwid < 8192u) ? r.dbg_clk + 2048 + 4 * 32768 + 4 * pwid : nullptr;
+    if (pwc) pwc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, false);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
     __syncthreads();
+    if (pwc) pwc[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    int ntile_run = 0;
     // stream k of a tile: list entry, segment start b, length L, NN phase
     struct Seg { int s, b, L, ph; bool ok; };
-    auto seg_of = [&](long long grp, int k) {
-        Seg g;
-        const long long i = grp * G + k;
-        g.ok = i < nrow;
-        g.s = g.ok ? (r.list ? r.list[i] : (int)i) : 0;
-        g.b = g.ok && r.seg_begin ? r.seg_begin[g.s] : 0;
-        g.L = g.ok ? (r.seg_len > 0 ? min(r.T, g.b + r.seg_len) : r.T) - g.b : 0;
-        g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
-        return g;
-    };
     // development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0's first tiles
     long long* clk = (r.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? r.dbg_clk + 12 : nullptr;
     int it = 0;
 #define PCLK(k) \
     if (clk && it < 64) clk[it * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime()
-    for (long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv; tile < ntiles;
-         tile += (long long)gridDim.x * (blockDim.x >> 6), ++it) {
+    // The tiles run as a software pipeline over their descriptors.  A tile's
+    // inputs are a chain of dependent loads (list entry -> segment start and
+    // phase -> the context features): one tile at a time exposed three HBM
+    // latencies per tile (~4.5 us per tile and wave).  The list entries are
+    // loaded two tiles ahead and the segment descriptors one tile ahead, so a
+    // tile waits only for its features.  (Prefetching the features as well
+    // took 16 more VGPRs per lane held across the FC layer: past 128, spills.)
+    const long long tstride = (long long)gridDim.x * (blockDim.x >> 6);
+    auto j0_of = [&](long long t) { return 16 * (int)(t - (t / ntps) * ntps); };
+    // lanes 0..G-1: the tile's stream k = lane (the others read by shuffle); -1: none
+    auto list_at = [&](long long t) {
+        const long long i = (t / ntps) * G + (lane < G ? lane : 0);
+        return i < nrow ? (r.list ? r.list[i] : (int)i) : -1;
+    };
+    auto seg_from = [&](int st) {
+        Seg g;
+        g.ok = st >= 0;
+        g.s = g.ok ? st : 0;
+        g.b = g.ok && r.seg_begin ? r.seg_begin[g.s] : 0;
+        g.L = g.ok ? (r.seg_len > 0 ? min(r.T, g.b + r.seg_len) : r.T) - g.b : 0;
+        g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
+        return g;
+    };
+    long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+    Seg mine_n = seg_from(list_at(tile));
+    int s_nn = list_at(tile + tstride);
+    for (; tile < ntiles; tile += tstride, ++it) {
         PCLK(0);
-        const long long grp = tile / ntps;
-        const int j0 = 16 * (int)(tile - grp * ntps);
-        // lanes 0..G-1 load the tile's stream descriptors; the others read them by shuffle
-        const Seg mine = seg_of(grp, lane < G ? lane : 0);
+        const Seg mine = mine_n;
+        mine_n = seg_from(s_nn);                     // the next tile's descriptors
+        s_nn = list_at(tile + 2 * tstride);          // the list entries of the one after
+        const int j0 = j0_of(tile);
         auto seg_k = [&](int k) {
             Seg g;
             g.s = __shfl(mine.s, k);
@@ -330,21 +355,46 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
         };
         // wave-uniform: skip a tile none of whose rows has a frame
         if (!__any(lane < G && mine.ok && 2 * j0 + mine.ph < mine.L)) continue;
+        ++ntile_run;
         // ---- union of the context windows: stream k's rows read
-        //      V_k[t0 .. t0 + FR - 1], V = prev5 ++ features[b..b+L), t0 = 2*j0 + phase
-        for (int c = lane; c < G * FR * 5; c += 64) {
-            const int k = c / (FR * 5), rem = c - k * FR * 5, fr = rem / 5, part = rem - 5 * fr;
-            const Seg g = seg_k(k);
-            const int idx = 2 * j0 + g.ph + fr;
-            int4 v = make_int4(0, 0, 0, 0);
-            if (g.ok) {
-                if (idx < 5)
-                    v = *reinterpret_cast<const int4*>(r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part);
-                else if (idx - 5 < g.L)
-                    v = feat8(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+        //      V_k[t0 .. t0 + FR - 1], V = prev5 ++ features[b..b+L), t0 = 2*j0 + phase.
+        //      Loaded straight into LDS (global_load_lds: element c = lane + 64 m
+        //      lands at uni + 16 c, lane-linear), no VGPRs, all in flight at once;
+        //      elements outside a segment read a zero row.
+        const Seg g1 = {__builtin_amdgcn_readfirstlane(mine.s), __builtin_amdgcn_readfirstlane(mine.b),
+                        __builtin_amdgcn_readfirstlane(mine.L), __builtin_amdgcn_readfirstlane(mine.ph),
+                        __builtin_amdgcn_readfirstlane((int)mine.ok) != 0};
+        auto union_g = [&](auto GC) {
+            constexpr int GG = decltype(GC)::value, FRG = 2 * (16 / GG) + 4, NU = GG * FRG * 5;
+#pragma unroll
+            for (int m = 0; m < (NU + 63) / 64; ++m) {
+                // opaque per tile: hoisted out of the tile loop, the per-lane
+                // element indices of the three G variants pinned ~70 VGPRs
+                int c = lane + 64 * m;
+                asm volatile("" : "+v"(c));
+                if (m < NU / 64 || c < NU) {
+                    const int k = c / (FRG * 5), rem = c - k * (FRG * 5), fr = rem / 5, part = rem - 5 * fr;
+                    const Seg g = GG == 1 ? g1 : seg_k(k);   // one stream per tile: scalar
+                    const int idx = 2 * j0 + g.ph + fr;
+                    const int16_t* src = reinterpret_cast<const int16_t*>(&nnsp_proj_zero16);
+                    if (g.ok) {
+                        if (idx < 5)
+                            src = r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part;
+                        else if (idx - 5 < g.L)
+                            src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+                    }
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                     (__attribute__((address_space(3))) void*)&P.uni[512 * m], 16, 0, 0);
+                }
             }
-            *reinterpret_cast<int4*>(&P.uni[8 * c]) = v;
-        }
+        };
+        if (G == 1)
+            union_g(std::integral_constant<int, 1>{});
+        else if (G == 2)
+            union_g(std::integral_constant<int, 2>{});
+        else
+            union_g(std::integral_constant<int, 4>{});
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the LDS-DMA writes landed
         wave_lds_sync();
         PCLK(1);
         // this lane's row sc: stream kr of the tile, its step j0 + jr
@@ -385,9 +435,7 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
                 in = out;
                 in_stride = PW::AS;
             }
-        }
-        // ---- LSTM input half (generic shape): gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
-        if constexpr (GEN) {
+            // ---- LSTM input half (generic shape): gx = sum_k Wx[row][k] x[k] (exact, before shift_64b)
             v4i bh[2], bl[2];
             load_b<2>(in, in_stride, nkt, lane, bh, bl);
             const uint8_t* A = W + (LL.a_off - r.a_off);
@@ -395,7 +443,7 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
             const int j = j0 + jr;
             const bool act = me.ok && j < r.nstep_max && 2 * j + me.ph < me.L;
             int32_t* dst = r.gx + ((size_t)me.s * r.nstep_max + j) * rows + 4 * q;
-            auto tile = [&](int rt) {
+            for (int rt = 0; rt < nrt; ++rt) {
                 v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
                 for (int kt = 0; kt < 2; ++kt)
@@ -411,18 +459,16 @@ __global__ __launch_bounds__(512) void proj_kernel(NnImage img, FastRun r) {
                 o.z = (ah[2] << 8) + al[2] + (int32_t)er[2].cst;
                 o.w = (ah[3] << 8) + al[3] + (int32_t)er[3].cst;
                 if (act) *reinterpret_cast<int4*>(dst + 16 * rt) = o;
-            };
-            if constexpr (!GEN) {
-#pragma unroll
-                for (int rt = 0; rt < SH::NRT; ++rt) tile(rt);
-            } else {
-                for (int rt = 0; rt < nrt; ++rt) tile(rt);
             }
+            wave_lds_sync();
+            PCLK(3);
         }
-        wave_lds_sync();
-        PCLK(3);
     }
 #undef PCLK
+    if (pwc) {
+        pwc[2] = (long long)__builtin_amdgcn_s_memrealtime();
+        pwc[3] = ntile_run;
+    }
 }
 
 // ---------------------------------------------------------------------------

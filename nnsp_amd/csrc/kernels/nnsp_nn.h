@@ -74,16 +74,25 @@ __device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) 
 // through another branch's base -- out of bounds, a memory fault in
 // recur_pipe_kernel.  With the select the base is a VGPR per lane.
 // fs.nring is wave-uniform.
-__device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
-                                      int part) {
-    if (!fs.nring) return *reinterpret_cast<const int4*>(feats + ((size_t)s * T + t) * 40 + 8 * part);
+__device__ __forceinline__ const int16_t* feat8_ptr(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
+                                                  int part) {
+    if (!fs.nring) return feats + ((size_t)s * T + t) * 40 + 8 * part;
     // only the first two frames of a segment can be cold: the fresh[] load
     // (and the dependent-load latency) only for those
     const bool cold = t - b < 2 && t - b + fs.fresh[s] < 2;
-    const unsigned slot = (unsigned)(fs.abs0 + t - fs.lookback + fs.ring) % (unsigned)fs.ring;
+    // (abs0 + t - lookback) mod ring with 0 <= abs0 < ring, 0 <= t < Tmax <=
+    // ring and lookback < ring (host): the sum plus ring is in [1, 3 ring),
+    // two conditional subtracts instead of a 32-bit division (~30 VALU)
+    const unsigned rg = (unsigned)fs.ring;
+    unsigned slot = (unsigned)(fs.abs0 + t - fs.lookback) + rg;
+    slot = slot >= rg ? slot - rg : slot;
+    slot = slot >= rg ? slot - rg : slot;
     const size_t row = cold ? (size_t)s * T + t : (size_t)s * fs.ring + slot;
     const uintptr_t base = cold ? (uintptr_t)feats : (uintptr_t)fs.nring;
-    return *reinterpret_cast<const int4*>(base + (row * 40 + 8 * part) * sizeof(int16_t));
+    return reinterpret_cast<const int16_t*>(base + (row * 40 + 8 * part) * sizeof(int16_t));
+}
+__device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t, int part) {
+    return *reinterpret_cast<const int4*>(feat8_ptr(fs, feats, s, T, b, t, part));
 }
 
 // Preload the B fragments (hi, lo) of nkt k-tiles of a [16][stride] int16 buffer.
