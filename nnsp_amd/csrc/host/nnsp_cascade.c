@@ -85,6 +85,7 @@ struct nnsp_cascade {
     int part;                       /* CUs of the front end's partition (0: off) */
     void *fe_stream;                /* look-ahead front end, CU-masked */
     void *own_ns[3];                /* the nets' CU-masked streams */
+    int netpart;                    /* experiment NNSP_NET_CUS: own_ns for every chunk */
     void *ev_fe_dep;                /* fe_stream waits for the cascade's stream there */
     int ahead_on_fe;                /* the last look-ahead ran on fe_stream */
     void *ev[2];
@@ -204,6 +205,19 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             if ((e = nnspk_event_create(&c->ev_fe_dep))) goto fail;
         } else {
             c->part = 0;
+        }
+        /* experiment (off unless NNSP_NET_CUS="lo:hi,lo:hi,lo:hi", nets in id
+         * order s2i, vad, kws; CU index space XCD-major, 32 per XCD): every
+         * round of each net on its own CUs (the front end stays unmasked) */
+        const char *nc = getenv("NNSP_NET_CUS");
+        c->netpart = 0;
+        if (!c->part && nc && cus > 0) {
+            int lo[3], hi[3];
+            if (sscanf(nc, "%d:%d,%d:%d,%d:%d", &lo[0], &hi[0], &lo[1], &hi[1], &lo[2], &hi[2]) == 6) {
+                for (int n = 0; n < 3; ++n)
+                    if ((e = nnspk_stream_create_cupart(&c->own_ns[n], lo[n], hi[n], 1))) goto fail;
+                c->netpart = 1;
+            }
         }
     }
     for (int i = 0; i < 2; ++i)
@@ -713,7 +727,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
      * partition it runs on fe_stream's CUs and the nets on theirs. */
     const int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
     const int part = ahead && c->part > 0;
-    for (int n = 0; n < 3; ++n) c->ns[n] = part ? c->own_ns[n] : c->net[n]->stream;
+    for (int n = 0; n < 3; ++n) c->ns[n] = part || c->netpart ? c->own_ns[n] : c->net[n]->stream;
     /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
