@@ -140,6 +140,29 @@ def mel_segments(max_len: int = 12, lanes: int = 64) -> np.ndarray:
     return np.asarray(segs, dtype=np.int32)
 
 
+def _cplx16_words(th: np.ndarray) -> np.ndarray:
+    """exp(-j th) as the portable build's COMPLEX16 words (imag << 16 | real):
+    real = min(floor(2^15 cos), 2^15 - 1), imag = floor(-2^15 sin) (matches
+    twiddle_fft_dif.c word for word, tests/test_tables.py)."""
+    re_ = np.minimum(np.floor(32768.0 * np.cos(th)), 32767).astype(np.int64)
+    im = np.floor(-32768.0 * np.sin(th)).astype(np.int64)
+    w = ((im & 0xFFFF) << 16) | (re_ & 0xFFFF)
+    return np.where(w >= 2 ** 31, w - 2 ** 32, w).astype(np.int32)
+
+
+def dif_twiddles() -> np.ndarray:
+    """fft_tw_coeff (twiddle_fft_dif.c, ARM_OPTIMIZED=0): per radix-4 index k
+    in 0..63 the four twiddles [W^0, W^2k, W^k, W^3k] of the DIF butterfly's
+    output slots, W = exp(-j 2 pi / 256)."""
+    k = np.arange(64)
+    return _cplx16_words(np.stack([0 * k, 2 * k, k, 3 * k], 1).reshape(-1) * 2 * np.pi / 256)
+
+
+def rfft_dif_twiddles() -> np.ndarray:
+    """rfft_tw_coeff (twiddle_fft_dif.c): exp(-j 2 pi i / 512), i in 0..255."""
+    return _cplx16_words(np.arange(256) * 2 * np.pi / 512)
+
+
 def bitrev8() -> np.ndarray:
     return np.array([int(f"{i:08b}"[::-1], 2) for i in range(256)], dtype=np.int32)
 
@@ -168,6 +191,8 @@ def header_text() -> str:
         _c_array("int32_t", "nnsp_tbl_tw256", cfft256_twiddles(), 6),
         _c_array("int32_t", "nnsp_tbl_split", rfft512_split_coefs(), 6),
         _c_array("int32_t", "nnsp_tbl_melseg", mel_segments(), 4),
+        _c_array("int32_t", "nnsp_tbl_dif_tw", dif_twiddles(), 8),
+        _c_array("int32_t", "nnsp_tbl_dif_rtw", rfft_dif_twiddles(), 8),
         "#endif\n",
     ]
     return "\n".join(parts)
@@ -189,6 +214,10 @@ def export_text() -> str:
         arr("const int16_t", "mfltrBank_coeff", mel),
         arr("const int16_t", "log_tayler_coeff", log_interp()),
         arr("int16_t", "coeffs_tanh", tanh_interp()),
+        # the ARM_OPTIMIZED=0 build's FFT tables (twiddle_fft_dif.c:8-77)
+        arr("const int32_t", "fft_tw_coeff", dif_twiddles()),
+        arr("const int32_t", "rfft_tw_coeff", rfft_dif_twiddles()),
+        arr("const int16_t", "br_coeff", bitrev8()),
     ])
 
 

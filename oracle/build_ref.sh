@@ -25,6 +25,10 @@
 #                              loop (affine.c:186-253 vs :311-339); it walks the
 #                              weights in the portable order and applies the
 #                              align shift that is dead in the shipped build (T1).
+#  libnnsp_ref_fe_portable.so  the reference's portable front end
+#                              (ARM_OPTIMIZED=0: fft.c, complex.c,
+#                              twiddle_fft_dif.c, spectrogram_module.c,
+#                              feature_module.c, mel, log10, window), row N4.
 #  libnnsp_ref_nets.so         evb/src/def_nn{0_s2i,1_vad,2_kws_galaxy}.c (the
 #                              reference's three nets as data) against the
 #                              reference headers, linked with the portable NN
@@ -52,6 +56,15 @@ gcc -O2 -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NNSP_DEBUG=0 -DA
 gcc -O2 -fPIC -shared -w -I"$API" \
     "$REF/evb/src/def_nn0_s2i.c" "$REF/evb/src/def_nn1_vad.c" "$REF/evb/src/def_nn2_kws_galaxy.c" \
     -L"$OUT" -lnnsp_ref_nn_portable -Wl,-rpath,'$ORIGIN' -Wl,-z,defs -o "$OUT/libnnsp_ref_nets.so"
+
+# the reference's own portable front end (ARM_OPTIMIZED=0, row N4): fft.c's
+# radix-4 DIF FFT and rfft split, complex.c, twiddle_fft_dif.c, and the
+# FeatureClass / stftModule / Mel / log10 files built with the same switches
+gcc -O2 -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NNSP_DEBUG=0 -DARM_OPTIMIZED=0 \
+    -I"$API" -I"$CORE" \
+    "$SRC/fft.c" "$SRC/complex.c" "$SRC/twiddle_fft_dif.c" "$SRC/spectrogram_module.c" "$SRC/feature_module.c" \
+    "$SRC/melSpecProc.c" "$SRC/melSpec_coeff.c" "$SRC/fixlog10.c" "$SRC/window_stft_coef.c" \
+    -Wl,-z,defs -o "$OUT/libnnsp_ref_fe_portable.so"
 
 # the reference timed beside the oracle on the same cores (container
 # calibration, BASELINE.md / SURVEY 8(d)): -O3 -march=native like the oracle

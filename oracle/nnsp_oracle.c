@@ -170,6 +170,98 @@ void or_rfft512(int32_t *x, int32_t *y)
 }
 
 /* ------------------------------------------------------------------------
+ * The ARM_OPTIMIZED=0 build's FFT (row N4): fft.c:27-221 (rfft, fft) with
+ * complex.c's complex32_affine / complex32_complex16_elmtprod / complex32_add
+ * and twiddle_fft_dif.c's tables (COMPLEX16 words: real low, imag high).
+ * 64-bit sums saturated to int32 where complex.c saturates; int32 adds wrap
+ * (-fwrapv) where the reference adds plain ints.
+ * ---------------------------------------------------------------------- */
+static inline i32 tw_re(int32_t w) { return (i32)(int16_t)(w & 0xffff); }
+static inline i32 tw_im(int32_t w) { return (i32)(int16_t)((u32)w >> 16); }
+
+/* complex32_complex16_elmtprod (complex.c:54-72): (a * w) >> 15, saturated */
+static void cmul15(i32 *re, i32 *im, int32_t w)
+{
+    const i64 r = (i64)*re * tw_re(w) - (i64)*im * tw_im(w);
+    const i64 i = (i64)*re * tw_im(w) + (i64)*im * tw_re(w);
+    *re = sat32(r >> 15);
+    *im = sat32(i >> 15);
+}
+
+/* fft.c:12-15: the radix-4 matrix M4 as (real, imag) pairs, row-major */
+static const int8_t M4[4][4][2] = {{{1, 0}, {1, 0}, {1, 0}, {1, 0}},
+                                   {{1, 0}, {1, 0}, {-1, 0}, {-1, 0}},
+                                   {{1, 0}, {-1, 0}, {0, -1}, {0, 1}},
+                                   {{1, 0}, {-1, 0}, {0, 1}, {0, -1}}};
+
+/* fft(8, ...): 256-pt radix-4 DIF in place on p (interleaved), then the
+ * 8-bit bit reversal into out (fft.c:128-221) */
+static void dif_fft256(i32 *p, i32 *out)
+{
+    int Nf = 256, Ng = 1, S = 1;
+    for (int s = 0; s < 4; ++s) {
+        const int Nfd4 = Nf >> 2;
+        for (int g = 0; g < Ng; ++g) {
+            int k = 0;
+            for (int m = 0; m < Nfd4; ++m) {
+                const int idx = g * Nf + m;
+                /* ti = (x0, x2, x1, x3): slots idx, idx + 2 Nf/4, idx + Nf/4, idx + 3 Nf/4 */
+                const int src[4] = {idx, idx + 2 * Nfd4, idx + Nfd4, idx + 3 * Nfd4};
+                i32 tr[4], ti[4];
+                for (int r = 0; r < 4; ++r) { /* complex32_affine, shift 0 (complex.c:14-53) */
+                    i64 re = 0, im = 0;
+                    for (int c = 0; c < 4; ++c) {
+                        const i64 ar = p[2 * src[c]], ai = p[2 * src[c] + 1];
+                        re += ar * M4[r][c][0] - ai * M4[r][c][1];
+                        im += ar * M4[r][c][1] + ai * M4[r][c][0];
+                    }
+                    tr[r] = sat32(re);
+                    ti[r] = sat32(im);
+                }
+                for (int r = 0; r < 4; ++r) cmul15(&tr[r], &ti[r], nnsp_tbl_dif_tw[4 * k + r]);
+                k += S;
+                for (int r = 0; r < 4; ++r) { /* written back to idx + r Nf/4 */
+                    p[2 * (idx + r * Nfd4)] = tr[r];
+                    p[2 * (idx + r * Nfd4) + 1] = ti[r];
+                }
+            }
+        }
+        Nf >>= 2;
+        Ng <<= 2;
+        S <<= 2;
+    }
+    for (int m = 0; m < 256; ++m) {
+        out[2 * m] = p[2 * rev8(m)];
+        out[2 * m + 1] = p[2 * rev8(m) + 1];
+    }
+}
+
+/* rfft(512, x, y) (fft.c:27-126): x 512 int32 (Frac15), y 257 complex */
+void or_rfft512_portable(const int32_t *x, int32_t *y)
+{
+    i32 cin[512], Z[512], Xe[512];
+    memcpy(cin, x, sizeof cin);
+    dif_fft256(cin, Z);
+    i32 *Xo = cin; /* fft.c:25: Xo aliases the (now free) FFT input */
+    for (int i = 0; i < 256; ++i) {
+        const int j = (256 - i) & 255; /* i = 0: the reference's special case is this formula with j = 0 */
+        const i32 tr = Z[2 * j], tim = sub(0, Z[2 * j + 1]); /* tmp = conj(Z(idx)) */
+        Xe[2 * i] = add(Z[2 * i], tr) >> 1;
+        Xe[2 * i + 1] = add(Z[2 * i + 1], tim) >> 1;
+        Xo[2 * i] = sub(Z[2 * i + 1], tim) >> 1;
+        Xo[2 * i + 1] = sub(0, sub(Z[2 * i], tr)) >> 1;
+    }
+    for (int i = 0; i < 256; ++i) {
+        i32 re = Xo[2 * i], im = Xo[2 * i + 1];
+        cmul15(&re, &im, nnsp_tbl_dif_rtw[i]);
+        y[2 * i] = add(re, Xe[2 * i]); /* complexArry32_add */
+        y[2 * i + 1] = add(im, Xe[2 * i + 1]);
+    }
+    y[512] = sub(Xe[0], Xo[0]);
+    y[513] = sub(Xe[1], Xo[1]);
+}
+
+/* ------------------------------------------------------------------------
  * Front end (ns-nnsp/src/feature_module.c, spectrogram_module.c,
  * melSpecProc.c, fixlog10.c)
  * ---------------------------------------------------------------------- */
@@ -228,10 +320,18 @@ void or_fe_exec(or_stream *st, const or_cfg *cfg, const int16_t *pcm) /* feature
     memmove(st->ctx, st->ctx + 40, 200 * sizeof(i16));
     memmove(st->buf, st->buf + 160, 320 * sizeof(i16)); /* spectrogram_module.c:103-108 */
     memcpy(st->buf + 320, pcm, 160 * sizeof(i16));
-    for (int i = 0; i < 480; ++i) x[i] = (i32)nnsp_tbl_window[i] * st->buf[i]; /* Q30 */
-    for (int i = 480; i < 514; ++i) x[i] = 0;
-    or_rfft512(x, spec);
-    or_spec2pspec(spec, spec, 257);
+    if (cfg->fe_portable) { /* ARM_OPTIMIZED=0: spectrogram_module.c:47-77, feature_module.c:58-60 */
+        for (int i = 0; i < 480; ++i) x[i] = ((i32)nnsp_tbl_window[i] * st->buf[i]) >> 15; /* Frac15 */
+        for (int i = 480; i < 514; ++i) x[i] = 0;
+        or_rfft512_portable(x, spec);
+        for (int i = 0; i < 257; ++i) /* spec2pspec (spectrogram_module.c:33-45) */
+            spec[i] = (i32)(((i64)spec[2 * i] * spec[2 * i] + (i64)spec[2 * i + 1] * spec[2 * i + 1]) >> 15);
+    } else {
+        for (int i = 0; i < 480; ++i) x[i] = (i32)nnsp_tbl_window[i] * st->buf[i]; /* Q30 */
+        for (int i = 480; i < 514; ++i) x[i] = 0;
+        or_rfft512(x, spec);
+        or_spec2pspec(spec, spec, 257);
+    }
     or_mel(spec, mel);
     for (int i = 0; i < 40; ++i) {
         const i64 d = (i64)or_log10(mel[i]) - cfg->mean[i];

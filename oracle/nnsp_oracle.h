@@ -76,10 +76,12 @@ typedef struct {
     int32_t qbit_out; /* FeatureClass.qbit_output = net qbit_input[0] */
     const int32_t *mean;
     const int32_t *stdR;
+    int32_t fe_portable; /* 1: the ARM_OPTIMIZED=0 build's FFT front end (row N4) */
 } or_cfg;
 
 /* front end stages */
 void or_rfft512(int32_t *x, int32_t *y); /* x: 512 q31 (clobbered); y: 1024 q31 */
+void or_rfft512_portable(const int32_t *x, int32_t *y); /* ARM_OPTIMIZED=0 rfft: x 512 Frac15; y 257 complex */
 void or_spec2pspec(int32_t *y, const int32_t *x, int n);
 void or_mel(const int32_t *pspec, int32_t *mel);
 int32_t or_log10(int32_t x);

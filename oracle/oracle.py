@@ -29,7 +29,8 @@ class or_net(C.Structure):
 
 class or_cfg(C.Structure):
     _fields_ = [("nn_id", C.c_int32), ("thresh_prob", C.c_int32), ("th_count", C.c_int32),
-                ("qbit_out", C.c_int32), ("mean", C.c_void_p), ("stdR", C.c_void_p)]
+                ("qbit_out", C.c_int32), ("mean", C.c_void_p), ("stdR", C.c_void_p),
+                ("fe_portable", C.c_int32)]
 
 
 class or_cascade_cfg(C.Structure):
@@ -68,7 +69,7 @@ class OracleNet:
     """or_net + or_cfg built from nnsp_amd.nets.NetData (packed byte layout)."""
 
     def __init__(self, data, acc32: bool = False, thresh_prob: int = 32767 >> 1, th_count: int = 4,
-                 portable: bool = False):
+                 portable: bool = False, fe_portable: bool = False):
         spec = data.spec
         Wp, Wrp, Bp = data.packed()
         self.keep = []
@@ -101,6 +102,7 @@ class OracleNet:
         c.qbit_out = spec.qi[0]
         c.mean = self.mean.ctypes.data
         c.stdR = self.stdR.ctypes.data
+        c.fe_portable = int(fe_portable)   # the ARM_OPTIMIZED=0 build's front end (row N4)
         self.cfg = c
         self.nout = spec.nout
 
@@ -206,6 +208,14 @@ def rfft512(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     y = np.zeros(1024, np.int32)
     lib().or_rfft512(p(xi), p(y))
     return y, xi[:512]
+
+
+def rfft512_portable(x: np.ndarray) -> np.ndarray:
+    """The ARM_OPTIMIZED=0 build's rfft(512): 512 Frac15 int32 -> 257 complex (514 int32)."""
+    xi = np.ascontiguousarray(x, np.int32)
+    y = np.zeros(514, np.int32)
+    lib().or_rfft512_portable(p(xi), p(y))
+    return y
 
 
 def synthetic_pcm(S: int, T: int, seed: int = 0x4E4E5350, t0: int = 0, s0: int = 0,

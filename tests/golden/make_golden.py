@@ -23,6 +23,10 @@ reference tree).
                    consecutive calls (LSTM state carried) on the three reference
                    nets and on the N3 shapes of nnsp_amd.nets.GEN_SPECS
 
+  ref_fe_portable.npz  the reference's ARM_OPTIMIZED=0 front end (row N4,
+                   oracle/_ref/libnnsp_ref_fe_portable.so): rfft(512) and
+                   FeatureClass_execute over consecutive frames
+
   test_wavs.npz    python/test_wavs/{speech,galaxy,galaxy_s2i}.wav samples
                    (16 kHz mono int16, 160000 each): the reference's own test
                    inputs, replayed by every 4th synthetic stream
@@ -43,6 +47,7 @@ sys.path.insert(0, ROOT)
 REF_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_partial.so")
 REF_NN_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nn_portable.so")
 REF_NETS_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nets.so")
+REF_FE_PORT_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_fe_portable.so")
 REF_PY = "/root/reference/python"
 
 from nnsp_amd._lib import FeatureClass, NeuralNetClass, NNSPClass  # noqa: E402  (ABI mirrors)
@@ -387,6 +392,54 @@ def nn() -> None:
 WAVS = ("speech", "galaxy", "galaxy_s2i")
 
 
+def fe_portable() -> None:
+    """ref_fe_portable.npz: the reference's ARM_OPTIMIZED=0 front end (row N4,
+    oracle/_ref/libnnsp_ref_fe_portable.so): rfft(512) on Frac15 vectors, and
+    FeatureClass_execute over consecutive frames (stftModule buffer and feature
+    context carried) on the reference's own test wavs and noise."""
+    R = C.CDLL(REF_FE_PORT_SO)
+    rng = np.random.default_rng(0x4E34)
+    out = {}
+    xs = []
+    for amp in (1 << 15, 1 << 14, 1 << 10, 64):
+        for _ in range(8):
+            xs.append(rng.integers(-amp, amp, 512))
+    xs.append(np.full(512, 32767))
+    xs.append(np.full(512, -32768))
+    xs = np.array(xs, np.int32)
+    xs[:, 480:] = 0
+    ys = np.zeros((len(xs), 514), np.int32)
+    for i, x in enumerate(xs):
+        xi = x.copy()
+        y = np.zeros(1024, np.int32)
+        R.rfft(512, P(xi), P(y))
+        ys[i] = y[:514]
+    out["rfft_in"], out["rfft_out"] = xs, ys
+    # FeatureClass_execute (feature_module.c:47-74) on 4 streams x 24 frames
+    wz = np.load(os.path.join(HERE, "test_wavs.npz"))
+    wav = [wz["speech"], wz["galaxy"]]
+    S, T = 4, 24
+    pcm = np.zeros((S, T, 160), np.int16)
+    pcm[0] = wav[0][16000:16000 + T * 160].reshape(T, 160)
+    pcm[1] = wav[1][32000:32000 + T * 160].reshape(T, 160)
+    pcm[2] = rng.integers(-32768, 32768, (T, 160))
+    pcm[3] = rng.integers(-300, 300, (T, 160))
+    means = rng.integers(-120000, -10000, (S, 40)).astype(np.int32)
+    stds = rng.integers(12000, 30000, (S, 40)).astype(np.int32)
+    qb = np.array([8, 10, 6, 8], np.int32)
+    feats = np.zeros((S, T, 40), np.int16)
+    for s in range(S):
+        fc = FeatureClass()
+        R.FeatureClass_construct(C.byref(fc), P(means[s]), P(stds[s]), C.c_int8(int(qb[s])))
+        R.FeatureClass_setDefault(C.byref(fc))
+        for t in range(T):
+            x = np.ascontiguousarray(pcm[s, t])
+            R.FeatureClass_execute(C.byref(fc), P(x))
+            feats[s, t] = np.array(fc.normFeatContext[200:240], np.int16)
+    out["fe_pcm"], out["fe_mean"], out["fe_stdR"], out["fe_qbit"], out["fe_feats"] = pcm, means, stds, qb, feats
+    np.savez_compressed(os.path.join(HERE, "ref_fe_portable.npz"), **out)
+
+
 def wavs() -> None:
     import wave
     out = {}
@@ -401,9 +454,9 @@ def main() -> None:
     for so in (REF_SO, REF_NN_SO, REF_NETS_SO):
         if not os.path.exists(so):
             sys.exit("build oracle/_ref first (oracle/build_ref.sh)")
-    which = sys.argv[1:] or ["stages", "nets", "nn", "wavs"]
+    which = sys.argv[1:] or ["stages", "nets", "nn", "wavs", "fe_portable"]
     for w in which:   # nets before nn: nn re-packs the dumped reference nets
-        {"stages": stages, "nets": nets, "nn": nn, "wavs": wavs}[w]()
+        {"stages": stages, "nets": nets, "nn": nn, "wavs": wavs, "fe_portable": fe_portable}[w]()
     print("wrote", sorted(os.listdir(HERE)))
 
 
