@@ -46,6 +46,20 @@ typedef struct {
 int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
                       const int32_t *mean, const int32_t *stdR, int16_t thresh_prob,
                       int16_t th_count, int n_streams, int max_frames);
+/* The same for either build of the reference (ARM_OPTIMIZED, ambiq_nnsp_debug.h:4;
+ * row N4 of SURVEY.md §8): arm_optimized = 1 is nnsp_batch_create (the shipped
+ * build: CMSIS arm_rfft_q31 front end, interleaved weights, trap T1);
+ * arm_optimized = 0 reproduces the reference compiled with ARM_OPTIMIZED=0:
+ *   - front end: Frac15 window, fft.c's radix-4 DIF rfft, spec2pspec >> 15
+ *     (spectrogram_module.c:33-77, feature_module.c:58-60);
+ *   - net: weights in the portable byte order (affine.c:261-346: per 4-row
+ *     block, per column pair, per row) and the live align shift before the bias
+ *     (affine.c:311-313).  Returns NNSP_EUNSUPPORTED (see nnsp_strerror) for a
+ *     layer whose align shift cannot be reproduced exactly (qbit_bias above
+ *     qbit_input + qbit_kernel, or a sum that the shift could clamp). */
+int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
+                         const int32_t *mean, const int32_t *stdR, int16_t thresh_prob,
+                         int16_t th_count, int n_streams, int max_frames, int arm_optimized);
 void nnsp_batch_destroy(nnsp_batch *b);
 
 /* NNSPClass_reset on the streams with mask[s] != 0 (mask == NULL: all). */

@@ -90,6 +90,7 @@ I = C.c_int
 def _declare(L: C.CDLL) -> None:
     sig = {
         "nnsp_batch_create": (I, [C.POINTER(P), P, I, P, P, C.c_int16, C.c_int16, I, I]),
+        "nnsp_batch_create_ex": (I, [C.POINTER(P), P, I, P, P, C.c_int16, C.c_int16, I, I, I]),
         "nnsp_batch_destroy": (None, [P]),
         "nnsp_batch_reset": (I, [P, P]),
         "nnsp_batch_exec": (I, [P, P, I, P, P, P]),
@@ -191,10 +192,11 @@ class NetHandle:
     """A NeuralNetClass built from nnsp_amd.nets.NetData, holding every buffer
     it points to (packed weights exactly as a def_nn*.c file holds them)."""
 
-    def __init__(self, data, acc32: bool = False):
+    def __init__(self, data, acc32: bool = False, arm_optimized: bool = True):
         from .nets import LSTM, LINEAR
         spec = data.spec
-        Wp, Wrp, Bp = data.packed()
+        # the byte order the reference build reads (ARM_OPTIMIZED 1: interleaved; 0: portable)
+        Wp, Wrp, Bp = data.packed() if arm_optimized else data.packed_portable()
         self.data = data
         self.keep = []
         n = NeuralNetClass()

@@ -163,7 +163,18 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
                       const int32_t *stdR, int16_t thresh_prob, int16_t th_count, int n_streams,
                       int max_frames)
 {
+    return nnsp_batch_create_ex(out, net, nn_id, mean, stdR, thresh_prob, th_count, n_streams, max_frames, 1);
+}
+
+int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id, const int32_t *mean,
+                         const int32_t *stdR, int16_t thresh_prob, int16_t th_count, int n_streams,
+                         int max_frames, int arm_optimized)
+{
     *out = NULL;
+    if (arm_optimized != 0 && arm_optimized != 1) {
+        nnsp_set_error("nnsp_batch_create_ex: arm_optimized must be 0 or 1");
+        return NNSP_EINVAL;
+    }
     if (!net || !mean || !stdR || n_streams <= 0 || max_frames <= 0) {
         nnsp_set_error("nnsp_batch_create: bad argument");
         return NNSP_EINVAL;
@@ -179,12 +190,14 @@ int nnsp_batch_create(nnsp_batch **out, const NeuralNetClass *net, int nn_id, co
     nnsp_layer_desc L[NN_MAX_LAYERS];
     int nl = 0, out_linear = 0;
     TRY(nnsp_describe_net(net, L, &nl, &out_linear));
+    for (int i = 0; i < nl; ++i) L[i].portable = !arm_optimized;
     nnsp_batch *b = (nnsp_batch *)calloc(1, sizeof *b);
     if (!b) return NNSP_ENOMEM;
     *out = b;
     b->S = n_streams;
     b->Tmax = max_frames;
     b->nn_id = nn_id;
+    b->port = !arm_optimized;
     b->out_linear = out_linear;
     b->norm_shift = 30 - net->qbit_input[0]; /* FeatureClass qbit_output, nn_speech.c:40-44 */
     int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count, 0);
@@ -308,6 +321,7 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     fa.hist = seg->hist;
     fa.hist_frames = seg->hist_frames;
     fa.seg_len = seg->seg_len;
+    fa.port = b->port;
     if (timed) TRY(nnspk_event_record(b->ev[0], stream));
     TRY(nnspk_launch_fe(&fa, stream));
     if (timed) TRY(nnspk_event_record(b->ev[1], stream));

@@ -142,6 +142,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             nnsp_set_error("nnsp_cascade_create: three nets of the same stream count required");
             return NNSP_EINVAL;
         }
+        if (nets[i]->port != nets[0]->port) {
+            nnsp_set_error("nnsp_cascade_create: nets of different builds (ARM_OPTIMIZED 1 and 0) share one front end");
+            return NNSP_EINVAL;
+        }
         if (nets[i]->nn_id != i) {
             nnsp_set_error("nnsp_cascade_create: nets[%d] was created with NNSP_ID %d (nets[] is indexed by NNSP_ID: "
                            "0 s2i, 1 vad, 2 kws)", i, nets[i]->nn_id);
@@ -465,6 +469,7 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     fa.abs0 = c->abs0;
     fa.fresh = c->d_fresh;
     fa.mode = FE_MODE_COLD;
+    fa.port = b->port;
     fa.list = c->d_cold_list[r & 1][n];
     fa.n_list_dev = cnt + 3 + n;
     return nnspk_launch_fe(&fa, stream);
@@ -609,6 +614,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     fa.mean = c->net[0]->d_mean; /* unused in FE_MODE_SHARED */
     fa.stdR = c->net[0]->d_stdR;
     fa.mode = FE_MODE_SHARED;
+    fa.port = c->net[0]->port;
     fa.ring = c->ring;
     fa.abs0 = abs0;
     for (int n = 0; n < 3; ++n) {

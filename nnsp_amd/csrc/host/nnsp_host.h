@@ -22,6 +22,9 @@ typedef struct {
     int qk, qb, qi, qir;
     const int8_t *W, *Wr;     /* interleaved byte streams (def_nn*.c layout) */
     const int16_t *B;         /* NULL: no bias */
+    int portable;             /* the ARM_OPTIMIZED=0 build (row N4): W / Wr in the portable byte order
+                                 (per 4-row block, per column pair, per row; affine.c:261-346) and the
+                                 live align shift (affine.c:311-313) */
 } nnsp_layer_desc;
 
 typedef struct {
@@ -47,6 +50,7 @@ int nnsp_act_of(void *(*fn)(void *, int32_t *, int));
 struct nnsp_batch {
     int S, Tmax, nout, out_linear, norm_shift;
     int nn_id;                        /* NNSP_ID given at create (post-processing kind) */
+    int port;                         /* 1: the ARM_OPTIMIZED=0 build (row N4), nnsp_batch_create_ex */
     nnsp_image im;
     void *stream;
     void *ev[3];

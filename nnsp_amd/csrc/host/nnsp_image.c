@@ -121,22 +121,113 @@ static size_t walk_block(const int8_t *w, int R, int K, int8_t *dst, int dst_ld,
     return o;
 }
 
+/* The ARM_OPTIMIZED=0 build's walk of one R-row block (affine.c:261-346):
+ * per column pair, per row, the pair's two bytes; an odd K's last column per
+ * row after the pairs. */
+static size_t walk_block_portable(const int8_t *w, int R, int K, int8_t *dst, int dst_ld, int row0)
+{
+    size_t o = 0;
+    for (int p = 0; p < K / 2; ++p)
+        for (int r = 0; r < R; ++r) {
+            dst[(size_t)(row0 + r) * dst_ld + 2 * p] = w[o++];
+            dst[(size_t)(row0 + r) * dst_ld + 2 * p + 1] = w[o++];
+        }
+    if (K & 1)
+        for (int r = 0; r < R; ++r) dst[(size_t)(row0 + r) * dst_ld + K - 1] = w[o++];
+    return o;
+}
+
+static size_t walk(int portable, const int8_t *w, int R, int K, int8_t *dst, int dst_ld, int row0)
+{
+    return portable ? walk_block_portable(w, R, K, dst, dst_ld, row0) : walk_block(w, R, K, dst, dst_ld, row0);
+}
+
 /* natural [N][K] from an fc_8x16 stream */
-static void unpack_fc(const int8_t *w, int N, int K, int8_t *dst)
+static void unpack_fc(const int8_t *w, int N, int K, int8_t *dst, int portable)
 {
     for (int r0 = 0; r0 < N; r0 += 4) {
         const int R = N - r0 < 4 ? N - r0 : 4;
-        w += walk_block(w, R, K, dst, K, r0);
+        w += walk(portable, w, R, K, dst, K, r0);
     }
 }
 
 /* natural gate-major [4N][K] (rows g*N + u) from an lstm_8x16 stream */
-static void unpack_lstm(const int8_t *w, int N, int K, int8_t *dst)
+static void unpack_lstm(const int8_t *w, int N, int K, int8_t *dst, int portable)
 {
     for (int u0 = 0; u0 < N; u0 += 4) {
         const int R = N - u0 < 4 ? N - u0 : 4;
-        for (int g = 0; g < 4; ++g) w += walk_block(w, R, K, dst, K, g * N + u0);
+        for (int g = 0; g < 4; ++g) w += walk(portable, w, R, K, dst, K, g * N + u0);
     }
+}
+
+/* The accumulator scale qs of an affine_Krows call with a bias (affine.c).
+ * Shipped build: max(qin + qk, 15), and the align shift is dead (T1), so the
+ * sums stay at Q(qin + qk) while the bias is aligned to qs.  Portable build:
+ * the sums are shifted left by 15 - (qin + qk) (clamped) before the bias is
+ * added (affine.c:311-313).  The engine's epilogue is bias-then-shift, so the
+ * portable form is run as qs = qin + qk: (s + (b << (qs - qb))) << L equals
+ * clamp(s << L) + (b << (15 - qb)) exactly when qb <= qs and no clamp can bind
+ * -- checked against the worst case |sum| of every row (bound). */
+static long long sum_bound(const nnsp_layer_desc *d, int bias_sh);
+static int bias_qs(const nnsp_layer_desc *d, int qin, int layer, int *qs)
+{
+    const int q = qin + d->qk;
+    *qs = q > 15 ? q : 15;
+    if (!d->portable || q >= 15) return 0;
+    const int L = 15 - q;
+    const long long bound = sum_bound(d, q - d->qb);
+    if (bound < 0) return NNSP_ENOMEM;
+    const long long lim = d->acc32 ? (1LL << (31 - L)) : (1LL << 62 >> (L - 1));
+    if (d->qb > q || bound >= lim) {
+        nnsp_set_error("layer %d: portable align shift %d with qbit_bias %d / sum bound %lld not exactly "
+                       "representable", layer, L, d->qb, bound);
+        return NNSP_EUNSUPPORTED;
+    }
+    *qs = q;
+    return 0;
+}
+
+/* max over rows of |W x| (LSTM: the x part after its qir - qi shift, plus
+ * |Wr h|) + |b << bias_sh| for any int16 inputs: the layer's worst-case
+ * accumulator (-1: out of memory) */
+static void unpack_lstm_bias(const int16_t *b, int N, int16_t *dst);
+static long long sum_bound(const nnsp_layer_desc *d, int bias_sh)
+{
+    const int lstm = d->type == NN_LSTM;
+    const int rows = lstm ? 4 * d->N : d->N;
+    int8_t *nat = (int8_t *)calloc((size_t)rows * d->K, 1);
+    int8_t *natr = lstm ? (int8_t *)calloc((size_t)rows * d->N, 1) : NULL;
+    int16_t *bn = (int16_t *)calloc((size_t)rows, sizeof(int16_t));
+    long long best = -1;
+    if (!nat || !bn || (lstm && !natr)) goto out;
+    if (lstm) {
+        unpack_lstm(d->W, d->N, d->K, nat, d->portable);
+        unpack_lstm(d->Wr, d->N, d->N, natr, d->portable);
+        if (d->B) unpack_lstm_bias(d->B, d->N, bn);
+    } else {
+        unpack_fc(d->W, d->N, d->K, nat, d->portable);
+        if (d->B) memcpy(bn, d->B, (size_t)rows * sizeof(int16_t));
+    }
+    best = 0;
+    for (int r = 0; r < rows; ++r) {
+        long long sx = 0, sr = 0;
+        for (int k = 0; k < d->K; ++k) sx += abs(nat[(size_t)r * d->K + k]);
+        if (lstm)
+            for (int k = 0; k < d->N; ++k) sr += abs(natr[(size_t)r * d->N + k]);
+        long long v = sx * 32768;
+        if (lstm) {
+            const int xs = d->qir - d->qi;
+            v = xs >= 0 ? (xs < 24 ? v << xs : (1LL << 62)) : v >> -xs;
+            v += sr * 32768;
+        }
+        v += (long long)abs(bn[r]) << (bias_sh > 0 ? bias_sh : 0);
+        if (v > best) best = v;
+    }
+out:
+    free(nat);
+    free(natr);
+    free(bn);
+    return best;
 }
 
 static void unpack_lstm_bias(const int16_t *b, int N, int16_t *dst)
@@ -215,7 +306,11 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
             const int qs1 = d->qi + d->qk; /* first rc half: no bias */
             (void)qs1;
             y->xs_sh = d->qir - d->qi;
-            const int qs2 = y->has_bias ? (d->qir + d->qk > 15 ? d->qir + d->qk : 15) : d->qir + d->qk;
+            int qs2 = d->qir + d->qk;
+            if (y->has_bias) {
+                const int e = bias_qs(d, d->qir, i, &qs2);
+                if (e) return e;
+            }
             y->bias_sh = qs2 - d->qb;
             y->out_sh = 15 - qs2;
         } else {
@@ -226,7 +321,11 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
             y->nrt = (d->N + 15) / 16;
             y->rows = d->N;
             a_bytes += (size_t)y->nrt * y->nkt * 1024;
-            const int qs = y->has_bias ? (d->qi + d->qk > 15 ? d->qi + d->qk : 15) : d->qi + d->qk;
+            int qs = d->qi + d->qk;
+            if (y->has_bias) {
+                const int e = bias_qs(d, d->qi, i, &qs);
+                if (e) return e;
+            }
             y->bias_sh = qs - d->qb;
             y->out_sh = 15 - qs;
         }
@@ -272,13 +371,13 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
         int16_t *bnat = (int16_t *)calloc((size_t)rows_nat, sizeof(int16_t));
         if (!nat || !bnat || (lstm && !natr)) return NNSP_ENOMEM;
         if (lstm) {
-            unpack_lstm(d->W, d->N, d->K, nat);
-            unpack_lstm(d->Wr, d->N, d->N, natr);
+            unpack_lstm(d->W, d->N, d->K, nat, d->portable);
+            unpack_lstm(d->Wr, d->N, d->N, natr, d->portable);
             if (d->B) unpack_lstm_bias(d->B, d->N, bnat);
             put_frags(im->A + y->a_off, nat, d->K, y->nrt, y->nkt, d->N, 1);
             put_frags(im->A + y->ar_off, natr, d->N, y->nrt, y->nkt_r, d->N, 1);
         } else {
-            unpack_fc(d->W, d->N, d->K, nat);
+            unpack_fc(d->W, d->N, d->K, nat, d->portable);
             if (d->B) memcpy(bnat, d->B, (size_t)d->N * sizeof(int16_t));
             put_frags(im->A + y->a_off, nat, d->K, y->nrt, y->nkt, d->N, 0);
         }

@@ -125,6 +125,57 @@ __device__ __forceinline__ int32_t pspec_of(int32_t re, int32_t im) {
     return (int32_t)(((int64_t)re * re + (int64_t)im * im) >> 27);
 }
 
+// ---- the ARM_OPTIMIZED=0 build's FFT (row N4): fft.c:27-221, complex.c -----
+// No saturation is reproduced: for int16 PCM the Frac15 window output is
+// |x| <= 32767, so every FFT value stays below 256 * 2^15.5 < 2^24 and the
+// split below 2^25 -- complex.c's int32 clamps (complex.c:29-31, 66-69) and
+// rfft's (fft.c:108-111) never bind, and its 64-bit 4-point sums equal the
+// wrapping int32 sums.
+// complex32_complex16_elmtprod (complex.c:54-72): (z * w) >> 15, w a COMPLEX16
+// word (real low, imag high); the low 32 bits of the shifted 64-bit sums
+__device__ __forceinline__ void cmul15(int32_t& re, int32_t& im, uint32_t w) {
+    const int32_t wr = (int32_t)(int16_t)(w & 0xffffu), wi = (int32_t)w >> 16;
+    const int64_t R = mad_i64_i32(re, wr, mad_i64_i32(im, -wi, 0));
+    const int64_t I = mad_i64_i32(re, wi, mad_i64_i32(im, wr, 0));
+    re = (int32_t)((uint64_t)R >> 15);
+    im = (int32_t)((uint64_t)I >> 15);
+}
+
+// one radix-4 DIF butterfly of fft() (fft.c:128-221): complex32_affine with
+// M4 (fft.c:12-15) on (x0, x2, x1, x3), then every output -- r = 0 too -- times
+// its twiddle tw[4k + r]; output r goes to slot idx + r N/4 (the same slots as
+// bfly4: a, c', b', d')
+__device__ __forceinline__ void bfly4_port(int32_t (&v)[8], uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const int32_t xa = v[0], ya = v[1], xb = v[2], yb = v[3], xc = v[4], yc = v[5], xd = v[6], yd = v[7];
+    const int32_t r1 = wadd(xa, xc), s1 = wadd(ya, yc), r2 = wsub(xa, xc), s2 = wsub(ya, yc);
+    const int32_t t1 = wadd(xb, xd), u1 = wadd(yb, yd), t2 = wsub(yb, yd), u2 = wsub(xb, xd);
+    v[0] = wadd(r1, t1); v[1] = wadd(s1, u1);   // x0 + x1 + x2 + x3
+    v[2] = wsub(r1, t1); v[3] = wsub(s1, u1);   // x0 + x2 - x1 - x3
+    v[4] = wadd(r2, t2); v[5] = wsub(s2, u2);   // x0 - x2 - j x1 + j x3
+    v[6] = wsub(r2, t2); v[7] = wadd(s2, u2);   // x0 - x2 + j x1 - j x3
+    cmul15(v[0], v[1], w0);
+    cmul15(v[2], v[3], w1);
+    cmul15(v[4], v[5], w2);
+    cmul15(v[6], v[7], w3);
+}
+
+// rfft's split (fft.c:59-120) for bin i in 0..255: Z = the bit-reversed
+// fft() output, (zr, zi) = Z[i], (nr, ni) = Z[(256 - i) & 255], w = rfft_tw[i]
+__device__ __forceinline__ void split_bin_port(int32_t zr, int32_t zi, int32_t nr, int32_t ni, uint32_t w,
+                                               int32_t& re, int32_t& im) {
+    const int32_t tim = wsub(0, ni);
+    const int32_t er = wadd(zr, nr) >> 1, ei = wadd(zi, tim) >> 1;
+    int32_t orr = wsub(zi, tim) >> 1, oi = wsub(0, wsub(zr, nr)) >> 1;
+    cmul15(orr, oi, w);
+    re = wadd(orr, er);
+    im = wadd(oi, ei);
+}
+
+// spec2pspec (spectrogram_module.c:33-45): truncating cast of (re^2+im^2)>>15
+__device__ __forceinline__ int32_t pspec15_of(int32_t re, int32_t im) {
+    return (int32_t)((uint64_t)mad_i64_i32(re, re, mad_i64_i32(im, im, 0)) >> 15);
+}
+
 // my_log10 + norm_oneTwo (fixlog10.c:9-50), bit_frac_in = 15
 __device__ __forceinline__ int32_t log10_q15(int32_t x) {
     if (x == 0) x = 1;

@@ -68,7 +68,8 @@ typedef struct {
     int32_t max_blocks;       /* > 0: cap on the grid */
     int32_t wave_frames;      /* > 0: frames per wave (short-lived workgroups: a look-ahead front end
                                  yields CU slots to the nets' kernels as it goes); 0: persistent grid */
-    int32_t pad2_;
+    int32_t port;             /* 1: the ARM_OPTIMIZED=0 build's front end (row N4): Frac15 window,
+                                 fft.c's rfft, spec2pspec >> 15 */
     long long *dbg_clk;       /* development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0 of
                                  workgroup 0, its first 64 frames: dbg_clk[1024 + 8 * frame + phase] */
 } FeArgs;

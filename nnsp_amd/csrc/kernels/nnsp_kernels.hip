@@ -65,14 +65,34 @@ __device__ __forceinline__ int32_t fe_norm_word(const FeArgs& a, int k) {
     return k < 120 ? a.nmean[n][b] : a.nstdR[n][b];
 }
 
+// ARM_OPTIMIZED=0 (row N4): the tw area holds, per stage and lane, the four
+// COMPLEX16 twiddles tw[4k + r] of the lane's butterfly (3 KB of its 4.5 KB)
+__device__ __forceinline__ uint4* fe_twp(FeTables& T) { return reinterpret_cast<uint4*>(&T.tw[0][0][0]); }
+__device__ __forceinline__ const uint4* fe_twp(const FeTables& T) {
+    return reinterpret_cast<const uint4*>(&T.tw[0][0][0]);
+}
+
+template <bool PORT>
 __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
-    for (int i = threadIdx.x; i < 576; i += blockDim.x) {
-        const int s = i / 192, j = (i / 64) % 3, l = i % 64;
-        const int k = s == 0 ? l : (s == 1 ? 4 * (l & 15) : 16 * (l >> 4));
-        T.tw[s][j][l] = make_int2(nnsp_tbl_tw256[2 * (j + 1) * k], nnsp_tbl_tw256[2 * (j + 1) * k + 1]);
+    if (PORT) {   // fft.c:128-221: stage s butterfly m of its group uses tw[4 m 4^s + r]
+        for (int i = threadIdx.x; i < 192; i += blockDim.x) {
+            const int s = i / 64, l = i % 64;
+            const int k = s == 0 ? l : (s == 1 ? 4 * (l & 15) : 16 * (l >> 4));
+            fe_twp(T)[i] = make_uint4((uint32_t)nnsp_tbl_dif_tw[4 * k], (uint32_t)nnsp_tbl_dif_tw[4 * k + 1],
+                                      (uint32_t)nnsp_tbl_dif_tw[4 * k + 2], (uint32_t)nnsp_tbl_dif_tw[4 * k + 3]);
+        }
+        for (int k = threadIdx.x; k < 256; k += blockDim.x)   // rfft's twiddle of bin k (fft.c:103-105)
+            T.split[k] = make_int4(nnsp_tbl_dif_rtw[k], 0, 0, fe_norm_word(a, k));
+    } else {
+        for (int i = threadIdx.x; i < 576; i += blockDim.x) {
+            const int s = i / 192, j = (i / 64) % 3, l = i % 64;
+            const int k = s == 0 ? l : (s == 1 ? 4 * (l & 15) : 16 * (l >> 4));
+            T.tw[s][j][l] = make_int2(nnsp_tbl_tw256[2 * (j + 1) * k], nnsp_tbl_tw256[2 * (j + 1) * k + 1]);
+        }
+        for (int k = threadIdx.x; k < 256; k += blockDim.x)
+            T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2],
+                                   fe_norm_word(a, k));
     }
-    for (int k = threadIdx.x; k < 256; k += blockDim.x)
-        T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], fe_norm_word(a, k));
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
     if (threadIdx.x < 64) {
@@ -146,10 +166,26 @@ __device__ __forceinline__ void xpose_rows(int32_t (&v)[8]) {
 
 // cFFT (arm_radix4_butterfly_q31) of one frame held in v in the stage-1
 // layout; leaves the output in X at natural bin order (arm_bitreversal_32).
+// PORT: the ARM_OPTIMIZED=0 build's fft() (fft.c:128-221) -- the same DIF
+// data flow and output order, unscaled butterflies with Q15 twiddles on all
+// four outputs (bfly4_port).
+template <bool PORT>
+__device__ __forceinline__ void fe_bfly(int32_t (&v)[8], const FeTables& TB, int s, int lane) {
+    if (PORT) {
+        const uint4 w = fe_twp(TB)[64 * s + lane];
+        bfly4_port(v, w.x, w.y, w.z, w.w);
+    } else if (s == 0) {
+        bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 0, lane));
+    } else {
+        bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, s, lane));
+    }
+}
+
+template <bool PORT>
 __device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const FeTables& TB, int lane) {
-    bfly4<true>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 0, lane));
+    fe_bfly<PORT>(v, TB, 0, lane);
     xpose_rows(v);
-    bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 1, lane));
+    fe_bfly<PORT>(v, TB, 1, lane);
     {   // T2: stage-2 layout out, stage-3 layout in
         const int cw = 64 * (lane >> 4) + (lane & 15);
 #pragma unroll
@@ -163,9 +199,13 @@ __device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const 
             v[2 * m] = p.x; v[2 * m + 1] = p.y;
         }
     }
-    bfly4<false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], lds_tw3(TB, 2, lane));
+    fe_bfly<PORT>(v, TB, 2, lane);
     xpose_rows(v);
-    bfly4_last(v);
+    if (PORT)   // last stage: k = 0, tw[0..3]
+        bfly4_port(v, (uint32_t)nnsp_tbl_dif_tw[0], (uint32_t)nnsp_tbl_dif_tw[1], (uint32_t)nnsp_tbl_dif_tw[2],
+                   (uint32_t)nnsp_tbl_dif_tw[3]);
+    else
+        bfly4_last(v);
     wave_lds_sync();
     {   // register m is DIF position 64*d3 + 16*d2 + 4*d1 + m; its bin is rev8 of that
         const int c = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + 4 * (lane >> 4);
@@ -178,13 +218,18 @@ __device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const 
 
 // Split of bin k = lane + 64m from the natural-order cFFT output in X.
 // (k = 0 yields a don't-care value; DC / Nyquist come from wave_split_dc.)
+// PORT: rfft's split of bin k (fft.c:59-120), k = 0 included.
+template <bool PORT>
 __device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeTables& TB, int lane, int m,
                                                int32_t& re, int32_t& im) {
     const int k = lane + 64 * m;
     const int4 cf = TB.split[k];
     const int2 zk = *reinterpret_cast<const int2*>(X + 2 * zslot(k));
     const int2 zn = *reinterpret_cast<const int2*>(X + 2 * zslot((256 - k) & 255));
-    split_bin(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re, im);
+    if (PORT)
+        split_bin_port(zk.x, zk.y, zn.x, zn.y, (uint32_t)cf.x, re, im);
+    else
+        split_bin(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re, im);
 }
 
 // DC and Nyquist bins: (p0 + p1) >> 1, (p0 - p1) >> 1 (arm_split_rfft_q31 tail)
@@ -200,7 +245,9 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // (256, 6): at most 80 VGPRs, six waves per SIMD (window and Mel coefficients in LDS)
 // One instantiation per mode (FE_MODE_*): the batch and cold modes keep the
 // 80-VGPR budget of six waves per SIMD without the shared mode's ring writes.
-template <int MODE>
+// PORT: the ARM_OPTIMIZED=0 build's front end (row N4: Frac15 window, fft.c's
+// rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
+template <int MODE, bool PORT>
 __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
     __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
@@ -220,7 +267,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const unsigned wid0 = blockIdx.x * 4u + (threadIdx.x >> 6);
     long long* wclk = (a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    fe_tables_init(TB, a);
+    fe_tables_init<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = Xs[wv];
@@ -357,6 +404,10 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             for (int m = 0; m < 4; ++m) {
                 v[2 * m] = (int32_t)(int16_t)(wn[m] & 0xffff) * (int32_t)(int16_t)(raw[m] & 0xffff);
                 v[2 * m + 1] = (int32_t)(int16_t)(wn[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
+                if (PORT) {   // Frac15 (spectrogram_module.c:64-68)
+                    v[2 * m] >>= 15;
+                    v[2 * m + 1] >>= 15;
+                }
             }
         }
         // pin the products here: sunk past the prefetch (next to their use)
@@ -372,14 +423,14 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         flush();
         pend = false;
         FCLK(1);
-        wave_cfft256(v, X, TB, lane);
+        wave_cfft256<PORT>(v, X, TB, lane);
         FCLK(2);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
             int32_t re, im;
-            wave_split_bin(X, TB, lane, m, re, im);
-            P[lane + 64 * m] = pspec_of(re, im);
+            wave_split_bin<PORT>(X, TB, lane, m, re, im);
+            P[lane + 64 * m] = PORT ? pspec15_of(re, im) : pspec_of(re, im);
             if (a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 const int k = lane + 64 * m;
@@ -389,7 +440,17 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 }
             }
         }
-        if (lane == 0) {
+        if (PORT) {
+            if (lane == 0) {   // X(N/2+1) = Xe(1) - Xo(1) (fft.c:122-125); bin 0 came from the loop
+                const int2 z0 = *reinterpret_cast<const int2*>(X);
+                const int32_t nyq = wsub(wadd(z0.x, z0.x) >> 1, wadd(z0.y, z0.y) >> 1);
+                P[256] = pspec15_of(nyq, 0);
+                if (a.dbg_spec) {
+                    int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
+                    ds[512] = nyq; ds[513] = 0;
+                }
+            }
+        } else if (lane == 0) {
             int32_t dc, nyq;
             wave_split_dc(X, dc, nyq);
             P[0] = pspec_of(dc, 0);
@@ -759,7 +820,7 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
     __shared__ __attribute__((aligned(16))) FeTables TB;
     FeArgs none{};
     none.mode = FE_MODE_BATCH;
-    fe_tables_init(TB, none);
+    fe_tables_init<false>(TB, none);
     const int lane = threadIdx.x;
     __syncthreads();
     for (int b = blockIdx.x; b < n; b += gridDim.x) {
@@ -769,11 +830,11 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
             v[2 * m] = xb[2 * (64 * m + lane)];
             v[2 * m + 1] = xb[2 * (64 * m + lane) + 1];
         }
-        wave_cfft256(v, X, TB, lane);
+        wave_cfft256<false>(v, X, TB, lane);
         int32_t* yb = y + (size_t)b * 1024;
         for (int m = 0; m < 4; ++m) {
             int32_t re, im;
-            wave_split_bin(X, TB, lane, m, re, im);
+            wave_split_bin<false>(X, TB, lane, m, re, im);
             const int k = lane + 64 * m;
             if (k) {
                 yb[2 * k] = re; yb[2 * k + 1] = im;
@@ -1029,12 +1090,18 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
-    if (a->mode == FE_MODE_SHARED)
-        hipLaunchKernelGGL(fe_kernel<FE_MODE_SHARED>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
-    else if (a->mode == FE_MODE_COLD)
-        hipLaunchKernelGGL(fe_kernel<FE_MODE_COLD>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
-    else
-        hipLaunchKernelGGL(fe_kernel<FE_MODE_BATCH>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, *a);
+    const dim3 g((unsigned)blocks), blk(256);
+    hipStream_t st = (hipStream_t)stream;
+    if (a->mode == FE_MODE_SHARED) {
+        if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, true>), g, blk, 0, st, *a);
+        else hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, false>), g, blk, 0, st, *a);
+    } else if (a->mode == FE_MODE_COLD) {
+        if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_COLD, true>), g, blk, 0, st, *a);
+        else hipLaunchKernelGGL((fe_kernel<FE_MODE_COLD, false>), g, blk, 0, st, *a);
+    } else {
+        if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_BATCH, true>), g, blk, 0, st, *a);
+        else hipLaunchKernelGGL((fe_kernel<FE_MODE_BATCH, false>), g, blk, 0, st, *a);
+    }
     return ok(hipGetLastError());
 }
 

@@ -20,19 +20,22 @@ from .nets import LOOKBACK, NN_ID, THRESH_CNTS, THRESH_PROB, TIMEOUT, NetData, s
 
 class NNSPBatch:
     def __init__(self, net: NetData | str, n_streams: int, max_frames: int, acc32: bool = False,
-                 thresh_prob: int = THRESH_PROB, th_count: int = THRESH_CNTS, seed: int = 1234):
+                 thresh_prob: int = THRESH_PROB, th_count: int = THRESH_CNTS, seed: int = 1234,
+                 arm_optimized: bool = True):
+        """arm_optimized=False: the reference built with ARM_OPTIMIZED=0 (row N4):
+        portable front end and weight byte order (nnsp_batch_create_ex)."""
         if isinstance(net, str):
             net = synth_net(net, seed)
         self.data = net
-        self.handle = _lib.NetHandle(net, acc32=acc32)
+        self.handle = _lib.NetHandle(net, acc32=acc32, arm_optimized=arm_optimized)
         self.S, self.Tmax = n_streams, max_frames
         self.nn_id = net.spec.nn_id
         L = _lib.lib()
         h = C.c_void_p()
-        _lib.check(L.nnsp_batch_create(C.byref(h), self.handle.addr, self.nn_id,
-                                       _lib.ptr(self.handle.mean), _lib.ptr(self.handle.stdR),
-                                       thresh_prob, th_count, n_streams, max_frames),
-                   "nnsp_batch_create")
+        _lib.check(L.nnsp_batch_create_ex(C.byref(h), self.handle.addr, self.nn_id,
+                                          _lib.ptr(self.handle.mean), _lib.ptr(self.handle.stdR),
+                                          thresh_prob, th_count, n_streams, max_frames, int(bool(arm_optimized))),
+                   "nnsp_batch_create_ex")
         self.h = h
         self.nout = L.nnsp_batch_nout(h)
 
