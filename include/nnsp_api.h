@@ -43,7 +43,9 @@ extern "C" {
 #define DIM_SLOTS 17
 
 #define AMBIQ_NNSP_DEBUG 0
+#ifndef ARM_OPTIMIZED
 #define ARM_OPTIMIZED 1 /* the shipped build: CMSIS q31 rFFT + interleaved weights */
+#endif
 
 #ifndef MAX
 #define MAX(x, y) (((x) > (y)) ? (x) : (y))
@@ -161,6 +163,13 @@ int stftModule_construct(stftModule *ps);
 int stftModule_setDefault(stftModule *ps);
 void spec2pspec_arm(int32_t *y, int32_t *x, int len);
 int stftModule_analyze_arm(void *ps, int16_t *x, int32_t *y);
+/* the ARM_OPTIMIZED=0 build's stages (spectrogram_module.c:33-77, fft.h:4-5);
+ * exported beside the shipped ones.  rfft: num_rfft 512 only (y: 257
+ * complex); fft: exp_nfft 8 only (in place on its input, like fft.c) */
+void spec2pspec(int32_t *y, int32_t *x, int len);
+int stftModule_analyze(stftModule *ps, int16_t *x, int32_t *y);
+void rfft(int num_rfft, int32_t *input, void *output_);
+void fft(int exp_nfft, void *input_, void *output_);
 
 typedef struct {
     stftModule state_stftModule;
@@ -229,6 +238,16 @@ void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger);
  * error: nnsp_legacy_status() returns it (0: none; nnsp_strerror() describes
  * it) until nnsp_legacy_clear().  The process is never aborted. */
 int nnsp_legacy_status(void);
+/* Which build of the reference the drop-in API reproduces (row N4): 1 (the
+ * default) the shipped ARM_OPTIMIZED=1 build, 0 the ARM_OPTIMIZED=0 one --
+ * FeatureClass_execute / NNSPClass_exec run the portable front end, and
+ * NeuralNetClass_exe, fc_8x16, lstm_8x16, affine_Krows_8x16, rc_* read the
+ * portable weight order with the live align shift.  The reference fixes this
+ * at compile time; here a portable application calls
+ * nnsp_set_arm_optimized(0) once, or runs with NNSP_ARM_OPTIMIZED=0 in the
+ * environment.  Returns 0, or NNSP_EINVAL (-1) for a value other than 0 / 1. */
+int nnsp_set_arm_optimized(int arm_optimized);
+int nnsp_get_arm_optimized(void);
 void nnsp_legacy_clear(void);
 
 #ifdef __cplusplus

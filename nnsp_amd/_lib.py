@@ -167,6 +167,14 @@ def _declare(L: C.CDLL) -> None:
         "shift_64b": (None, [P, C.c_int8, I]),
         "shift_32b": (None, [P, C.c_int8, I]),
         "arm_fft_init": (None, []),
+        # the ARM_OPTIMIZED=0 build (row N4)
+        "nnsp_set_arm_optimized": (I, [I]),
+        "nnsp_get_arm_optimized": (I, []),
+        "rfft": (None, [I, P, P]),
+        "fft": (None, [I, P, P]),
+        "spec2pspec": (None, [P, P, I]),
+        "stftModule_analyze": (I, [P, P, P]),
+        "stftModule_setDefault": (I, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -35,7 +35,29 @@ static struct {
     int depth;   /* nesting of public entry points (the outermost holds jb) */
     jmp_buf jb;
     int sticky;  /* first error since nnsp_legacy_clear(); 0 = none */
-} G;
+    int port;    /* 1: the reference's ARM_OPTIMIZED=0 build (row N4); 2: not yet read */
+} G = {.port = 2};
+
+/* The build the drop-in API reproduces: the reference selects it at compile
+ * time (ARM_OPTIMIZED, ambiq_nnsp_debug.h:4); here nnsp_set_arm_optimized()
+ * or, before the first call, the environment (NNSP_ARM_OPTIMIZED=0). */
+static int port_on(void)
+{
+    if (G.port == 2) {
+        const char *e = getenv("NNSP_ARM_OPTIMIZED");
+        G.port = e && e[0] == '0' && e[1] == 0;
+    }
+    return G.port;
+}
+
+int nnsp_set_arm_optimized(int arm_optimized)
+{
+    if (arm_optimized != 0 && arm_optimized != 1) return NNSP_EINVAL;
+    G.port = !arm_optimized;
+    return 0;
+}
+
+int nnsp_get_arm_optimized(void) { return !port_on(); }
 
 static void fail(int code, const char *what)
 {
@@ -213,6 +235,7 @@ static img_node *net_image(const NeuralNetClass *net)
         h *= 1099511628211ULL;                   \
     } while (0)
     MIX(net->numlayers);
+    MIX(port_on());
     for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i) {
         MIX(net->size_layer[i]); MIX(net->size_layer[i + 1]); MIX(net->net_layer_type[i]);
         MIX(net->qbit_kernel[i]); MIX(net->qbit_input[i]); MIX(net->qbit_bias[i]); MIX(net->activation_type[i]);
@@ -223,6 +246,7 @@ static img_node *net_image(const NeuralNetClass *net)
     nnsp_layer_desc L[NN_MAX_LAYERS];
     int nl = 0, lin = 0;
     CK(nnsp_describe_net(net, L, &nl, &lin));
+    for (int i = 0; i < nl; ++i) L[i].portable = port_on();
     uint64_t bytes = 1469598103934665603ULL;
     for (int i = 0; i < nl; ++i) bytes = layer_bytes_hash(bytes, &L[i]);
     const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
@@ -304,13 +328,14 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
     d.acc32 = acc32;
     d.qk = qk; d.qb = qb; d.qi = qi; d.qir = qir;
     d.W = p_kernel; d.Wr = p_kernel_rec; d.B = p_bias;
+    d.portable = port_on();
     d.act = type == NN_LSTM ? 1 : nnsp_act_of(act);
     if (d.act < 0) {
         fprintf(stderr, "libnnsp_mi355x: unsupported activation function pointer\n");
         return -1;
     }
     const int ik[8] = {type, acc32, dim_output, dim_input, qk, qb, qi, (qir << 4) | d.act};
-    const uint64_t bytes = layer_bytes_hash(1469598103934665603ULL, &d);
+    const uint64_t bytes = layer_bytes_hash(1469598103934665603ULL, &d) ^ (d.portable ? 0x9e3779b97f4a7c15ULL : 0);
     img_node *n = img_find(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes);
     if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes, &d, 1, d.act == 3);
     int16_t in_pad[NN_MAX_K];
@@ -466,11 +491,12 @@ static void arm_fft_exec_impl(int32_t *y, int32_t *x) /* fft_arm.c:16-20 -> arm_
 
 /* one FE frame on the GPU: tail = dataBuffer[160..479] before the shift */
 static void fe_frame(const int16_t *tail, const int16_t *pcm, const int32_t *mean, const int32_t *stdR,
-                     int qbit, int16_t *feat40, int32_t *log40, int32_t *spec1024)
+                     int qbit, int16_t *feat40, int32_t *log40, int32_t *spec1024, int port)
 {
     begin();
     FeArgs a;
     memset(&a, 0, sizeof a);
+    a.port = port;
     a.pcm = (const int16_t *)up(pcm, 160 * 2);
     a.tail = (const int16_t *)up(tail, 320 * 2);
     a.S = 1; a.T = 1;
@@ -493,7 +519,7 @@ static int stftModule_analyze_arm_impl(void *ps_, int16_t *x, int32_t *y) /* :94
     stftModule *ps = (stftModule *)ps_;
     int16_t tail[320];
     memcpy(tail, ps->dataBuffer + 160, sizeof tail);
-    fe_frame(tail, x, NULL, NULL, 8, NULL, NULL, y);
+    fe_frame(tail, x, NULL, NULL, 8, NULL, NULL, y, 0);
     memmove(ps->dataBuffer, ps->dataBuffer + 160, 320 * 2);
     memcpy(ps->dataBuffer + 320, x, 160 * 2);
     return 0;
@@ -505,9 +531,66 @@ static void spec2pspec_arm_impl(int32_t *y, int32_t *x, int len) /* :79-92 */
     begin();
     int32_t *dx = (int32_t *)up(x, (size_t)2 * len * 4);
     int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
-    CK(nnspk_launch_pspec(dy, dx, len, 1, G.stream));
+    CK(nnspk_launch_pspec(dy, dx, len, 1, 27, G.stream));
     down(y, dy, (size_t)len * 4);
     fin();
+}
+
+/* ---- the ARM_OPTIMIZED=0 build's front-end stages (row N4) ---- */
+static int stftModule_analyze_impl(stftModule *ps, int16_t *x, int32_t *y) /* spectrogram_module.c:47-77 */
+{
+    int16_t tail[320];
+    int32_t spec[1024];
+    memcpy(tail, ps->dataBuffer + 160, sizeof tail);
+    fe_frame(tail, x, NULL, NULL, 8, NULL, NULL, spec, 1);
+    memcpy(y, spec, 514 * 4); /* rfft writes bins 0..256 (fft.c:27-126) */
+    memmove(ps->dataBuffer, ps->dataBuffer + 160, 320 * 2);
+    memcpy(ps->dataBuffer + 320, x, 160 * 2);
+    return 0;
+}
+
+static void spec2pspec_impl(int32_t *y, int32_t *x, int len) /* spectrogram_module.c:33-45 */
+{
+    if (len <= 0) return;
+    if (len > 1024) fail(NNSP_EINVAL, "spec2pspec: len > 1024");
+    begin();
+    int32_t *dx = (int32_t *)up(x, (size_t)2 * len * 4);
+    int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
+    CK(nnspk_launch_pspec(dy, dx, len, 1, 15, G.stream));
+    down(y, dy, (size_t)len * 4);
+    fin();
+}
+
+static void rfft_impl(int num_rfft, int32_t *input, void *output) /* fft.c:27-126 */
+{
+    if (num_rfft != 512) fail(NNSP_EUNSUPPORTED, "rfft: only num_rfft = 512 (the front end's) is supported");
+    begin();
+    int32_t *dx = (int32_t *)up(input, 512 * 4);
+    int32_t *dy = (int32_t *)up(NULL, 514 * 4);
+    CK(nnspk_launch_rfft_port(dx, dy, 1, 0, G.stream));
+    down(output, dy, 514 * 4);
+    fin();
+}
+
+static void fft_impl(int exp_nfft, void *input, void *output) /* fft.c:128-221 */
+{
+    if (exp_nfft != 8) fail(NNSP_EUNSUPPORTED, "fft: only exp_nfft = 8 (256 points, rfft(512)'s) is supported");
+    begin();
+    int32_t *dx = (int32_t *)up(input, 512 * 4);
+    int32_t *dy = (int32_t *)up(NULL, 512 * 4);
+    CK(nnspk_launch_rfft_port(dx, dy, 1, 1, G.stream));
+    int32_t z[512];
+    down(z, dy, sizeof z);
+    fin();
+    memcpy(output, z, sizeof z);
+    /* fft() works in place on its input: afterwards input[m] = Z[rev8(m)] */
+    int32_t *in = (int32_t *)input;
+    for (int m = 0; m < 256; ++m) {
+        unsigned r = 0;
+        for (int b = 0; b < 8; ++b) r |= ((m >> b) & 1u) << (7 - b);
+        in[2 * m] = z[2 * r];
+        in[2 * m + 1] = z[2 * r + 1];
+    }
 }
 
 static void melSpecProc_impl(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
@@ -576,7 +659,7 @@ static void FeatureClass_execute_impl(FeatureClass *ps, int16_t *input) /* :47-7
 {
     int16_t tail[320], f5[40];
     memcpy(tail, ps->state_stftModule.dataBuffer + 160, sizeof tail);
-    fe_frame(tail, input, ps->pt_norm_mean, ps->pt_norm_stdR, ps->qbit_output, f5, ps->feature, NULL);
+    fe_frame(tail, input, ps->pt_norm_mean, ps->pt_norm_stdR, ps->qbit_output, f5, ps->feature, NULL, port_on());
     memmove(ps->normFeatContext, ps->normFeatContext + 40, 200 * 2);
     memcpy(ps->normFeatContext + 200, f5, 80);
     memmove(ps->state_stftModule.dataBuffer, ps->state_stftModule.dataBuffer + 160, 320 * 2);
@@ -653,6 +736,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     a.norm_shift = 30 - fe->qbit_output;
     a.feats = (int16_t *)up(NULL, 80);
     a.dbg_log = (int32_t *)up(NULL, 160);
+    a.port = port_on();
     CK(nnspk_launch_fe(&a, G.stream));
     NnPost ps;
     post_pack(pt_inst, &ps);
@@ -765,6 +849,7 @@ static int affine_rows_call(int16_t R, int16_t **pp_output, int8_t **pp_kernel, 
     a.acc32 = acc32 != NULL;
     a.is_out = is_out;
     a.act = a_t;
+    a.port = port_on();
     int64_t acc[4];
     for (int i = 0; i < R; ++i) acc[i] = acc32 ? (int64_t)acc32[i] : acc64[i];
     a.w = (const int8_t *)up(*pp_kernel, (size_t)R * K);
@@ -823,6 +908,7 @@ static int rc_rows_call(int rows, int16_t *p_output, const int8_t *w, const int8
     a.acc32 = acc32;
     a.is_out = 1;
     a.act = a_t;
+    a.port = port_on();
     a.w = (const int8_t *)up(w, (size_t)rows * K);
     a.wr = (const int8_t *)up(wr, (size_t)rows * Kr);
     a.b = bias ? (const int16_t *)up(bias, (size_t)rows * 2) : NULL;
@@ -1079,6 +1165,55 @@ void spec2pspec_arm(int32_t *y, int32_t *x, int len)
         }
     }
     spec2pspec_arm_impl(y, x, len);
+    --G.depth;
+}
+
+int stftModule_analyze(stftModule *ps, int16_t *x, int32_t *y)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return G.sticky;
+        }
+    }
+    int r = stftModule_analyze_impl(ps, x, y);
+    --G.depth;
+    return r;
+}
+
+void spec2pspec(int32_t *y, int32_t *x, int len)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    spec2pspec_impl(y, x, len);
+    --G.depth;
+}
+
+void rfft(int num_rfft, int32_t *input, void *output)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    rfft_impl(num_rfft, input, output);
+    --G.depth;
+}
+
+void fft(int exp_nfft, void *input, void *output)
+{
+    if (G.depth++ == 0) {
+        if (setjmp(G.jb)) {
+            G.depth = 0;
+            return;
+        }
+    }
+    fft_impl(exp_nfft, input, output);
     --G.depth;
 }
 

@@ -174,7 +174,8 @@ typedef struct {
     int64_t *acc;             /* ROWS_AFFINE: [rows] accumulators in/out (int32 values for acc32) */
     int32_t mode, rows, K, Kr;
     int32_t qk, qb, qi, qir;
-    int32_t acc32, is_out, act, pad;
+    int32_t acc32, is_out, act;
+    int32_t port;             /* 1: the ARM_OPTIMIZED=0 build (portable byte order, live align shift) */
 } RowArgs;
 int nnspk_launch_rows(const RowArgs *a, void *stream);
 /* shift_64b / shift_32b (affine.c:565-591, affine_acc32b.c:566-592) over n values */
@@ -202,7 +203,9 @@ int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, cons
 int nnspk_launch_synth_pcm(int16_t *out, int S, int T, unsigned long long seed, int s0, long long t0, int amp,
                            const int16_t *wavs, int n_wavs, int wav_len, int every, void *stream);
 int nnspk_launch_rfft(int32_t *x, int32_t *y, int n, void *stream);
-int nnspk_launch_pspec(int32_t *y, const int32_t *x, int len, int n, void *stream);
+int nnspk_launch_pspec(int32_t *y, const int32_t *x, int len, int n, int shift, void *stream);
+/* the ARM_OPTIMIZED=0 build's rfft(512) (y [n][514]) or, cfft_only, fft(8) (y [n][512]) */
+int nnspk_launch_rfft_port(const int32_t *x, int32_t *y, int n, int cfft_only, void *stream);
 int nnspk_launch_mel(const int32_t *spec, int32_t *mel, int n, void *stream);
 int nnspk_launch_log10(int32_t *out, const int32_t *x, int n, int add, void *stream);
 int nnspk_launch_act(int type, const int32_t *x, void *y, int n, void *stream);

@@ -434,7 +434,9 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             if (a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 const int k = lane + 64 * m;
-                if (k) {
+                if (PORT) {   // rfft's output: bins 0..256 only
+                    ds[2 * k] = re; ds[2 * k + 1] = im;
+                } else if (k) {
                     ds[2 * k] = re; ds[2 * k + 1] = im;
                     ds[1024 - 2 * k] = re; ds[1024 - 2 * k + 1] = wsub(0, im);
                 }
@@ -855,12 +857,58 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
     }
 }
 
-__global__ void k_pspec(int32_t* y, const int32_t* x, int len, int n) {
+// The ARM_OPTIMIZED=0 build's rfft(512) (fft.c:27-126; cfft_only: its
+// fft(8, ...), fft.c:128-221, natural-order output) on n vectors: x [n][512]
+// (Frac15 reals, or 256 COMPLEX32), y [n][514] (bins 0..256) / [n][512].
+// The input is not modified (rfft copies it into cinput, fft.c:53-57).
+__global__ __launch_bounds__(64) void k_rfft_port(const int32_t* x, int32_t* y, int n, int cfft_only) {
+    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW];
+    __shared__ __attribute__((aligned(16))) FeTables TB;
+    FeArgs none{};
+    none.mode = FE_MODE_BATCH;
+    fe_tables_init<true>(TB, none);
+    const int lane = threadIdx.x;
+    __syncthreads();
+    for (int b = blockIdx.x; b < n; b += gridDim.x) {
+        const int32_t* xb = x + (size_t)b * 512;
+        int32_t v[8];
+        for (int m = 0; m < 4; ++m) {   // stage-1 layout: complex 64*m + lane
+            v[2 * m] = xb[2 * (64 * m + lane)];
+            v[2 * m + 1] = xb[2 * (64 * m + lane) + 1];
+        }
+        wave_cfft256<true>(v, X, TB, lane);
+        if (cfft_only) {
+            int32_t* yb = y + (size_t)b * 512;
+            for (int c = lane; c < 256; c += 64) {
+                yb[2 * c] = X[2 * zslot(c)];
+                yb[2 * c + 1] = X[2 * zslot(c) + 1];
+            }
+        } else {
+            int32_t* yb = y + (size_t)b * 514;
+            for (int m = 0; m < 4; ++m) {
+                int32_t re, im;
+                wave_split_bin<true>(X, TB, lane, m, re, im);
+                const int k = lane + 64 * m;
+                yb[2 * k] = re;
+                yb[2 * k + 1] = im;
+            }
+            if (lane == 0) {
+                const int2 z0 = *reinterpret_cast<const int2*>(X);
+                yb[512] = wsub(wadd(z0.x, z0.x) >> 1, wadd(z0.y, z0.y) >> 1);
+                yb[513] = 0;
+            }
+        }
+        wave_lds_sync();
+    }
+}
+
+// spec2pspec_arm (shift 27) / spec2pspec (shift 15): x [n][1024], y [n][1024]
+__global__ void k_pspec(int32_t* y, const int32_t* x, int len, int n, int shift) {
     const int b = blockIdx.y;
     if (b >= n) return;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < len; i += gridDim.x * blockDim.x) {
         const int32_t* xb = x + (size_t)b * 1024;
-        y[(size_t)b * 1024 + i] = pspec_of(xb[2 * i], xb[2 * i + 1]);
+        y[(size_t)b * 1024 + i] = shift == 15 ? pspec15_of(xb[2 * i], xb[2 * i + 1]) : pspec_of(xb[2 * i], xb[2 * i + 1]);
     }
 }
 
@@ -972,10 +1020,11 @@ __device__ __forceinline__ int rows_wofs(int R, int r, int c) {
     return R == 4 ? (r >> 1) * 4 + 2 * c + (r & 1) : (R == 3 ? (r < 2 ? 2 * c + r : 4 + c) : (R == 2 ? 2 * c + r : c));
 }
 // sum_k W[i][k] x[k] of row i (the SMLALD pairs, then the odd-column tail)
-__device__ int64_t rows_dot(const int8_t* w, const int16_t* x, int K, int rows, int i) {
+// port: the ARM_OPTIMIZED=0 order (affine.c:261-346), per column pair, per row
+__device__ int64_t rows_dot(const int8_t* w, const int16_t* x, int K, int rows, int i, int port) {
     const int g = i >> 2, r = i & 3, R = min(4, rows - 4 * g);
     const int8_t* wg = w + (size_t)g * 4 * K;
-    const int o0 = rows_wofs(R, r, 0), o1 = rows_wofs(R, r, 1);
+    const int o0 = port ? 2 * r : rows_wofs(R, r, 0), o1 = port ? 2 * r + 1 : rows_wofs(R, r, 1);
     int64_t s = 0;
     for (int p = 0; p < (K >> 1); ++p)
         s += (int64_t)wg[2 * R * p + o0] * x[2 * p] + (int64_t)wg[2 * R * p + o1] * x[2 * p + 1];
@@ -995,16 +1044,20 @@ __global__ void k_rows(RowArgs a) {
     int64_t s;
     int qs;
     if (a.mode == ROWS_RC) {
-        int64_t s1 = rows_dot(a.w, a.x, a.K, a.rows, i);   // no bias: qbit_s = qi + qk
+        int64_t s1 = rows_dot(a.w, a.x, a.K, a.rows, i, a.port);   // no bias: qbit_s = qi + qk
         if (a.acc32) s1 = shift32((int32_t)wrap32(s1), a.qir - a.qi);
         else s1 = shift64(s1, a.qir - a.qi);
-        s = s1 + rows_dot(a.wr, a.xr, a.Kr, a.rows, i);
+        s = s1 + rows_dot(a.wr, a.xr, a.Kr, a.rows, i, a.port);
         qs = a.b ? max(15, a.qir + a.qk) : a.qir + a.qk;
     } else {
-        s = a.acc[i] + rows_dot(a.w, a.x, a.K, a.rows, i);
+        s = a.acc[i] + rows_dot(a.w, a.x, a.K, a.rows, i, a.port);
         qs = a.b ? max(15, a.qi + a.qk) : a.qi + a.qk;
     }
     if (a.acc32) s = wrap32(s);
+    if (a.port) {   // the ARM_OPTIMIZED=0 build's live align shift (affine.c:311-313): 0 without a bias
+        const int al = qs - (a.mode == ROWS_RC ? a.qir : a.qi) - a.qk;
+        s = a.acc32 ? (int64_t)shift32((int32_t)s, al) : shift64(s, al);
+    }
     if (a.b) {
         const int sh = qs - a.qb;
         const int16_t bv = a.b[i];
@@ -1169,9 +1222,15 @@ int nnspk_launch_rfft(int32_t* x, int32_t* y, int n, void* stream) {
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_pspec(int32_t* y, const int32_t* x, int len, int n, void* stream) {
+int nnspk_launch_pspec(int32_t* y, const int32_t* x, int len, int n, int shift, void* stream) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_pspec, dim3((len + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, y, x, len, n);
+    hipLaunchKernelGGL(k_pspec, dim3((len + 255) / 256, n), dim3(256), 0, (hipStream_t)stream, y, x, len, n, shift);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_rfft_port(const int32_t* x, int32_t* y, int n, int cfft_only, void* stream) {
+    if (n <= 0) return 0;
+    hipLaunchKernelGGL(k_rfft_port, dim3(n < 4096 ? n : 4096), dim3(64), 0, (hipStream_t)stream, x, y, n, cfft_only);
     return ok(hipGetLastError());
 }
 
