@@ -256,8 +256,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
-    for (int i = 0; i < 3; ++i)
-        if ((e = nnspk_malloc((void **)&c->d_nring[i], S * (size_t)c->ring * 40 * 2))) goto fail;
+    /* the three rings in one allocation, ring n at n * S * ring * 40: the
+     * shared front end then stores through one base pointer */
+    if ((e = nnspk_malloc((void **)&c->d_nring[0], 3 * S * (size_t)c->ring * 40 * 2))) goto fail;
+    for (int i = 1; i < 3; ++i) c->d_nring[i] = c->d_nring[0] + (size_t)i * S * c->ring * 40;
     if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
     if ((e = nnspk_malloc((void **)&c->d_fresh, S))) goto fail;
     for (int i = 0; i < 3; ++i) {
@@ -367,7 +369,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     void *bufs[] = {c->d_st,      c->d_seg_begin, c->d_zero,    c->d_trig[0], c->d_trig[1],
                     c->d_trig[2], c->d_mask[0],   c->d_mask[1],
                     c->d_mask[2], c->d_list[0][0], c->d_list[0][1], c->d_list[0][2], c->d_hist[0], c->d_hist[1], c->d_hist[2],
-                    c->d_nring[0], c->d_nring[1], c->d_nring[2], c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
+                    c->d_nring[0], c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
                     c->d_ran,     c->d_pdef,      c->d_cold_list[0][0],
                     c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
                     c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2]};

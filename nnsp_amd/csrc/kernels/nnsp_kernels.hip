@@ -341,6 +341,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     };
     if (fbeg >= fend) return;
     const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
+    const unsigned nstride = shared ? (unsigned)a.S * (unsigned)a.ring * 40u : 0u;   // elements between rings
     Pos nx;
     nx.i = fbeg / W;
     nx.k = fbeg - nx.i * W;
@@ -363,10 +364,13 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     auto flush = [&]() {
         if (pend && lane < 40) {
             if constexpr (shared) {
+                // the host allocates the three rings contiguously (nring[n] =
+                // nring[0] + n * nstride): one base pointer live in the loop
                 const unsigned o = po * 40u + (unsigned)lane;   // < 2^31 (host)
-                a.nring[0][o] = (int16_t)(pv01 & 0xffff);
-                a.nring[1][o] = (int16_t)(pv01 >> 16);
-                a.nring[2][o] = (int16_t)pv2;
+                int16_t* r0 = a.nring[0] + o;
+                r0[0] = (int16_t)(pv01 & 0xffff);
+                r0[nstride] = (int16_t)(pv01 >> 16);
+                r0[2 * (size_t)nstride] = (int16_t)pv2;
             } else {
                 a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
@@ -431,7 +435,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             int32_t re, im;
             wave_split_bin<PORT>(X, TB, lane, m, re, im);
             P[lane + 64 * m] = PORT ? pspec15_of(re, im) : pspec_of(re, im);
-            if (a.dbg_spec) {
+            if (MODE == FE_MODE_BATCH && a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 const int k = lane + 64 * m;
                 if (PORT) {   // rfft's output: bins 0..256 only
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 const int2 z0 = *reinterpret_cast<const int2*>(X);
                 const int32_t nyq = wsub(wadd(z0.x, z0.x) >> 1, wadd(z0.y, z0.y) >> 1);
                 P[256] = pspec15_of(nyq, 0);
-                if (a.dbg_spec) {
+                if (MODE == FE_MODE_BATCH && a.dbg_spec) {
                     int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                     ds[512] = nyq; ds[513] = 0;
                 }
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             wave_split_dc(X, dc, nyq);
             P[0] = pspec_of(dc, 0);
             P[256] = pspec_of(nyq, 0);
-            if (a.dbg_spec) {
+            if (MODE == FE_MODE_BATCH && a.dbg_spec) {
                 int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
                 ds[0] = dc; ds[1] = 0; ds[512] = nyq; ds[513] = 0;
             }
@@ -492,7 +496,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
             for (int k = 0; k < FE_MEL_MAXSEG; ++k)
                 if (k < L.mcnt) mac += Mp[L.mfirst + k];
             const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
-            if (a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
+            if (MODE == FE_MODE_BATCH && a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
             if constexpr (shared) {
                 // (abs0 + t) % ring with t < T <= ring: one conditional subtract
                 unsigned slot = ring0 + (unsigned)t;
