@@ -200,6 +200,7 @@ int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
     b->port = !arm_optimized;
     b->out_linear = out_linear;
     b->norm_shift = 30 - net->qbit_input[0]; /* FeatureClass qbit_output, nn_speech.c:40-44 */
+    b->norm32 = nnsp_norm_fits32(mean, stdR, 40, b->norm_shift);
     int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count, 0);
     if (e) goto fail;
     b->nout = b->im.img.nout;
@@ -322,6 +323,7 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     fa.hist_frames = seg->hist_frames;
     fa.seg_len = seg->seg_len;
     fa.port = b->port;
+    fa.norm32 = b->norm32;
     if (timed) TRY(nnspk_event_record(b->ev[0], stream));
     TRY(nnspk_launch_fe(&fa, stream));
     if (timed) TRY(nnspk_event_record(b->ev[1], stream));

@@ -472,6 +472,7 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     fa.fresh = c->d_fresh;
     fa.mode = FE_MODE_COLD;
     fa.port = b->port;
+    fa.norm32 = b->norm32;
     fa.list = c->d_cold_list[r & 1][n];
     fa.n_list_dev = cnt + 3 + n;
     return nnspk_launch_fe(&fa, stream);
@@ -617,6 +618,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     fa.stdR = c->net[0]->d_stdR;
     fa.mode = FE_MODE_SHARED;
     fa.port = c->net[0]->port;
+    fa.norm32 = c->net[0]->norm32 && c->net[1]->norm32 && c->net[2]->norm32;
     fa.ring = c->ring;
     fa.abs0 = abs0;
     for (int n = 0; n < 3; ++n) {

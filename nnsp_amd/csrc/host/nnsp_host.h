@@ -51,6 +51,7 @@ struct nnsp_batch {
     int S, Tmax, nout, out_linear, norm_shift;
     int nn_id;                        /* NNSP_ID given at create (post-processing kind) */
     int port;                         /* 1: the ARM_OPTIMIZED=0 build (row N4), nnsp_batch_create_ex */
+    int norm32;                       /* normalisation fits int32 (nnsp_norm_fits32) */
     nnsp_image im;
     void *stream;
     void *ev[3];

@@ -72,7 +72,28 @@ typedef struct {
                                  fft.c's rfft, spec2pspec >> 15 */
     long long *dbg_clk;       /* development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0 of
                                  workgroup 0, its first 64 frames: dbg_clk[1024 + 8 * frame + phase] */
+    int32_t norm32;           /* 1: every normalisation's (feature - mean) * stdR >> shift provably fits
+                                 int32 (nnsp_norm_fits32): the 32-bit clamp path */
+    int32_t pad3_;
 } FeArgs;
+
+/* feature_module.c:67-73 in 32 bits: |log10 output| < 2^18 (|table| * 0x3796 >> 15
+ * plus 15 * 0x2688), so with m = max |mean|, r = max |stdR| the 64-bit
+ * (feature - mean) * stdR >> shift fits int32 when (2^18 + m) * r < 2^(31 + shift) */
+static inline int nnsp_norm_fits32(const int32_t *mean, const int32_t *stdR, int n, int shift)
+{
+    if (shift < 0 || shift > 31) return 0;
+    long long m = 0, r = 0;
+    for (int i = 0; i < n; ++i) {
+        const long long a = mean[i] < 0 ? -(long long)mean[i] : mean[i];
+        const long long b = stdR[i] < 0 ? -(long long)stdR[i] : stdR[i];
+        if (a > m) m = a;
+        if (b > r) r = b;
+    }
+    const long long d = (1LL << 18) + m;
+    if (d >= (1LL << 31)) return 0;
+    return d * r < ((1LL << 31) << shift); /* d, r < 2^31: no overflow */
+}
 
 /* Cascade: where a net's segment features come from -- its ring of the shared
  * front end's normalised output, except the frames within 2 frames of the

@@ -133,6 +133,17 @@ __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
     }
 }
 
+// feature_module.c:67-73: sat16(((int64)feature - mean) * stdR >> sh).  fast
+// (host-proved, nnsp_norm_fits32): the product's shifted value fits int32, so
+// one v_mad_i64_i32, the 32 bits at sh and a v_med3 clamp are exact.
+__device__ __forceinline__ int16_t fe_norm(int32_t lg, int32_t mn, int32_t sr, int sh, int fast) {
+    if (fast) {
+        const int32_t v = (int32_t)((uint64_t)mad_i64_i32(wsub(lg, mn), sr, 0) >> sh);
+        return (int16_t)min(max(v, -32768), 32767);   // v_med3_i32
+    }
+    return sat16((((int64_t)lg - mn) * sr) >> sh);
+}
+
 // log10 with the (value, slope) table in LDS (fixlog10.c:31-61, bit_frac_in 15)
 __device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp) {
     if (x == 0) x = 1;
@@ -509,14 +520,13 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
 #pragma unroll
                 for (int n = 0; n < 3; ++n) {   // each net's normalisation (feature_module.c:67-73)
                     const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
-                    nv[n] = sat16(mad_i64_i32(wsub(lg, mn), sr, 0) >> a.nshift[n]);
+                    nv[n] = fe_norm(lg, mn, sr, a.nshift[n], a.norm32);
                 }
                 pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
                 pv2 = nv[2];
             } else {
-                const int64_t d = (int64_t)lg - mean;
                 po = fo;
-                pv01 = (uint32_t)(uint16_t)sat16((d * stdR) >> a.norm_shift);
+                pv01 = (uint32_t)(uint16_t)fe_norm(lg, mean, stdR, a.norm_shift, a.norm32);
             }
         }
         pend = true;
