@@ -36,6 +36,9 @@ using namespace nnsp;
 // bit reversal), where the split reads bins k and 256-k.  LDS slots are
 // swizzled (zslot) so that every one of these accesses is bank-conflict-free.
 #define FE_MEL_MAXSEG 3   // max lane segments per Mel bank (nnsp_tbl_melseg)
+#ifndef FE_PAIR_DEFAULT
+#define FE_PAIR_DEFAULT 1   // fe_kernel2 (two frames per wave) for the batch mode
+#endif
 #define FE_X_DW 512   // dwords of one frame's complex buffer (256 complex)
 __device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (FE_MODE_COLD)
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
@@ -175,6 +178,43 @@ __device__ __forceinline__ void xpose_rows(int32_t (&v)[8]) {
     }
 }
 
+// T1 / T3 through LDS instead of permlane swaps (FE_XPOSE_LDS bit 0 / bit 1;
+// a v_permlane*_swap costs ~3 VALU issue slots, an LDS round trip none):
+//   T1 (stage-1 -> stage-2 layout): position c at slot c + 16 (c >> 6) -- rows
+//      of 64 padded to 80 -- conflict-free both ways; needs 320 slots, i.e. X
+//      and the P buffer behind it (P is dead during the cFFT)
+//   T3 (stage-3 -> stage-4 layout): zslot, as T2 / the final store
+#ifndef FE_XPOSE_LDS
+#define FE_XPOSE_LDS 0
+#endif
+__device__ __forceinline__ void xpose_t1_lds(int32_t (&v)[8], int32_t* X, int lane) {
+    int2* X2 = reinterpret_cast<int2*>(X);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) X2[80 * m + lane] = make_int2(v[2 * m], v[2 * m + 1]);
+    wave_lds_sync();
+    const int rb = 80 * (lane >> 4) + (lane & 15);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int2 p = X2[rb + 16 * m];
+        v[2 * m] = p.x; v[2 * m + 1] = p.y;
+    }
+    wave_lds_sync();
+}
+__device__ __forceinline__ void xpose_t3_lds(int32_t (&v)[8], int32_t* X, int lane) {
+    const int cw = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + (lane >> 4);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        *reinterpret_cast<int2*>(X + 2 * zslot(cw + 4 * m)) = make_int2(v[2 * m], v[2 * m + 1]);
+    wave_lds_sync();
+    const int cr = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + 4 * (lane >> 4);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+        const int2 p = *reinterpret_cast<const int2*>(X + 2 * zslot(cr + m));
+        v[2 * m] = p.x; v[2 * m + 1] = p.y;
+    }
+    wave_lds_sync();
+}
+
 // cFFT (arm_radix4_butterfly_q31) of one frame held in v in the stage-1
 // layout; leaves the output in X at natural bin order (arm_bitreversal_32).
 // PORT: the ARM_OPTIMIZED=0 build's fft() (fft.c:128-221) -- the same DIF
@@ -195,7 +235,10 @@ __device__ __forceinline__ void fe_bfly(int32_t (&v)[8], const FeTables& TB, int
 template <bool PORT>
 __device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const FeTables& TB, int lane) {
     fe_bfly<PORT>(v, TB, 0, lane);
-    xpose_rows(v);
+    if (FE_XPOSE_LDS & 1)
+        xpose_t1_lds(v, X, lane);
+    else
+        xpose_rows(v);
     fe_bfly<PORT>(v, TB, 1, lane);
     {   // T2: stage-2 layout out, stage-3 layout in
         const int cw = 64 * (lane >> 4) + (lane & 15);
@@ -211,7 +254,10 @@ __device__ __forceinline__ void wave_cfft256(int32_t (&v)[8], int32_t* X, const 
         }
     }
     fe_bfly<PORT>(v, TB, 2, lane);
-    xpose_rows(v);
+    if (FE_XPOSE_LDS & 2)
+        xpose_t3_lds(v, X, lane);
+    else
+        xpose_rows(v);
     if (PORT)   // last stage: k = 0, tw[0..3]
         bfly4_port(v, (uint32_t)nnsp_tbl_dif_tw[0], (uint32_t)nnsp_tbl_dif_tw[1], (uint32_t)nnsp_tbl_dif_tw[2],
                    (uint32_t)nnsp_tbl_dif_tw[3]);
@@ -260,8 +306,10 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
 template <int MODE, bool PORT>
 __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
-    __shared__ __attribute__((aligned(16))) int32_t Xs[4][FE_X_DW];
-    __shared__ __attribute__((aligned(16))) int32_t Ps[4][272];   // 257 used; +pad for branch-free Mel reads
+    // per wave: the cFFT buffer X (256 complex) and, right behind it, the
+    // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
+    // contiguous so that the padded T1 transpose may use both
+    __shared__ __attribute__((aligned(16))) int32_t XPs[4][FE_X_DW + 272];
     __shared__ int64_t Ms[4][64];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
@@ -281,8 +329,8 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     fe_tables_init<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    int32_t* X = Xs[wv];
-    int32_t* P = Ps[wv];
+    int32_t* X = XPs[wv];
+    int32_t* P = XPs[wv] + FE_X_DW;
     int64_t* Mp = Ms[wv];
     FeLane L;
     fe_lane_init(L, lane);
@@ -540,6 +588,296 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     }
 #undef FCLK
 }
+// ---- two frames per wave (FE_MODE_BATCH / FE_MODE_SHARED) -----------------
+// The same per-frame arithmetic as fe_kernel, with two frames' instruction
+// streams interleaved stage by stage: each LDS round trip of one frame
+// (T2, the split reads, the Mel reads, the bank sums) has the other frame's
+// butterflies to issue behind it.  About twice the registers (4 waves per
+// SIMD instead of 6: 8 frames in flight instead of 6); per wave the X / P
+// buffers of both frames; the Mel partial sums live in the frame's P (dead by
+// then).
+template <bool PORT>
+__device__ __forceinline__ void wave_cfft256x2(int32_t (&va)[8], int32_t (&vb)[8], int32_t* XA, int32_t* XB,
+                                               const FeTables& TB, int lane) {
+    fe_bfly<PORT>(va, TB, 0, lane);
+    fe_bfly<PORT>(vb, TB, 0, lane);
+    xpose_rows(va);
+    xpose_rows(vb);
+    fe_bfly<PORT>(va, TB, 1, lane);
+    fe_bfly<PORT>(vb, TB, 1, lane);
+    {   // T2 of both frames
+        const int cw = 64 * (lane >> 4) + (lane & 15);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            *reinterpret_cast<int2*>(XA + 2 * zslot(cw + 16 * m)) = make_int2(va[2 * m], va[2 * m + 1]);
+            *reinterpret_cast<int2*>(XB + 2 * zslot(cw + 16 * m)) = make_int2(vb[2 * m], vb[2 * m + 1]);
+        }
+        wave_lds_sync();
+        const int cr = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + (lane >> 4);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            const int2 p = *reinterpret_cast<const int2*>(XA + 2 * zslot(cr + 4 * m));
+            const int2 q = *reinterpret_cast<const int2*>(XB + 2 * zslot(cr + 4 * m));
+            va[2 * m] = p.x; va[2 * m + 1] = p.y;
+            vb[2 * m] = q.x; vb[2 * m + 1] = q.y;
+        }
+    }
+    fe_bfly<PORT>(va, TB, 2, lane);
+    fe_bfly<PORT>(vb, TB, 2, lane);
+    xpose_rows(va);
+    xpose_rows(vb);
+    if (PORT) {
+        bfly4_port(va, (uint32_t)nnsp_tbl_dif_tw[0], (uint32_t)nnsp_tbl_dif_tw[1], (uint32_t)nnsp_tbl_dif_tw[2],
+                   (uint32_t)nnsp_tbl_dif_tw[3]);
+        bfly4_port(vb, (uint32_t)nnsp_tbl_dif_tw[0], (uint32_t)nnsp_tbl_dif_tw[1], (uint32_t)nnsp_tbl_dif_tw[2],
+                   (uint32_t)nnsp_tbl_dif_tw[3]);
+    } else {
+        bfly4_last(va);
+        bfly4_last(vb);
+    }
+    wave_lds_sync();
+    {
+        const int c = 64 * ((lane >> 2) & 3) + 16 * (lane & 3) + 4 * (lane >> 4);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            *reinterpret_cast<int2*>(XA + 2 * zslot(rev8(c + m))) = make_int2(va[2 * m], va[2 * m + 1]);
+            *reinterpret_cast<int2*>(XB + 2 * zslot(rev8(c + m))) = make_int2(vb[2 * m], vb[2 * m + 1]);
+        }
+    }
+    wave_lds_sync();
+}
+
+template <int MODE, bool PORT>
+__global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
+    static_assert(MODE != FE_MODE_COLD, "the cold front end runs fe_kernel");
+    __shared__ __attribute__((aligned(16))) int32_t XPs[4][2][FE_X_DW + 272];
+    __shared__ __attribute__((aligned(16))) FeTables TB;
+    const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
+    const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
+    constexpr bool shared = MODE == FE_MODE_SHARED;
+    const unsigned nfr = nrow * W;   // host guarantees < 2^31
+    const unsigned nw = gridDim.x * 4u;
+    const unsigned per = ((nfr + nw - 1) / nw + 1) & ~1u;   // even: whole pairs per wave
+    if (blockIdx.x * 4u * per >= nfr) return;
+    fe_tables_init<PORT>(TB, a);
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    int32_t* XA = XPs[wv][0];
+    int32_t* XB = XPs[wv][1];
+    int32_t* PA = XA + FE_X_DW;
+    int32_t* PB = XB + FE_X_DW;
+    FeLane L;
+    fe_lane_init(L, lane);
+    const int32_t mean = lane < 40 ? a.mean[lane] : 0;
+    const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
+    __syncthreads();
+    const unsigned wid = blockIdx.x * 4u + (unsigned)wv;
+    const unsigned fbeg = wid * per;
+    const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
+    if (fbeg >= fend) return;
+    struct Pos { unsigned i, k; int s, b, t, lim; };
+    // the shared front end runs every stream's whole chunk (no list, no
+    // segments, no look-back): row i is stream i, b = 0
+    auto row_of = [&](Pos& p) {
+        if constexpr (shared) {
+            p.s = (int)p.i;
+            p.b = 0;
+        } else {
+            p.s = a.list ? a.list[p.i] : (int)p.i;
+            p.b = a.seg_begin ? a.seg_begin[p.s] : 0;
+        }
+        p.lim = a.T;
+    };
+    auto advance = [&](Pos& p) {
+        if (++p.k == W) { p.k = 0; ++p.i; row_of(p); }
+        p.t = p.b + (int)p.k;
+    };
+    auto frame_ptr = [&](const Pos& p, int fi) -> const int16_t* {
+        if (fi < p.b)
+            return a.tail + (size_t)p.s * (a.tail_stride ? (unsigned)a.tail_stride : 320u) + (fi - p.b + 2) * 160;
+        if constexpr (shared) return a.pcm + ((size_t)p.s * a.T + fi) * 160;
+        const int x = fi - a.lookback;
+        return x >= 0 ? a.pcm + ((size_t)p.s * a.T + x) * 160
+                      : a.hist + ((size_t)p.s * a.hist_frames + a.hist_frames + x) * 160;
+    };
+    auto load_frame = [&](const Pos& p, uint32_t (&r)[4]) {
+        const int o = 2 * lane;
+        const int x0 = shared ? p.t - 2 : p.t - 2 - a.lookback;
+        if (p.t - 2 >= p.b && x0 >= 0) {
+            const int16_t* q = a.pcm + ((size_t)p.s * a.T + x0) * 160 + o;
+            r[0] = *reinterpret_cast<const uint32_t*>(q);
+            r[1] = *reinterpret_cast<const uint32_t*>(q + 128);
+            r[2] = *reinterpret_cast<const uint32_t*>(q + 256);
+            r[3] = *reinterpret_cast<const uint32_t*>(q + (lane < 48 ? 384 : 0));
+            return;
+        }
+        const int16_t* p0 = frame_ptr(p, p.t - 2);
+        const int16_t* p1 = frame_ptr(p, p.t - 1);
+        const int16_t* p2 = frame_ptr(p, p.t);
+        r[0] = *reinterpret_cast<const uint32_t*>(p0 + o);
+        r[1] = *reinterpret_cast<const uint32_t*>(lane < 16 ? p0 + 128 + o : p1 + o - 32);
+        r[2] = *reinterpret_cast<const uint32_t*>(lane < 32 ? p1 + 96 + o : p2 + o - 64);
+        r[3] = *reinterpret_cast<const uint32_t*>(lane < 48 ? p2 + 64 + o : p2 + o - 96);
+    };
+    auto window = [&](const uint32_t (&raw)[4], int32_t (&v)[8]) {
+        const uint4 w4 = TB.win[lane];
+        const uint32_t wn[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            v[2 * m] = (int32_t)(int16_t)(wn[m] & 0xffff) * (int32_t)(int16_t)(raw[m] & 0xffff);
+            v[2 * m + 1] = (int32_t)(int16_t)(wn[m] >> 16) * (int32_t)(int16_t)(raw[m] >> 16);
+            if (PORT) {
+                v[2 * m] >>= 15;
+                v[2 * m + 1] >>= 15;
+            }
+        }
+    };
+    auto hist_store = [&](const Pos& p, const uint32_t (&raw)[4]) {
+        if (a.hist_out && p.t >= a.T - a.hist_frames) {
+            int16_t* h = a.hist_out + ((size_t)p.s * a.hist_frames + (p.t - (a.T - a.hist_frames))) * 160;
+            if (lane >= 32) *reinterpret_cast<uint32_t*>(h + 2 * lane - 64) = raw[2];
+            if (lane < 48) *reinterpret_cast<uint32_t*>(h + 64 + 2 * lane) = raw[3];
+        }
+    };
+    const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
+    const unsigned nstride = shared ? (unsigned)a.S * (unsigned)a.ring * 40u : 0u;
+    // pending outputs of the previous pair (stored after the next pair's window multiply)
+    bool pendA = false, pendB = false;
+    unsigned poA = 0, poB = 0;
+    uint32_t pvA = 0u, pvB = 0u;
+    int32_t p2A = 0, p2B = 0;
+    auto flush1 = [&](bool pend, unsigned po, uint32_t pv01, int32_t pv2) {
+        if (pend && lane < 40) {
+            if constexpr (shared) {
+                int16_t* r0 = a.nring[0] + (po * 40u + (unsigned)lane);
+                r0[0] = (int16_t)(pv01 & 0xffff);
+                r0[nstride] = (int16_t)(pv01 >> 16);
+                r0[2 * (size_t)nstride] = (int16_t)pv2;
+            } else {
+                a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
+            }
+        }
+    };
+    // log10 + normalise of one frame (lanes < 40) from its Mel partial sums in Mq
+    auto tail = [&](const Pos& p, const int64_t* Mq, unsigned& po, uint32_t& pv01, int32_t& pv2) {
+        if (lane < 40) {
+            int64_t mac = 0;
+#pragma unroll
+            for (int k = 0; k < FE_MEL_MAXSEG; ++k)
+                if (k < L.mcnt) mac += Mq[L.mfirst + k];
+            const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
+            if constexpr (shared) {
+                unsigned slot = ring0 + (unsigned)p.t;
+                if (slot >= (unsigned)a.ring) slot -= (unsigned)a.ring;
+                po = (unsigned)p.s * (unsigned)a.ring + slot;
+                __asm__ volatile("" ::: "memory");
+                int16_t nv[3];
+#pragma unroll
+                for (int n = 0; n < 3; ++n) {
+                    const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
+                    nv[n] = fe_norm(lg, mn, sr, a.nshift[n], a.norm32);
+                }
+                pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
+                pv2 = nv[2];
+            } else {
+                po = (unsigned)p.s * (unsigned)a.T + (unsigned)p.t;
+                pv01 = (uint32_t)(uint16_t)fe_norm(lg, mean, stdR, a.norm_shift, a.norm32);
+            }
+        }
+    };
+    Pos nA, nB;
+    nA.i = fbeg / W;
+    nA.k = fbeg - nA.i * W;
+    row_of(nA);
+    nA.t = nA.b + (int)nA.k;
+    nB = nA;
+    uint32_t rawA[4] = {0u, 0u, 0u, 0u}, rawB[4] = {0u, 0u, 0u, 0u};
+    load_frame(nA, rawA);
+    if (fbeg + 1 < fend) {
+        advance(nB);
+        load_frame(nB, rawB);
+    }
+    for (unsigned f = fbeg; f < fend; f += 2) {
+        const Pos cA = nA, cB = nB;
+        const bool hasB = f + 1 < fend;   // wave-uniform
+        hist_store(cA, rawA);
+        if (hasB) hist_store(cB, rawB);
+        int32_t va[8], vb[8];
+        window(rawA, va);
+        window(rawB, vb);
+        asm volatile("" : "+v"(va[0]), "+v"(va[1]), "+v"(va[2]), "+v"(va[3]), "+v"(va[4]), "+v"(va[5]), "+v"(va[6]),
+                     "+v"(va[7]));
+        asm volatile("" : "+v"(vb[0]), "+v"(vb[1]), "+v"(vb[2]), "+v"(vb[3]), "+v"(vb[4]), "+v"(vb[5]), "+v"(vb[6]),
+                     "+v"(vb[7]));
+        if (f + 2 < fend) {   // prefetch the next pair
+            nA = cB;
+            advance(nA);
+            load_frame(nA, rawA);
+            if (f + 3 < fend) {
+                nB = nA;
+                advance(nB);
+                load_frame(nB, rawB);
+            }
+        }
+        flush1(pendA, poA, pvA, p2A);
+        flush1(pendB, poB, pvB, p2B);
+        wave_cfft256x2<PORT>(va, vb, XA, XB, TB, lane);
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+            int32_t ra, ia, rb, ib;
+            wave_split_bin<PORT>(XA, TB, lane, m, ra, ia);
+            wave_split_bin<PORT>(XB, TB, lane, m, rb, ib);
+            PA[lane + 64 * m] = PORT ? pspec15_of(ra, ia) : pspec_of(ra, ia);
+            PB[lane + 64 * m] = PORT ? pspec15_of(rb, ib) : pspec_of(rb, ib);
+        }
+        if (lane == 0) {
+            if (PORT) {
+                const int2 za = *reinterpret_cast<const int2*>(XA), zb = *reinterpret_cast<const int2*>(XB);
+                PA[256] = pspec15_of(wsub(wadd(za.x, za.x) >> 1, wadd(za.y, za.y) >> 1), 0);
+                PB[256] = pspec15_of(wsub(wadd(zb.x, zb.x) >> 1, wadd(zb.y, zb.y) >> 1), 0);
+            } else {
+                int32_t dc, nyq;
+                wave_split_dc(XA, dc, nyq);
+                PA[0] = pspec_of(dc, 0);
+                PA[256] = pspec_of(nyq, 0);
+                wave_split_dc(XB, dc, nyq);
+                PB[0] = pspec_of(dc, 0);
+                PB[256] = pspec_of(nyq, 0);
+            }
+        }
+        wave_lds_sync();
+        {   // Mel (melSpecProc.c:6-27) of both frames; partial sums into the dead X
+            int64_t ma = 0, mb = 0;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const uint2 c2 = TB.mc[j][lane];
+                const uint32_t cc[2] = {c2.x, c2.y};
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int i = 2 * j + h;
+                    const int2 pa = make_int2(PA[L.mj0 + 2 * i], PA[L.mj0 + 2 * i + 1]);
+                    const int2 pb = make_int2(PB[L.mj0 + 2 * i], PB[L.mj0 + 2 * i + 1]);
+                    const int32_t c0 = (int32_t)(int16_t)(cc[h] & 0xffff), c1 = (int32_t)cc[h] >> 16;
+                    ma = mad_i64_i32(c0, pa.x, ma);
+                    mb = mad_i64_i32(c0, pb.x, mb);
+                    ma = mad_i64_i32(c1, pa.y, ma);
+                    mb = mad_i64_i32(c1, pb.y, mb);
+                }
+            }
+            reinterpret_cast<int64_t*>(XA)[lane] = ma;
+            reinterpret_cast<int64_t*>(XB)[lane] = mb;
+        }
+        wave_lds_sync();
+        tail(cA, reinterpret_cast<const int64_t*>(XA), poA, pvA, p2A);
+        tail(cB, reinterpret_cast<const int64_t*>(XB), poB, pvB, p2B);
+        pendA = true;
+        pendB = hasB;
+        wave_lds_sync();
+    }
+    flush1(pendA, poA, pvA, p2A);
+    flush1(pendB, poB, pvB, p2B);
+}
+
 // ============================================================================
 // NN: generic fc / lstm stack on int8 MFMA
 // ============================================================================
@@ -832,7 +1170,7 @@ __global__ __launch_bounds__(256) void nring_fill_kernel(NringFill f, int ring, 
 // Stage kernels (legacy scalar API + per-stage parity tests)
 // ============================================================================
 __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
-    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW];
+    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW + 272];   // + room for the padded T1
     __shared__ __attribute__((aligned(16))) FeTables TB;
     FeArgs none{};
     none.mode = FE_MODE_BATCH;
@@ -876,7 +1214,7 @@ __global__ __launch_bounds__(64) void k_rfft(int32_t* x, int32_t* y, int n) {
 // (Frac15 reals, or 256 COMPLEX32), y [n][514] (bins 0..256) / [n][512].
 // The input is not modified (rfft copies it into cinput, fft.c:53-57).
 __global__ __launch_bounds__(64) void k_rfft_port(const int32_t* x, int32_t* y, int n, int cfft_only) {
-    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW];
+    __shared__ __attribute__((aligned(16))) int32_t X[FE_X_DW + 272];   // + room for the padded T1
     __shared__ __attribute__((aligned(16))) FeTables TB;
     FeArgs none{};
     none.mode = FE_MODE_BATCH;
@@ -1159,6 +1497,31 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
     const dim3 g((unsigned)blocks), blk(256);
     hipStream_t st = (hipStream_t)stream;
+    // two frames per wave (fe_kernel2): NNSP_FE_PAIR = 0 off, 1 the batch mode
+    // only (default), 2 the shared mode too.  Measured (A/B on one box): batch
+    // FE 0.55 -> 0.52 ms (VAD, 8192 streams); shared FE 2.18 -> 2.34 ms (fewer
+    // waves per SIMD keep its VALU less busy: SQ_ACTIVE_INST_VALU 95 -> 88 %)
+    static const int pair = [] {
+        const char* e = getenv("NNSP_FE_PAIR");
+        return e ? atoi(e) : FE_PAIR_DEFAULT;
+    }();
+    const bool use_pair = a->mode == FE_MODE_BATCH ? pair >= 1 : (a->mode == FE_MODE_SHARED && pair >= 2);
+    // (no segments: every frame of a listed row is inside the chunk)
+    if (use_pair && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk && a->wave_frames <= 0) {
+        // whole multiples of the resident workgroups at four per CU
+        long long b2 = (nfr + 7) / 8;
+        if (b2 > 256LL * 4 * 4) b2 = 256LL * 4 * 4;
+        if (a->max_blocks > 0 && b2 > a->max_blocks) b2 = a->max_blocks;
+        const dim3 g2((unsigned)b2);
+        if (a->mode == FE_MODE_SHARED) {
+            if (a->port) hipLaunchKernelGGL((fe_kernel2<FE_MODE_SHARED, true>), g2, blk, 0, st, *a);
+            else hipLaunchKernelGGL((fe_kernel2<FE_MODE_SHARED, false>), g2, blk, 0, st, *a);
+        } else {
+            if (a->port) hipLaunchKernelGGL((fe_kernel2<FE_MODE_BATCH, true>), g2, blk, 0, st, *a);
+            else hipLaunchKernelGGL((fe_kernel2<FE_MODE_BATCH, false>), g2, blk, 0, st, *a);
+        }
+        return ok(hipGetLastError());
+    }
     if (a->mode == FE_MODE_SHARED) {
         if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, true>), g, blk, 0, st, *a);
         else hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, false>), g, blk, 0, st, *a);

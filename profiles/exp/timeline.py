@@ -3,7 +3,7 @@ the per-round gap accounting (development helper)."""
 import csv, sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-big = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("fe_kernel")
+big = [i for i, r in enumerate(rows) if r["Kernel_Name"].replace("void ", "").startswith("fe_kernel<1")
        and int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) > 1e6]
 i0, i1 = big[-2], big[-1]
 t0 = int(rows[i0]["Start_Timestamp"])
