@@ -796,9 +796,13 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
             }
         }
         TRY(join_rounds(c, r));
-        int32_t cnt[3];
-        TRY(nnspk_d2h(cnt, c->d_counts + 6 * (r % 3), 12, c->stream));
+        /* all the chunk's counters in one copy (the next round's list lengths
+         * among them): if no round is left they are final, and the
+         * bookkeeping needs no further host wait */
+        TRY(nnspk_d2h(c->h_book, c->d_zero, ZERO_BYTES, c->stream));
+        TRY(nnspk_event_record(c->ev_book, c->stream));
         TRY(nnspk_sync(c->stream));
+        const int32_t *cnt = (const int32_t *)((const char *)c->h_book + 3 * 8) + 6 * (r % 3);
         if (cnt[0] + cnt[1] + cnt[2] == 0) break;
         R = r + 2;
     }
@@ -810,15 +814,15 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         c->pre_T = next_T;
     }
     TRY(nnspk_event_record(c->ev[1], c->stream));
-    /* bookkeeping without a host wait: the counters to pinned memory, then
-     * cleared for the next chunk (book_take reads the copy) */
-    TRY(nnspk_d2h(c->h_book, c->d_zero, ZERO_BYTES, c->stream));
-    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream));
-    TRY(nnspk_event_record(c->ev_book, c->stream));
+    /* bookkeeping: h_book was copied before the last synchronisation, so it
+     * is taken now (no host wait at the next call), and the device counters
+     * are cleared for the next chunk behind the rounds */
     c->book_pending = 1;
     c->book_rounds = r;
     c->book_ahead = ahead_launched;
     c->book_ahead_done = ahead_done;
+    TRY(book_take(c));
+    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream));
     return 0;
 }
 

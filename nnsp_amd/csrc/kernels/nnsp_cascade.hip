@@ -28,8 +28,16 @@ using nnsp::list_next;
 
 inline int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
-__global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
+// Round 0's lists: every stream under the net at its sequence position.  The
+// appends are aggregated per 1024-thread workgroup (one global atomic per list
+// and workgroup, 9 in all): per-wave atomics on the same six counters (4 600
+// for 32 768 streams) serialised at the L2 and took ~40 us.
+__global__ __launch_bounds__(1024) void casc_begin_kernel(CascArgs a) {
+    __shared__ int wcnt[16][6];   // per wave: entries for list k (k < 3) and cold list k - 3
+    __shared__ int gbase[6];
+    __shared__ unsigned long long fsum[3];
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nwv = blockDim.x >> 6;
     const bool ok_s = s < a.S;
     int n = 0, fr = 2;
     if (ok_s) {
@@ -37,8 +45,44 @@ __global__ __launch_bounds__(256) void casc_begin_kernel(CascArgs a) {
         n = nnsp::seq_at(a, a.st[s].pos);
         fr = a.fresh[s];
     }
-    list_next(a, n, s, ok_s, fr);
-    add_frames(a, n, ok_s ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, a.T) : a.T) : 0ull);
+    unsigned long long m[6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        m[k] = __ballot(ok_s && n == k);
+        m[k + 3] = __ballot(ok_s && n == k && fr < 2);
+    }
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) wcnt[w][j] = __popcll(m[j]);
+    if (threadIdx.x < 3) fsum[threadIdx.x] = 0ull;
+    __syncthreads();
+    if (threadIdx.x < 6) {   // exclusive prefix over the waves, one global atomic per list
+        const int j = threadIdx.x;
+        int tot = 0;
+        for (int q = 0; q < nwv; ++q) {
+            const int c = wcnt[q][j];
+            wcnt[q][j] = tot;
+            tot += c;
+        }
+        gbase[j] = tot ? atomicAdd(&a.counts[j], tot) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+        if ((m[j] >> lane) & 1ull) {
+            int32_t* lst = j < 3 ? a.list[j] : a.cold_list[j - 3];
+            lst[gbase[j] + wcnt[w][j] + __popcll(m[j] & ((1ull << lane) - 1ull))] = s;
+        }
+    // frames scheduled per net (statistics): wave sums, then one atomic per net
+    const unsigned long long v = ok_s ? (unsigned long long)(a.seg_len > 0 ? min(a.seg_len, a.T) : a.T) : 0ull;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        unsigned long long x = n == k ? v : 0ull;
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+        if (lane == 0 && x) atomicAdd(&fsum[k], x);
+    }
+    __syncthreads();
+    if (threadIdx.x < 3 && fsum[threadIdx.x] && a.frames) atomicAdd(&a.frames[threadIdx.x], fsum[threadIdx.x]);
 }
 
 __global__ __launch_bounds__(256) void casc_control_kernel(CascArgs a) {
@@ -158,7 +202,7 @@ extern "C" {
 
 int nnspk_launch_casc_begin(const CascArgs* a, void* stream) {
     if (a->S <= 0) return 0;
-    hipLaunchKernelGGL(casc_begin_kernel, dim3((a->S + 255) / 256), dim3(256), 0, (hipStream_t)stream, *a);
+    hipLaunchKernelGGL(casc_begin_kernel, dim3((a->S + 1023) / 1024), dim3(1024), 0, (hipStream_t)stream, *a);
     return ok(hipGetLastError());
 }
 
