@@ -796,6 +796,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
             }
         }
         TRY(join_rounds(c, r));
+        TRY(nnspk_event_record(c->ev[1], c->stream)); /* the rounds' end (complete at the sync below) */
         /* all the chunk's counters in one copy (the next round's list lengths
          * among them): if no round is left they are final, and the
          * bookkeeping needs no further host wait */
@@ -813,7 +814,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         c->pre_pcm = next_pcm;
         c->pre_T = next_T;
     }
-    TRY(nnspk_event_record(c->ev[1], c->stream));
     /* bookkeeping: h_book was copied before the last synchronisation, so it
      * is taken now (no host wait at the next call), and the device counters
      * are cleared for the next chunk behind the rounds */

@@ -34,9 +34,10 @@ def kname(full: str, grid: int = 0) -> str:
             args = parts[2].split(",")
             tag = net.get(args[6].strip(), "gen") if len(args) > 6 else "gen"
         short = f"{short}[{tag}]"
-    # fe_kernel<MODE>: 0 batch, 1 shared (cascade), 2 cold (cascade rounds)
-    if short == "fe_kernel":
-        mode = base.split("<", 1)[1].split(">")[0].strip() if "<" in base else ""
+    # fe_kernel<MODE, PORT> / fe_kernel2<MODE, PORT> (two frames per wave):
+    # MODE 0 batch, 1 shared (cascade), 2 cold (cascade rounds)
+    if short in ("fe_kernel", "fe_kernel2"):
+        mode = base.split("<", 1)[1].split(">")[0].split(",")[0].strip() if "<" in base else ""
         return {"0": "fe_kernel[batch]", "1": "fe_kernel[shared]", "2": "fe_kernel[cold]"}.get(mode, short)
     return short
 

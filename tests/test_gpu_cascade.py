@@ -11,7 +11,7 @@ import ctypes as C
 import numpy as np
 import pytest
 
-from oracle import OracleCascade, OracleNet, lib, synthetic_pcm
+from oracle import OracleCascade, OracleNet, lib, load_wavs, synthetic_pcm
 
 from nnsp_amd.engine import NNSPBatch, NNSPCascade
 from nnsp_amd.nets import synth_net
@@ -177,4 +177,28 @@ def test_cascade_lookahead_front_end(weights):
         np.testing.assert_array_equal(g_det, o_det, err_msg=f"detected chunk {i}")
         np.testing.assert_array_equal(g_o3, o_o3, err_msg=f"outputs3 chunk {i}")
         t0 += Tc
+    gc.close()
+
+
+def test_stats_right_after_exec_device():
+    """The statistics getters may be called right after an asynchronous
+    exec_device, with the chunk's tail work still queued (no sync): they must
+    return, not report a not-ready event (bench.py reads them that way), and
+    the per-net frame counts must add up to the chunk's frames at least."""
+    import torch
+    from nnsp_amd.nets import ref_net
+    S, T = 256, 100
+    gnets = {n: NNSPBatch(ref_net(n), S, T) for n in ("vad", "kws", "s2i")}
+    gc = NNSPCascade(gnets)
+    pcm = torch.from_numpy(synthetic_pcm(S, 3 * T, wavs=load_wavs(), every=2)).cuda()
+    ran = torch.empty((S, T), dtype=torch.int8, device="cuda")
+    for i in range(3):
+        chunk = pcm[:, i * T:(i + 1) * T].contiguous()
+        gc.exec_device(chunk.data_ptr(), T, ran.data_ptr())
+        rounds, frames, ms = gc.last_stats()
+        assert rounds >= 1 and frames >= S * T and ms > 0
+        assert gc.fe_stats() >= 0
+        for n in ("vad", "kws", "s2i"):
+            gc.net_stats(n)
+    gc.sync()
     gc.close()
