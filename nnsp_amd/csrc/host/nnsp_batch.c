@@ -388,7 +388,9 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
             if (need < blocks) blocks = (int)need;
         }
-        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
+        if (seg->phase != 2) TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
+        if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
+        if (seg->phase == 1) return 0;
         for (int i = 0; i < 2; ++i)
             if (seg->recur_wait[i]) TRY(nnspk_stream_wait(stream, seg->recur_wait[i]));
         f.a_off = b->rec_a_off;

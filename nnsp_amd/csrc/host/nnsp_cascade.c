@@ -91,6 +91,8 @@ struct nnsp_cascade {
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
+    void *ev_pj[3];                 /* per net: its proj of the round done (proj join) */
+    int proj_join;                  /* rounds < proj_join: every net's recur waits for all three projs */
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
@@ -235,7 +237,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
          * hardware queues (HIP's default) the look-ahead front end on
          * c->stream never shares an in-order queue with a net's rounds */
         c->ns[n] = nets[n]->stream;   /* per chunk: own_ns[n] when partitioned */
-        if ((e = nnspk_event_create(&c->ev_join[n])) ||
+        if ((e = nnspk_event_create(&c->ev_join[n])) || (e = nnspk_event_create(&c->ev_pj[n])) ||
             (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
             goto fail;
         for (int r = 0; r < MAX_TIMED; ++r)
@@ -346,6 +348,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->ahead_after = aa ? atoi(aa) : (c->part ? 0 : 1);
         const char *cf = getenv("NNSP_COLD_FIRST");
         c->cold_first = cf ? atoi(cf) != 0 : 0;   /* measured: +1 % reference nets, -5 % synthetic */
+        const char *pj = getenv("NNSP_PROJ_JOIN");
+        c->proj_join = pj ? atoi(pj) : 0;
         const char *vl = getenv("NNSP_VAD_LAST");
         c->vad_last = vl ? atoi(vl) != 0 : 0;   /* measured: -2 % reference nets, -7 % synthetic */
         const char *w = getenv("NNSP_CASCADE_WINDOW");
@@ -385,6 +389,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     }
     for (int n = 0; n < 3; ++n) {
         nnspk_event_destroy(c->ev_join[n]);
+        nnspk_event_destroy(c->ev_pj[n]);
         nnspk_event_destroy(c->ev_rnd[0][n]);
         nnspk_event_destroy(c->ev_rnd[1][n]);
         for (int r = 0; r < MAX_TIMED; ++r)
@@ -481,7 +486,7 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
 static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
-                    int wait_cold, void *const recur_wait[2])
+                    int wait_cold, void *const recur_wait[2], int phase)
 {
     const int timed = c->timing && r < MAX_TIMED;
     if (wait_cold)
@@ -507,7 +512,10 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
         seg.recur_wait[0] = recur_wait[0];
         seg.recur_wait[1] = recur_wait[1];
     }
+    seg.phase = phase;
+    if (phase == 1) seg.proj_done = c->ev_pj[n];
     TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
+    if (phase == 1) return 0;
     DBG(st, "proj + recur", n, r);
     if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
     if (c->fused) {
@@ -546,6 +554,8 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
     const int vad_last = c->fused && !c->serial && c->vad_last;
     static const int order_vad_last[3] = {0, 2, 1}, order_plain[3] = {0, 1, 2};
     const int *order = vad_last ? order_vad_last : order_plain;
+    /* proj join (NNSP_PROJ_JOIN=R: rounds < R): measured below */
+    const int pjoin = c->fused && !c->serial && !cold_first && !vad_last && r < c->proj_join;
     for (int i = 0; i < 3; ++i) {
         const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];
@@ -571,9 +581,19 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
                 w[0] = c->ev_rnd[r & 1][0];
                 w[1] = c->ev_rnd[r & 1][2];
             }
-            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w));
+            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w, pjoin ? 1 : 0));
         }
     }
+    if (pjoin)   /* every net's recur after all three projs of the round (they then run on a GPU of their own) */
+        for (int i = 0; i < 3; ++i) {
+            const int n = order[i];
+            void *st = c->ns[n];
+            void *w[2] = {NULL, NULL};
+            int k = 0;
+            for (int m = 0; m < 3; ++m)
+                if (m != n) w[k++] = c->ev_pj[m];
+            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w, 2));
+        }
     if (cold_first)
         for (int i = 0; i < 3; ++i) {
             const int n = order[i];
@@ -582,7 +602,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
                 w[0] = c->ev_rnd[r & 1][0];
                 w[1] = c->ev_rnd[r & 1][2];
             }
-            TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1, w));
+            TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1, w, 0));
         }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);

@@ -92,6 +92,8 @@ typedef struct {
     int net_id;
     const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
     void *recur_wait[2];       /* events the stream waits for between proj and recur (NULL: none) */
+    int phase;                 /* split path: 0 proj + recur, 1 proj only, 2 recur only */
+    void *proj_done;           /* non-NULL: recorded on the stream after proj */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
