@@ -120,7 +120,8 @@ def native_oracle() -> tuple[str | None, str]:
         return None, "prebuilt oracle/liboracle.so (-O3; gcc -march=native build unavailable)"
 
 
-def cpu_baseline(net: str, acc32: bool, weights: str, mix: bool, seconds: float, procs: int | None = None) -> dict:
+def cpu_baseline(net: str, acc32: bool, weights: str, mix: bool, seconds: float, procs: int | None = None,
+                 portable: bool = False) -> dict:
     """The C oracle timed on the host cores, one process per core (the
     reference library keeps global scratch and is not re-entrant, so it scales
     by processes -- SURVEY 8(d))."""
@@ -130,18 +131,19 @@ def cpu_baseline(net: str, acc32: bool, weights: str, mix: bool, seconds: float,
     procs = procs or cpu["usable_cores"]
     lib, flags = native_oracle()
     with mp.get_context("fork").Pool(procs) as pool:
-        res = pool.starmap(_cpu_worker, [(net, acc32, weights, mix, seconds, i, lib) for i in range(procs)])
+        res = pool.starmap(_cpu_worker, [(net, acc32, weights, mix, seconds, i, lib, portable) for i in range(procs)])
     rate = sum(f / t for f, t in res)   # the processes run concurrently: their rates add
     return {"value": rate, "unit": "frames/s", "cores": procs, "kind": "port",
             "cpu_model": cpu["model"], "host_cores": cpu["host_cores"], "quota": cpu["cgroup_or_env_quota"],
             "build": flags,
             "sample": f"{procs} concurrent processes x ~{seconds:.0f} s each of 32 continuous streams in 100-frame "
                       f"chunks (the bench's input mix and weights, inputs generated before the timed loop), "
-                      f"{net}, {'32' if acc32 else '64'}b accumulator; value = sum of per-process frames / timed s"}
+                      f"{net}, {'32' if acc32 else '64'}b accumulator"
+                      f"{', the ARM_OPTIMIZED=0 build' if portable else ''}; value = sum of per-process frames / timed s"}
 
 
 def _cpu_worker(net: str, acc32: bool, weights: str, mix: bool, seconds: float, idx: int,
-                lib: str | None) -> tuple[int, float]:
+                lib: str | None, portable: bool = False) -> tuple[int, float]:
     if lib:
         os.environ["NNSP_ORACLE_LIB"] = lib
     sys.path.insert(0, ROOT)
@@ -153,11 +155,12 @@ def _cpu_worker(net: str, acc32: bool, weights: str, mix: bool, seconds: float, 
     wavs = load_wavs() if mix else None
     S, T, NC = 32, 100, 16
     if net == "cascade":
-        orc = OracleCascade({n: OracleNet(get_net(n, weights), acc32=acc32) for n in ("vad", "kws", "s2i")})
+        orc = OracleCascade({n: OracleNet(get_net(n, weights), acc32=acc32, portable=portable, fe_portable=portable)
+                             for n in ("vad", "kws", "s2i")})
         st = orc.new_states(S)
         run = lambda pcm: orc.run(pcm, st)  # noqa: E731
     else:
-        orc = OracleNet(get_net(net, weights), acc32=acc32)
+        orc = OracleNet(get_net(net, weights), acc32=acc32, portable=portable, fe_portable=portable)
         st = orc.new_states(S)
         run = lambda pcm: orc.run(pcm, st, want_logits=False, want_feats=False)  # noqa: E731
     chunks = [synthetic_pcm(S, T, SEED, t0=c * T, s0=idx * S, amp=AMP, wavs=wavs) for c in range(NC)]
@@ -173,17 +176,18 @@ def _cpu_worker(net: str, acc32: bool, weights: str, mix: bool, seconds: float, 
 # ---------------------------------------------------------------------------
 # GPU run
 # ---------------------------------------------------------------------------
-def make_engine(net: str, S: int, T: int, acc32: bool, weights: str, window: int):
+def make_engine(net: str, S: int, T: int, acc32: bool, weights: str, window: int, arm_optimized: bool = True):
     from nnsp_amd.engine import NNSPBatch, NNSPCascade
     from nnsp_amd.nets import get_net
 
     if net == "cascade":
-        nets = {n: NNSPBatch(get_net(n, weights), S, T, acc32=acc32) for n in ("vad", "kws", "s2i")}
+        nets = {n: NNSPBatch(get_net(n, weights), S, T, acc32=acc32, arm_optimized=arm_optimized)
+                for n in ("vad", "kws", "s2i")}
         eng = NNSPCascade(nets)
         if window >= 0:
             eng.set_window(window)
         return eng
-    return NNSPBatch(get_net(net, weights), S, T, acc32=acc32)
+    return NNSPBatch(get_net(net, weights), S, T, acc32=acc32, arm_optimized=arm_optimized)
 
 
 def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
@@ -195,7 +199,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
 
     T, K, W = args.frames, args.steps, args.warmup
     cascade = args.net == "cascade"
-    eng = make_engine(args.net, S, T, args.acc32, weights, args.window)
+    eng = make_engine(args.net, S, T, args.acc32, weights, args.window, args.build == "shipped")
     dwav = None
     if args.input == "mix":
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -367,6 +371,8 @@ def main() -> None:
                     help="cascade: no look-ahead front end of the next chunk (overlapped with the nets)")
     ap.add_argument("--frames", type=int, default=100, help="frames per step (chunk)")
     ap.add_argument("--acc32", action="store_true")
+    ap.add_argument("--build", default="shipped", choices=["shipped", "portable"],
+                    help="the reference build reproduced: shipped (ARM_OPTIMIZED=1) or portable (ARM_OPTIMIZED=0, row N4)")
     ap.add_argument("--weights", default="ref", choices=["ref", "synth"])
     ap.add_argument("--input", default="mix", choices=["mix", "noise"])
     ap.add_argument("--no-stress", action="store_true",
@@ -406,7 +412,11 @@ def main() -> None:
                   "nn_ms": {n: r2["instrumented"][n]["nn_ms"] for n in ("vad", "kws", "s2i")}}
     if rank == 0:
         info = device_info()
-        dom, extra = roofline_blocks(args, res, info, load_profile(args, S, args.weights))
+        dom, extra = roofline_blocks(args, res, info,
+                                     load_profile(args, S, args.weights) if args.build == "shipped" else None)
+        if args.build == "portable":
+            dom["note"] = ("work counted as the shipped build's 5912 multiplies per frame; the portable FFT does 16 "
+                           "64-bit products per butterfly (fft.c) instead of 12 truncated ones; no PMC profile")
         value = frames / elapsed
         out = {
             "metric": "audio frames/sec (16 kHz, 10 ms hop) per node; bit-exact vs ref",
@@ -429,6 +439,7 @@ def main() -> None:
                        "streams_total": S * world if args.scaling == "weak" else args.total_streams,
                        "frames_per_step": args.frames, "accumulator": "32b" if args.acc32 else "64b",
                        "weights": args.weights, "input": args.input,
+                       "build": "ARM_OPTIMIZED=1 (shipped)" if args.build == "shipped" else "ARM_OPTIMIZED=0 (portable)",
                        "parallelism": f"stream shards x{world}" + (" (RCCL process group)" if dist else "")},
             "roofline": dom,
             **{f"roofline_{k}": v for k, v in extra.items()},
@@ -447,7 +458,7 @@ def main() -> None:
             out["nn_ms_per_step"] = res["nn_ms"]
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.net, args.acc32, args.weights, args.input == "mix",
-                                               args.cpu_seconds)
+                                               args.cpu_seconds, portable=args.build == "portable")
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()
