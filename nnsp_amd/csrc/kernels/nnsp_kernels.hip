@@ -346,9 +346,16 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     // t >= lim: nothing to do (past the chunk; COLD: past the segment or not
     // within 2 frames of the reset); z: COLD, input frames before z are zero
     struct Pos { unsigned i, k; int s, b, t, lim, z; };
+    // the shared front end runs every stream's whole chunk (no list, no
+    // segments, no look-back: the host never sets them for that mode)
     auto row_of = [&](Pos& p) {
-        p.s = a.list ? a.list[p.i] : (int)p.i;
-        p.b = a.seg_begin ? a.seg_begin[p.s] : 0;
+        if constexpr (shared) {
+            p.s = (int)p.i;
+            p.b = 0;
+        } else {
+            p.s = a.list ? a.list[p.i] : (int)p.i;
+            p.b = a.seg_begin ? a.seg_begin[p.s] : 0;
+        }
         p.lim = a.T;
         p.z = 0;
         if (cold) {
@@ -369,6 +376,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         } else if (fi < p.b) {
             return a.tail + (size_t)p.s * (a.tail_stride ? (unsigned)a.tail_stride : 320u) + (fi - p.b + 2) * 160;
         }
+        if constexpr (shared) return a.pcm + ((size_t)p.s * a.T + fi) * 160;
         const int x = fi - a.lookback;
         return x >= 0 ? a.pcm + ((size_t)p.s * a.T + x) * 160
                       : a.hist + ((size_t)p.s * a.hist_frames + a.hist_frames + x) * 160;
@@ -376,7 +384,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     // lane's window samples 128*m + 2*lane, +1 of frames t-2, t-1, t
     auto load_frame = [&](const Pos& p, uint32_t (&r)[4]) {
         const int o = 2 * lane;
-        const int x0 = p.t - 2 - a.lookback;
+        const int x0 = shared ? p.t - 2 : p.t - 2 - a.lookback;
         if (!cold && p.t - 2 >= p.b && x0 >= 0) {
             // common case (wave-uniform): frames t-2..t are consecutive in the
             // chunk, so the window is 480 contiguous samples from one pointer
