@@ -120,6 +120,20 @@ __device__ __forceinline__ void split_bin(int32_t xr, int32_t xi, int32_t yr, in
     im = wadd(wadd(rnd_add(xr, A2), rnd_add(xi, A1)), wadd(rnd_sub(yi, B1), rnd_sub(yr, A2)));
 }
 
+// Bins k and 256-k together (k in 1..128).  CMSIS's coefficients are
+// symmetric -- A1[256-k] = A1[k], A2[256-k] = -A2[k], B1[256-k] = B1[k] (checked
+// by tests/test_tables.py) -- and rnd_sub(x, -c) = rnd_add(x, c), so bin 256-k
+// is split_bin with x and y swapped and two of its eight rounded products,
+// xr*A2 (SMMLAR) and yr*A2 (SMMLSR), are bin k's own: 14 products per pair.
+__device__ __forceinline__ void split_pair(int32_t xr, int32_t xi, int32_t yr, int32_t yi, int32_t A1, int32_t A2,
+                                           int32_t B1, int32_t& re0, int32_t& im0, int32_t& re1, int32_t& im1) {
+    const int32_t xa2 = rnd_add(xr, A2), ya2 = rnd_sub(yr, A2);
+    re0 = wadd(wadd(rnd_add(xr, A1), rnd_sub(xi, A2)), wadd(rnd_sub(yi, A2), rnd_add(yr, B1)));
+    im0 = wadd(wadd(xa2, rnd_add(xi, A1)), wadd(rnd_sub(yi, B1), ya2));
+    re1 = wadd(wadd(rnd_add(yr, A1), rnd_add(yi, A2)), wadd(rnd_add(xi, A2), rnd_add(xr, B1)));
+    im1 = wadd(wadd(ya2, rnd_add(yi, A1)), wadd(rnd_sub(xi, B1), xa2));
+}
+
 // spec2pspec_arm (spectrogram_module.c:79-92): truncating cast of (re^2+im^2)>>27
 __device__ __forceinline__ int32_t pspec_of(int32_t re, int32_t im) {
     return (int32_t)(((int64_t)re * re + (int64_t)im * im) >> 27);

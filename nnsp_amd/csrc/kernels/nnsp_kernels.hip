@@ -289,6 +289,17 @@ __device__ __forceinline__ void wave_split_bin(const int32_t* X, const FeTables&
         split_bin(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re, im);
 }
 
+// The shipped split of bins k = lane + 64 pr + 1 and 256 - k (pr = 0, 1:
+// every bin 1..255 once, bin 128 twice) from one pair of LDS reads.
+__device__ __forceinline__ void wave_split_pair(const int32_t* X, const FeTables& TB, int lane, int pr, int& k,
+                                                int32_t& re0, int32_t& im0, int32_t& re1, int32_t& im1) {
+    k = lane + 64 * pr + 1;
+    const int4 cf = TB.split[k];
+    const int2 zk = *reinterpret_cast<const int2*>(X + 2 * zslot(k));
+    const int2 zn = *reinterpret_cast<const int2*>(X + 2 * zslot(256 - k));
+    split_pair(zk.x, zk.y, zn.x, zn.y, cf.x, cf.y, cf.z, re0, im0, re1, im1);
+}
+
 // DC and Nyquist bins: (p0 + p1) >> 1, (p0 - p1) >> 1 (arm_split_rfft_q31 tail)
 __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int32_t& nyq) {
     const int2 z0 = *reinterpret_cast<const int2*>(X);
@@ -497,8 +508,25 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         wave_cfft256<PORT>(v, X, TB, lane);
         FCLK(2);
         // ---- split + power (arm_split_rfft_q31, spec2pspec_arm)
+        if (!PORT) {
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+            for (int pr = 0; pr < 2; ++pr) {
+                int k;
+                int32_t re0, im0, re1, im1;
+                wave_split_pair(X, TB, lane, pr, k, re0, im0, re1, im1);
+                P[k] = pspec_of(re0, im0);
+                P[256 - k] = pspec_of(re1, im1);
+                if (MODE == FE_MODE_BATCH && a.dbg_spec) {
+                    int32_t* ds = a.dbg_spec + (size_t)fo * 1024;
+                    ds[2 * k] = re0; ds[2 * k + 1] = im0;
+                    ds[1024 - 2 * k] = re0; ds[1024 - 2 * k + 1] = wsub(0, im0);
+                    ds[512 - 2 * k] = re1; ds[512 - 2 * k + 1] = im1;
+                    ds[512 + 2 * k] = re1; ds[512 + 2 * k + 1] = wsub(0, im1);
+                }
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < (PORT ? 4 : 0); ++m) {
             int32_t re, im;
             wave_split_bin<PORT>(X, TB, lane, m, re, im);
             P[lane + 64 * m] = PORT ? pspec15_of(re, im) : pspec_of(re, im);
@@ -830,8 +858,21 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
         flush1(pendA, poA, pvA, p2A);
         flush1(pendB, poB, pvB, p2B);
         wave_cfft256x2<PORT>(va, vb, XA, XB, TB, lane);
+        if (!PORT) {
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+            for (int pr = 0; pr < 2; ++pr) {
+                int k;
+                int32_t a0, a1, a2, a3, b0, b1, b2, b3;
+                wave_split_pair(XA, TB, lane, pr, k, a0, a1, a2, a3);
+                wave_split_pair(XB, TB, lane, pr, k, b0, b1, b2, b3);
+                PA[k] = pspec_of(a0, a1);
+                PA[256 - k] = pspec_of(a2, a3);
+                PB[k] = pspec_of(b0, b1);
+                PB[256 - k] = pspec_of(b2, b3);
+            }
+        }
+#pragma unroll
+        for (int m = 0; m < (PORT ? 4 : 0); ++m) {
             int32_t ra, ia, rb, ib;
             wave_split_bin<PORT>(XA, TB, lane, m, ra, ia);
             wave_split_bin<PORT>(XB, TB, lane, m, rb, ib);
