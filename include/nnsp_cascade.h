@@ -61,8 +61,9 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask);
  * finished on the device (its outputs are final): the host reads back the list
  * lengths of the round after the last one it launched to decide whether more
  * rounds are needed, so it cannot queue the next chunk while this one runs.
- * The chunk's bookkeeping (counter copy, the next chunk's STFT tail and
- * look-back history, a look-ahead front end) may still run on
+ * The chunk's counters come back with that read; its bookkeeping (clearing
+ * them, the next chunk's STFT tail and look-back history, a look-ahead front
+ * end) may still run on
  * nnsp_cascade_stream when it returns; the next call, the statistics getters,
  * nnsp_cascade_sync and nnsp_cascade_reset order themselves after it. */
 int nnsp_cascade_exec(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran,

@@ -125,6 +125,12 @@ __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, 
     for (int i = threadIdx.x; i < bytes / 16; i += blockDim.x) d[i] = s[i];
 }
 
+// Row tiles per load group of a compiled-shape FC layer: all of a layer's
+// tiles (up to FC_GROUP_MAX) in one group, so that its LDS loads and MFMA
+// chains overlap once instead of once per group of 3.
+#ifndef FC_GROUP_MAX
+#define FC_GROUP_MAX 3
+#endif
 // One FC layer on a 16-row tile: B from an LDS buffer (row stride in_stride),
 // A fragments from LDS, output to an LDS buffer (row stride out_stride).
 // NRT/NKT/ROWS > 0 and ACT >= 0 are compile-time; otherwise taken from Ly.
@@ -166,7 +172,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
         // store -- the compiler cannot move loads across stores into the same
         // LDS, so a per-tile load/compute/store order would expose the full
         // latency per tile; groups of <= 3 tiles bound the registers
-        constexpr int CH = NRT < 3 ? NRT : 3;
+        constexpr int CH = NRT <= FC_GROUP_MAX ? NRT : 3;
 #pragma unroll
         for (int r0 = 0; r0 < NRT; r0 += CH) {
             v4i w[CH][NKT];

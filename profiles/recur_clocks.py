@@ -17,7 +17,11 @@ net = sys.argv[1] if len(sys.argv) > 1 else "vad"
 S = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 T = 100
 torch.cuda.set_device(0)
-eng = NNSPBatch(net, S, T)
+if len(sys.argv) > 3 and sys.argv[3] == "ref":   # the reference's own tables (ref_nets.npz)
+    from nnsp_amd.nets import ref_net  # noqa: E402
+    eng = NNSPBatch(ref_net(net), S, T)
+else:
+    eng = NNSPBatch(net, S, T)
 pcm = torch.empty((S, T, 160), dtype=torch.int16, device="cuda")
 trig = torch.empty((S, T), dtype=torch.int16, device="cuda")
 L = _lib.lib()
