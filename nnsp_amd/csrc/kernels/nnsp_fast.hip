@@ -134,7 +134,12 @@ __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, 
 // One FC layer on a 16-row tile: B from an LDS buffer (row stride in_stride),
 // A fragments from LDS, output to an LDS buffer (row stride out_stride).
 // NRT/NKT/ROWS > 0 and ACT >= 0 are compile-time; otherwise taken from Ly.
-template <bool ACC32, int NRT, int NKT, int ACT, int ROWS, int MAXKT>
+// PAD (compiled shapes): also compute and store the padding rows of the last
+// row tile (rows .. 16 NRT - 1; their epilogue constants are zero), so that no
+// output store sits behind a lane-dependent branch.  Only for outputs whose
+// row stride holds 16 NRT values and whose padding only ever meets zero A
+// columns of the next layer (recur's stage buffers).
+template <bool ACC32, int NRT, int NKT, int ACT, int ROWS, int MAXKT, bool PAD = false>
 __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, const EpRow* ep, const int16_t* in,
                                          int in_stride, int16_t* out, int out_stride, const int16_t* tt, int lane) {
     const int nrt = NRT > 0 ? NRT : Ly.nrt;
@@ -187,7 +192,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
                         const int row = 16 * rt + 4 * q + i;
-                        cst[c][i] = row < rows ? ep_cst<ACC32>(ep[row]) : 0;
+                        cst[c][i] = (PAD || row < rows) ? ep_cst<ACC32>(ep[row]) : 0;
                     }
                 }
             }
@@ -208,7 +213,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     const int row = 16 * (r0 + c) + 4 * q + i;
-                    if (r0 + c < NRT && row < rows) {
+                    if (r0 + c < NRT && (PAD || row < rows)) {
                         const int32_t v = ep_out<ACC32>((ah[c][i] << 8) + al[c][i], cst[c][i], rsh, lsh);
                         if (act == ACT_LINEAR)
                             reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
@@ -838,6 +843,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     using PT = PipeTile<SH>;
     constexpr int RGP = CF::LW, RPW = CF::RPW, RS = PT::RS;
     constexpr int N = SH::NW, nrt = SH::NRT, nkt_r = SH::NKR;
+    // the FC stages store their padding rows too (fc_layer<..., PAD>): the
+    // rows must fit a stage buffer's row (int32 logits: two int16 each)
+    static_assert(16 * SH::R1 <= RS && 16 * SH::R2 <= RS && 32 * SH::R3 <= RS, "padded FC rows exceed RS");
     const bool ctl = ca.st != nullptr;
     // the round after next appends to counts_clear: zero it (every net's recur
     // does; nothing reads or appends to it during this round)
@@ -1088,19 +1096,19 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             }
         } else if constexpr (role == 1) {   // stage 1: step j-1
             if (j >= 1 && j - 1 < nsteps)
-                fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
+                fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
                     L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
                     RS, tt, lane);
             if (!SPL) flush(cur ^ 1);
         } else if constexpr (role == 2) {   // stage 2: step j-2
             if (j >= 2 && j - 2 < nsteps)
-                fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR>(
+                fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
                     L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                     &R.a3[cur][0][0], RS, tt, lane);
             if (!SPL) flush(cur ^ 1);
         } else if constexpr (role == 3) {   // stage 3 (split): step j-3
             if (j >= 3 && j - 3 < nsteps)
-                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
+                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
                     L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                     &R.a4[cur][0][0], RS, tt, lane);
             flush(cur ^ 1);   // the post wave's outputs of the previous iteration
@@ -1112,7 +1120,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             t = b + 2 * jj + phase;
             const bool active = valid && t < e;
             if (!SPL) {   // the last FC layer on this wave too
-                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR>(
+                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
                     L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                     &R.a4[cur][0][0], RS, tt, lane);
                 wave_lds_sync();
