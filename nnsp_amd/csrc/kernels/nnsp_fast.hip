@@ -208,19 +208,40 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
                         al[c] = mfma8(w[c][kt], bl[kt], al[c]);
                     }
             }
+            // int32 accumulators without a left shift (every int32 kernel of
+            // the reference nets): shift_32b is a plain arithmetic shift, so
+            // no per-value select between the two shift forms
+            const int rsh3 = min(rsh + 3, 31);   // (v >> rsh) >> 3 == v >> min(rsh + 3, 31)
+            auto epilogue = [&](auto nolsh) {
 #pragma unroll
-            for (int c = 0; c < CH; ++c)
+                for (int c = 0; c < CH; ++c)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const int row = 16 * (r0 + c) + 4 * q + i;
-                    if (r0 + c < NRT && (PAD || row < rows)) {
-                        const int32_t v = ep_out<ACC32>((ah[c][i] << 8) + al[c][i], cst[c][i], rsh, lsh);
-                        if (act == ACT_LINEAR)
-                            reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
-                        else
-                            out[sc * out_stride + row] = act16(act, v, tt);
+                    for (int i = 0; i < 4; ++i) {
+                        const int row = 16 * (r0 + c) + 4 * q + i;
+                        if (r0 + c < NRT && (PAD || row < rows)) {
+                            const int32_t acc = (ah[c][i] << 8) + al[c][i];
+                            int32_t v;
+                            if constexpr (decltype(nolsh)::value) {
+                                if (act == ACT_RELU6) {   // relu6_q12's >> 3 folded into the layer shift
+                                    const int32_t u = wadd(acc, (int32_t)cst[c][i]) >> rsh3;
+                                    out[sc * out_stride + row] = (int16_t)min(max(u, 0), 24576);
+                                    continue;
+                                }
+                                v = wadd(acc, (int32_t)cst[c][i]) >> rsh;
+                            } else {
+                                v = ep_out<ACC32>(acc, cst[c][i], rsh, lsh);
+                            }
+                            if (act == ACT_LINEAR)
+                                reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
+                            else
+                                out[sc * out_stride + row] = act16(act, v, tt);
+                        }
                     }
-                }
+            };
+            if (ACC32 && lsh == 0)
+                epilogue(std::true_type{});
+            else
+                epilogue(std::false_type{});
         }
     } else if constexpr (NRT > 0) {
 #pragma unroll
@@ -989,8 +1010,13 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     const NnLayer& L4 = img.L[r.li + 3];
     // development probe (NNSP_RECUR_CLOCKS): s_memtime at the start and end of each
     // iteration's work of LSTM wave 0 and the three stage waves, tile 0
-    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && sub == 0 && lane == 0 && (g == 0 || g >= RGP))
-                         ? r.dbg_clk + 2 * (g == 0 ? 0 : g - RGP + 1)
+    // (RECUR_CLK_WAVE: which LSTM wave records into slots 0-1; development)
+#ifndef RECUR_CLK_WAVE
+#define RECUR_CLK_WAVE 0
+#endif
+    constexpr int CLKW = RECUR_CLK_WAVE < RGP ? RECUR_CLK_WAVE : 0;
+    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && sub == 0 && lane == 0 && (g == CLKW || g >= RGP))
+                         ? r.dbg_clk + 2 * (g == CLKW ? 0 : g - RGP + 1)
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the
     // loop runs two iterations per trip), so every LDS access of the stages
@@ -998,7 +1024,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // parity cost the S2I post wave ~1100 of its ~6000 cycles per step
     // LSTM wave 0's sub-phases (dbg_clk[1536 + 8 j + k]): loads + MFMA, gates, stores, x_half, load_x
     // (in time order 0, 3, 4, 1, 2)
-    long long* lclk = (clk && g == 0) ? r.dbg_clk + 1536 : nullptr;
+    long long* lclk = (clk && g == CLKW) ? r.dbg_clk + 1536 : nullptr;
 #define LCLK(k) \
     if (lclk && j < 64) lclk[8 * j + (k)] = (long long)__builtin_amdgcn_s_memtime()
     auto iteration = [&](const int j, auto CUR, auto RL) {
@@ -1058,30 +1084,45 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 LCLK(4);
                 int32_t c_new[RPW];
                 int16_t hv[RPW];
+                // (nolsh: int32 accumulators, no left shift -- as fc_layer)
+                const int rsh1 = min(rsh + 1, 31);   // (v >> rsh) >> 1 == v >> min(rsh + 1, 31)
+                auto gates = [&](auto nolsh) {
 #pragma unroll
-                for (int k = 0; k < RPW; ++k) {
-                    const int rt = g + RGP * k;
-                    c_new[k] = 0;
-                    hv[k] = 0;
-                    if (rt < nrt && 4 * rt + q < N) {
-                        int16_t gt[4];
+                    for (int k = 0; k < RPW; ++k) {
+                        const int rt = g + RGP * k;
+                        c_new[k] = 0;
+                        hv[k] = 0;
+                        if (rt < nrt && 4 * rt + q < N) {
+                            int16_t gt[4];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            // exact Wx.x + Wh.h (|.| < 2^31 for N <= 128: int32)
-                            const int32_t hx = (hh[k][i] << 8) + hl[k][i];
-                            int32_t v;
-                            if (ACC32) {
-                                v = ep_out<true>(hx, cst[k][i], rsh, lsh);
-                            } else {
-                                const int64_t pre = (int64_t)hx + cst[k][i];
-                                v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
+                            for (int i = 0; i < 4; ++i) {
+                                // exact Wx.x + Wh.h (|.| < 2^31 for N <= 128: int32)
+                                const int32_t hx = (hh[k][i] << 8) + hl[k][i];
+                                int32_t v;
+                                if constexpr (decltype(nolsh)::value) {
+                                    const int32_t u = wadd(hx, (int32_t)cst[k][i]);
+                                    if (i != 1) {   // sigmoid_q15's >> 1 folded into the layer shift
+                                        gt[i] = (int16_t)((tanh_q15(u >> rsh1, tt) >> 1) + 16384);
+                                        continue;
+                                    }
+                                    v = u >> rsh;
+                                } else if (ACC32) {
+                                    v = ep_out<true>(hx, cst[k][i], rsh, lsh);
+                                } else {
+                                    const int64_t pre = (int64_t)hx + cst[k][i];
+                                    v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
+                                }
+                                gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
                             }
-                            gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                            c_new[k] = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old[k]) >> 15);
+                            hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
                         }
-                        c_new[k] = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old[k]) >> 15);
-                        hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
                     }
-                }
+                };
+                if (ACC32 && lsh == 0)
+                    gates(std::true_type{});
+                else
+                    gates(std::false_type{});
                 LCLK(1);
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
