@@ -35,6 +35,17 @@ __device__ __forceinline__ int64_t mad_i64_i32(int32_t a, int32_t b, int64_t acc
     return r;
 }
 
+// sat32(((int64)a * b + (int64)c * d) >> 15) for int16 a, b, c and int32 d
+// (lstm.c's cell update): one v_mad_i64_i32, the shifted low word from one
+// funnel shift, and the range check on the high word in 32-bit compares
+// (|x| < 2^47: x >> 15 fits int32 iff x >> 46 is 0 or -1)
+__device__ __forceinline__ int32_t cell_q15(int32_t a, int32_t b, int32_t c, int32_t d) {
+    const int64_t x = mad_i64_i32(c, d, (int64_t)(a * b));
+    const int32_t hi = (int32_t)(x >> 32);
+    const int32_t y = (int32_t)__builtin_amdgcn_alignbit((uint32_t)hi, (uint32_t)x, 15);
+    return (uint32_t)((hi >> 14) + 1) < 2u ? y : ((hi >> 31) ^ INT32_MAX);
+}
+
 // SMMLAR / SMMULR contribution: floor((x*c + 2^31) / 2^32)
 __device__ __forceinline__ int32_t rnd_add(int32_t x, int32_t c) {
     return (int32_t)(((int64_t)x * c + 0x80000000LL) >> 32);

@@ -1114,7 +1114,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                 }
                                 gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
                             }
-                            c_new[k] = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old[k]) >> 15);
+                            c_new[k] = cell_q15(gt[0], gt[1], gt[2], c_old[k]);
                             hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
                         }
                     }
