@@ -1,0 +1,37 @@
+"""The range check of nnsp_dev.h's cell_q15 (recur_pipe_kernel's LSTM cell
+update, lstm.c's sat32((i*g + f*c) >> 15)) restated in numpy and checked
+against the plain 64-bit saturating form over the operand extremes: the
+kernel tests the high word only (x >> 15 fits int32 iff x >> 46 is 0 or -1,
+for |x| < 2^47) and takes the low word from a funnel shift."""
+import numpy as np
+
+
+def _sat32_ref(x):
+    return np.clip(x >> 15, -2**31, 2**31 - 1)
+
+
+def _cell_q15(x):
+    hi = (x >> 32).astype(np.int64)            # the high word, arithmetic
+    y = ((x >> 15) & 0xFFFFFFFF).astype(np.int64)
+    y = np.where(y >= 2**31, y - 2**32, y)     # alignbit(hi, lo, 15) as int32
+    fits = (((hi >> 14) + 1) & 0xFFFFFFFF) < 2
+    sat = np.where(hi < 0, -2**31, 2**31 - 1)
+    return np.where(fits, y, sat)
+
+
+def test_cell_q15_matches_sat32_at_the_extremes():
+    g = np.array([-32768, -32767, -16384, -1, 0, 1, 16384, 32767], np.int64)
+    c = np.array([-2**31, -2**31 + 1, -2**30, -65536, -32768, -1, 0, 1, 32767, 65536, 2**30,
+                  2**31 - 2, 2**31 - 1], np.int64)
+    a, b, f, cc = np.meshgrid(g, g, g, c, indexing="ij")
+    x = a * b + f * cc
+    np.testing.assert_array_equal(_cell_q15(x.ravel()), _sat32_ref(x.ravel()))
+
+
+def test_cell_q15_matches_sat32_random():
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    a, b, f = (rng.integers(-32768, 32768, n) for _ in range(3))
+    cc = rng.integers(-2**31, 2**31, n)
+    x = a * b + f * cc
+    np.testing.assert_array_equal(_cell_q15(x), _sat32_ref(x))
