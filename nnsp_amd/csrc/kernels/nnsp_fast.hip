@@ -442,17 +442,27 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                                                           in, in_stride, &P.act[0][0][0], PW::AS, tt, lane);
             wave_lds_sync();
             PCLK(2);
-            // ---- the LSTM's input x of every row to HBM (int16, xs per row;
-            //      columns N..xs-1 are the zeros set at kernel start)
-            constexpr int XC = SH::XS / 8;   // 16-byte chunks per row
+            // ---- the LSTM's input x of every row to HBM, already in the MFMA
+            //      B operand's split form (split_hilo): per row xs high bytes,
+            //      then xs low bytes ^ 0x80 (columns N..xs-1: the zeros set at
+            //      kernel start) -- split here once instead of by each of
+            //      recur's LSTM waves every step
+            constexpr int XC = SH::XS / 8;   // 8-element chunks per row
             for (int c = lane; c < 16 * XC; c += 64) {
                 const int row = c / XC, part = c - row * XC;
                 const int kx = row / SPT, jx = row - kx * SPT;
                 const Seg g = seg_k(kx);
                 const int j = j0 + jx;
-                if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L)
-                    *reinterpret_cast<int4*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS + 8 * part) =
-                        *reinterpret_cast<const int4*>(&P.act[0][row][8 * part]);
+                if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L) {
+                    const int4 v = *reinterpret_cast<const int4*>(&P.act[0][row][8 * part]);
+                    uint8_t* dst = reinterpret_cast<uint8_t*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS) + 8 * part;
+                    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
+                    *reinterpret_cast<uint2*>(dst) = make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, HS),
+                                                                __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, HS));
+                    *reinterpret_cast<uint2*>(dst + SH::XS) =
+                        make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, LS) ^ 0x80808080u,
+                                   __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, LS) ^ 0x80808080u);
+                }
             }
             wave_lds_sync();
             PCLK(3);
@@ -955,24 +965,28 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // The loads land in xr untouched (lanes past the row read column 0 of it)
     // and x_half zeroes those lanes: any use of a load result right after it
     // (a select, a copy) made the wave wait the full load latency every step.
-    auto load_x = [&](int jj) {   // raw x of step jj for the lane's stream (B-fragment layout)
+    auto load_x = [&](int jj) {   // split x of step jj for the lane's stream (B fragments: high, low bytes)
         const bool ok = valid && b + 2 * jj + phase < e;
-        const int16_t* src = r.xg + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * XS;
+        const uint8_t* src =
+            reinterpret_cast<const uint8_t*>(r.xg + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * XS);
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
             const int k0 = 64 * kt + 16 * q;
-            const int16_t* p = src + (k0 < XS ? k0 : 0);
+            const uint8_t* p = src + (k0 < XS ? k0 : 0);
             xr[kt][0] = *reinterpret_cast<const int4*>(p);
-            xr[kt][1] = *reinterpret_cast<const int4*>(p + 8);
+            xr[kt][1] = *reinterpret_cast<const int4*>(p + XS);
         }
     };
     auto x_half = [&]() {   // axh/axl := Wx . x (hi / lo planes) from xr
         v4i bxh[nkt_r], bxl[nkt_r];
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
+            // (past xs: the split of zeros; the A columns there are zero too)
             const bool in = 64 * kt + 16 * q < XS;
-            const int4 z = make_int4(0, 0, 0, 0);
-            split_hilo_r(in ? xr[kt][0] : z, in ? xr[kt][1] : z, bxh[kt], bxl[kt]);
+            const int4 h = in ? xr[kt][0] : make_int4(0, 0, 0, 0);
+            const int4 l = in ? xr[kt][1] : make_int4(0x80808080, 0x80808080, 0x80808080, 0x80808080);
+            bxh[kt] = v4i{h.x, h.y, h.z, h.w};
+            bxl[kt] = v4i{l.x, l.y, l.z, l.w};
         }
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {   // one row tile's fragments at a time (no LDS stores here)
