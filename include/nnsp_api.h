@@ -164,12 +164,40 @@ int stftModule_setDefault(stftModule *ps);
 void spec2pspec_arm(int32_t *y, int32_t *x, int len);
 int stftModule_analyze_arm(void *ps, int16_t *x, int32_t *y);
 /* the ARM_OPTIMIZED=0 build's stages (spectrogram_module.c:33-77, fft.h:4-5);
- * exported beside the shipped ones.  rfft: num_rfft 512 only (y: 257
- * complex); fft: exp_nfft 8 only (in place on its input, like fft.c) */
+ * exported beside the shipped ones.  rfft: num_rfft 256 or 512 (y: num_rfft/2
+ * + 1 complex); fft: exp_nfft 0..8 (in place on its input, like fft.c) -- the
+ * sizes fft.c's twiddle and bit-reversal tables serve; others return with
+ * nnsp_legacy_status() = NNSP_EUNSUPPORTED */
 void spec2pspec(int32_t *y, int32_t *x, int len);
 int stftModule_analyze(stftModule *ps, int16_t *x, int32_t *y);
 void rfft(int num_rfft, int32_t *input, void *output_);
 void fft(int exp_nfft, void *input_, void *output_);
+
+/* complex.h (the ARM_OPTIMIZED=0 build's complex helpers, complex.c):
+ * int64 products with int32 clamps where complex.c has them, int32 wrap
+ * elsewhere.  complex32_sub negates *b in place, as complex.c:108-113 does. */
+typedef struct {
+    int32_t real;
+    int32_t imag;
+} COMPLEX32;
+typedef struct {
+    int16_t real;
+    int16_t imag;
+} COMPLEX16;
+void complex32_copy(COMPLEX32 *dst, COMPLEX32 *src);
+void complex32_affine(COMPLEX32 *out, COMPLEX32 *Mat, COMPLEX32 *input, int shift_r, int len);
+void complex32_interprod(COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX32 *arry2, int shift_r, int len);
+void complex32_complex16_elmtprod(COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX16 *arry2, int len);
+void complex32_add(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2);
+void complexArry32_add(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2, int len);
+void complex32_neg(COMPLEX32 *out, COMPLEX32 *in);
+void complex32_sub(COMPLEX32 *out, COMPLEX32 *a, COMPLEX32 *b);
+void complex32_mul(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2);
+void complex32_init(COMPLEX32 *inst, int32_t real, int32_t imag);
+void complex32_real2cmplx(COMPLEX32 *inst, int32_t real);
+void complexArry32_real2cmplx(COMPLEX32 *inst, int32_t *real, int32_t len);
+void complexArry32_init(COMPLEX32 *inst, int32_t *real, int32_t *imag, int len);
+void complexArry32_print(COMPLEX32 *inst, int len);
 
 typedef struct {
     stftModule state_stftModule;

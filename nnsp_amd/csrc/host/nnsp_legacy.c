@@ -29,7 +29,9 @@
  * ------------------------------------------------------------------------- */
 static struct {
     void *stream;
-    uint8_t *arena, *retired;
+    uint8_t *arena;
+    uint8_t *retired[8]; /* arenas outgrown during the current call (their pointers may be live) */
+    int n_retired;
     size_t cap, used;
     int ready;
     int depth;   /* nesting of public entry points (the outermost holds jb) */
@@ -93,17 +95,16 @@ static void *dscratch(size_t n)
 {
     n = (n + 255) & ~(size_t)255;
     if (G.used + n > G.cap) {
-        /* grow: pointers handed out earlier in this call stay valid (the old
-         * arena is retired, freed by the next begin()) */
+        /* grow: pointers handed out earlier in this call stay valid -- every
+         * outgrown arena of the call is retired, and all of them are freed by
+         * the next begin(), after the call's synchronisation */
+        if (G.n_retired == (int)(sizeof G.retired / sizeof G.retired[0]))
+            fail(NNSP_ENOMEM, "legacy scratch: too many arena growths in one call");
         size_t cap = G.cap * 2;
         while (cap < n) cap *= 2;
         uint8_t *a = NULL;
         CK(nnspk_malloc((void **)&a, cap));
-        if (G.retired) {   /* a second growth in one call: keep the older arena alive too */
-            CK(nnspk_sync(G.stream));
-            nnspk_free(G.retired);
-        }
-        G.retired = G.arena;
+        G.retired[G.n_retired++] = G.arena;
         G.arena = a;
         G.cap = cap;
         G.used = 0;
@@ -118,9 +119,12 @@ const char *nnsp_strerror(int code);
 static void begin(void)
 {
     CK(gctx());
-    if (G.retired) { /* the previous call synchronised: nothing uses it any more */
-        nnspk_free(G.retired);
-        G.retired = NULL;
+    /* the previous call synchronised (fin) or failed after a sync-free
+     * launch error: wait for the stream, then nothing uses the old arenas */
+    if (G.n_retired) {
+        nnspk_sync(G.stream);
+        for (int i = 0; i < G.n_retired; ++i) nnspk_free(G.retired[i]);
+        G.n_retired = 0;
     }
     G.used = 0;
 }
@@ -530,7 +534,7 @@ static void spec2pspec_arm_impl(int32_t *y, int32_t *x, int len) /* :79-92 */
     if (len <= 0) return;
     begin();
     int32_t *dx = (int32_t *)up(x, (size_t)2 * len * 4);
-    int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
+    int32_t *dy = (int32_t *)up(NULL, (size_t)len * 4);   /* one vector: any len */
     CK(nnspk_launch_pspec(dy, dx, len, 1, 27, G.stream));
     down(y, dy, (size_t)len * 4);
     fin();
@@ -552,10 +556,9 @@ static int stftModule_analyze_impl(stftModule *ps, int16_t *x, int32_t *y) /* sp
 static void spec2pspec_impl(int32_t *y, int32_t *x, int len) /* spectrogram_module.c:33-45 */
 {
     if (len <= 0) return;
-    if (len > 1024) fail(NNSP_EINVAL, "spec2pspec: len > 1024");
     begin();
     int32_t *dx = (int32_t *)up(x, (size_t)2 * len * 4);
-    int32_t *dy = (int32_t *)up(NULL, 1024 * 4);
+    int32_t *dy = (int32_t *)up(NULL, (size_t)len * 4);   /* one vector: any len */
     CK(nnspk_launch_pspec(dy, dx, len, 1, 15, G.stream));
     down(y, dy, (size_t)len * 4);
     fin();
@@ -563,34 +566,102 @@ static void spec2pspec_impl(int32_t *y, int32_t *x, int len) /* spectrogram_modu
 
 static void rfft_impl(int num_rfft, int32_t *input, void *output) /* fft.c:27-126 */
 {
-    if (num_rfft != 512) fail(NNSP_EUNSUPPORTED, "rfft: only num_rfft = 512 (the front end's) is supported");
+    /* the reference's twiddle and bit-reversal tables serve 256 and 512
+     * points; for other sizes it reads past them (rfft: R = 256, fft: 2^0) */
+    if (num_rfft != 512 && num_rfft != 256)
+        fail(NNSP_EUNSUPPORTED, "rfft: num_rfft must be 256 or 512 (the sizes fft.c's tables serve)");
+    const int e = num_rfft == 512 ? 8 : 7;
     begin();
-    int32_t *dx = (int32_t *)up(input, 512 * 4);
-    int32_t *dy = (int32_t *)up(NULL, 514 * 4);
-    CK(nnspk_launch_rfft_port(dx, dy, 1, 0, G.stream));
-    down(output, dy, 514 * 4);
+    int32_t *dx = (int32_t *)up(input, (size_t)num_rfft * 4);
+    int32_t *dy = (int32_t *)up(NULL, (size_t)(num_rfft + 2) * 4);
+    CK(nnspk_launch_fft_dif(dx, dy, e, 1, G.stream));
+    down(output, dy, (size_t)(num_rfft + 2) * 4);
     fin();
 }
 
 static void fft_impl(int exp_nfft, void *input, void *output) /* fft.c:128-221 */
 {
-    if (exp_nfft != 8) fail(NNSP_EUNSUPPORTED, "fft: only exp_nfft = 8 (256 points, rfft(512)'s) is supported");
+    if (exp_nfft < 0 || exp_nfft > 8)
+        fail(NNSP_EUNSUPPORTED, "fft: exp_nfft must be 0..8 (the sizes fft.c's tables serve)");
+    const size_t bytes = (size_t)8 << exp_nfft;
     begin();
-    int32_t *dx = (int32_t *)up(input, 512 * 4);
-    int32_t *dy = (int32_t *)up(NULL, 512 * 4);
-    CK(nnspk_launch_rfft_port(dx, dy, 1, 1, G.stream));
-    int32_t z[512];
-    down(z, dy, sizeof z);
+    int32_t *dx = (int32_t *)up(input, bytes);
+    int32_t *dy = (int32_t *)up(NULL, bytes);
+    CK(nnspk_launch_fft_dif(dx, dy, exp_nfft, 0, G.stream));
+    down(output, dy, bytes);
+    down(input, dx, bytes); /* fft() works in place on its input (fft.c:180-195) */
     fin();
-    memcpy(output, z, sizeof z);
-    /* fft() works in place on its input: afterwards input[m] = Z[rev8(m)] */
-    int32_t *in = (int32_t *)input;
-    for (int m = 0; m < 256; ++m) {
-        unsigned r = 0;
-        for (int b = 0; b < 8; ++b) r |= ((m >> b) & 1u) << (7 - b);
-        in[2 * m] = z[2 * r];
-        in[2 * m + 1] = z[2 * r + 1];
-    }
+}
+
+/* ---- complex.c (the drop-in complex.h): one k_cplx launch per call ---- */
+static void cplx(int op, int32_t *out, size_t out_n, const void *a, size_t a_n, int32_t *b, size_t b_n, int shift,
+                 int len, int b_back)
+{
+    begin();
+    int32_t *da = (int32_t *)up(a, a_n * 4);
+    int32_t *db = b_n ? (int32_t *)up(b, b_n * 4) : NULL;
+    int32_t *dout = (int32_t *)up(NULL, out_n * 4);
+    CK(nnspk_launch_cplx(op, dout, da, db, shift, len, G.stream));
+    if (b_back) down(b, db, b_n * 4);
+    down(out, dout, out_n * 4);
+    fin();
+}
+static size_t nz(int len) { return len > 0 ? (size_t)len : 0; }
+static void complex32_copy_impl(COMPLEX32 *dst, COMPLEX32 *src)
+{
+    cplx(NNSP_CPLX_COPY, &dst->real, 2, src, 2, NULL, 0, 0, 1, 0);
+}
+static void complex32_affine_impl(COMPLEX32 *out, COMPLEX32 *Mat, COMPLEX32 *input, int shift_r, int len)
+{
+    if (len <= 0) return;
+    cplx(NNSP_CPLX_AFFINE, &out->real, 2 * nz(len), Mat, 2 * nz(len) * nz(len), &input->real, 2 * nz(len), shift_r,
+         len, 0);
+}
+static void complex32_interprod_impl(COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX32 *arry2, int shift_r, int len)
+{
+    cplx(NNSP_CPLX_INTERPROD, &out->real, 2, arry2, 2 * nz(len), &arry1->real, 2 * nz(len), shift_r, len, 0);
+}
+static void complex32_complex16_elmtprod_impl(COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX16 *arry2, int len)
+{
+    if (len <= 0) return;
+    cplx(NNSP_CPLX_ELMTPROD, &out->real, 2 * nz(len), arry1, 2 * nz(len), (int32_t *)arry2, nz(len), 0, len, 0);
+}
+static void complex32_add_impl(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2)
+{
+    cplx(NNSP_CPLX_ADD, &out->real, 2, addr1, 2, &addr2->real, 2, 0, 1, 0);
+}
+static void complexArry32_add_impl(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2, int len)
+{
+    if (len <= 0) return;
+    cplx(NNSP_CPLX_ARRY_ADD, &out->real, 2 * nz(len), addr1, 2 * nz(len), &addr2->real, 2 * nz(len), 0, len, 0);
+}
+static void complex32_neg_impl(COMPLEX32 *out, COMPLEX32 *in)
+{
+    cplx(NNSP_CPLX_NEG, &out->real, 2, in, 2, NULL, 0, 0, 1, 0);
+}
+static void complex32_sub_impl(COMPLEX32 *out, COMPLEX32 *a, COMPLEX32 *b)
+{
+    cplx(NNSP_CPLX_SUB, &out->real, 2, a, 2, &b->real, 2, 0, 1, 1);
+}
+static void complex32_mul_impl(COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2)
+{
+    cplx(NNSP_CPLX_MUL, &out->real, 2, addr1, 2, &addr2->real, 2, 0, 1, 0);
+}
+static void complex32_init_impl(COMPLEX32 *inst, int32_t real, int32_t imag)
+{
+    const int32_t v[2] = {real, imag};
+    cplx(NNSP_CPLX_INIT, &inst->real, 2, v, 2, NULL, 0, 0, 1, 0);
+}
+static void complex32_real2cmplx_impl(COMPLEX32 *inst, int32_t real) { complex32_init_impl(inst, real, 0); }
+static void complexArry32_real2cmplx_impl(COMPLEX32 *inst, int32_t *real, int32_t len)
+{
+    if (len <= 0) return;
+    cplx(NNSP_CPLX_ARRY_INIT, &inst->real, 2 * nz(len), real, nz(len), NULL, 0, 0, len, 0);
+}
+static void complexArry32_init_impl(COMPLEX32 *inst, int32_t *real, int32_t *imag, int len)
+{
+    if (len <= 0) return;
+    cplx(NNSP_CPLX_ARRY_INIT, &inst->real, 2 * nz(len), real, nz(len), imag, nz(len), 0, len, 0);
 }
 
 static void melSpecProc_impl(int32_t *specs, int32_t *melSpecs) /* melSpecProc.c:6-27 */
@@ -999,500 +1070,128 @@ static void shift_32b_impl(int32_t *x, int8_t shift, int len) { shift_call(x, sh
  * 0 or void).  Nested entry points (NNSPClass_reset -> FeatureClass_setDefault)
  * share the outermost jump target.
  * ------------------------------------------------------------------------- */
-void *relu6_fix(int16_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return NULL;
-        }
+/* The public entry points: the outermost one sets fail()'s longjmp target
+ * and returns onfail (void: nothing) when a GPU step fails inside it. */
+#define LEGACY_ENTRY(ret, name, params, args, onfail) \
+    ret name params                                   \
+    {                                                 \
+        if (G.depth++ == 0) {                         \
+            if (setjmp(G.jb)) {                       \
+                G.depth = 0;                          \
+                return onfail;                        \
+            }                                         \
+        }                                             \
+        ret r_ = name##_impl args;                    \
+        --G.depth;                                    \
+        return r_;                                    \
     }
-    void *r = relu6_fix_impl(y, x, len);
-    --G.depth;
-    return r;
+#define LEGACY_ENTRY_VOID(name, params, args) \
+    void name params                          \
+    {                                         \
+        if (G.depth++ == 0) {                 \
+            if (setjmp(G.jb)) {               \
+                G.depth = 0;                  \
+                return;                       \
+            }                                 \
+        }                                     \
+        name##_impl args;                     \
+        --G.depth;                            \
+    }
+
+LEGACY_ENTRY(void *, relu6_fix, (int16_t *y, int32_t *x, int len), (y, x, len), NULL)
+
+LEGACY_ENTRY(void *, tanh_fix, (int16_t *y, int32_t *x, int len), (y, x, len), NULL)
+
+LEGACY_ENTRY(void *, sigmoid_fix, (int16_t *y, int32_t *x, int len), (y, x, len), NULL)
+
+LEGACY_ENTRY(void *, linear_fix, (int32_t *y, int32_t *x, int len), (y, x, len), NULL)
+
+LEGACY_ENTRY(int, fc_8x16, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
+
+LEGACY_ENTRY(int, fc_8x16_acc32b, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
+
+LEGACY_ENTRY(int, lstm_8x16, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
+
+LEGACY_ENTRY(int, lstm_8x16_acc32b, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
+
+LEGACY_ENTRY_VOID(NeuralNetClass_exe, (NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer), (pt_inst, input, output, debug_layer))
+
+LEGACY_ENTRY_VOID(arm_fft_exec, (int32_t *y, int32_t *x), (y, x))
+
+LEGACY_ENTRY(int, stftModule_analyze_arm, (void *ps_, int16_t *x, int32_t *y), (ps_, x, y), G.sticky)
+
+LEGACY_ENTRY_VOID(spec2pspec_arm, (int32_t *y, int32_t *x, int len), (y, x, len))
+
+LEGACY_ENTRY(int, stftModule_analyze, (stftModule *ps, int16_t *x, int32_t *y), (ps, x, y), G.sticky)
+
+LEGACY_ENTRY_VOID(spec2pspec, (int32_t *y, int32_t *x, int len), (y, x, len))
+
+LEGACY_ENTRY_VOID(rfft, (int num_rfft, int32_t *input, void *output), (num_rfft, input, output))
+
+LEGACY_ENTRY_VOID(fft, (int exp_nfft, void *input, void *output), (exp_nfft, input, output))
+
+LEGACY_ENTRY_VOID(complex32_copy, (COMPLEX32 *dst, COMPLEX32 *src), (dst, src))
+LEGACY_ENTRY_VOID(complex32_affine, (COMPLEX32 *out, COMPLEX32 *Mat, COMPLEX32 *input, int shift_r, int len),
+                  (out, Mat, input, shift_r, len))
+LEGACY_ENTRY_VOID(complex32_interprod, (COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX32 *arry2, int shift_r, int len),
+                  (out, arry1, arry2, shift_r, len))
+LEGACY_ENTRY_VOID(complex32_complex16_elmtprod, (COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX16 *arry2, int len),
+                  (out, arry1, arry2, len))
+LEGACY_ENTRY_VOID(complex32_add, (COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2), (out, addr1, addr2))
+LEGACY_ENTRY_VOID(complexArry32_add, (COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2, int len),
+                  (out, addr1, addr2, len))
+LEGACY_ENTRY_VOID(complex32_neg, (COMPLEX32 *out, COMPLEX32 *in), (out, in))
+LEGACY_ENTRY_VOID(complex32_sub, (COMPLEX32 *out, COMPLEX32 *a, COMPLEX32 *b), (out, a, b))
+LEGACY_ENTRY_VOID(complex32_mul, (COMPLEX32 *out, COMPLEX32 *addr1, COMPLEX32 *addr2), (out, addr1, addr2))
+LEGACY_ENTRY_VOID(complex32_init, (COMPLEX32 *inst, int32_t real, int32_t imag), (inst, real, imag))
+LEGACY_ENTRY_VOID(complex32_real2cmplx, (COMPLEX32 *inst, int32_t real), (inst, real))
+LEGACY_ENTRY_VOID(complexArry32_real2cmplx, (COMPLEX32 *inst, int32_t *real, int32_t len), (inst, real, len))
+LEGACY_ENTRY_VOID(complexArry32_init, (COMPLEX32 *inst, int32_t *real, int32_t *imag, int len), (inst, real, imag, len))
+
+/* complex.c:174-184 (AMBIQ_NNSP_DEBUG builds): host-side text output only */
+void complexArry32_print(COMPLEX32 *inst, int len)
+{
+    for (int i = 0; i < len; i++) printf("%d: (%d, %d)\n", i, inst[i].real, inst[i].imag);
 }
 
-void *tanh_fix(int16_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return NULL;
-        }
-    }
-    void *r = tanh_fix_impl(y, x, len);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(melSpecProc, (int32_t *specs, int32_t *melSpecs), (specs, melSpecs))
 
-void *sigmoid_fix(int16_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return NULL;
-        }
-    }
-    void *r = sigmoid_fix_impl(y, x, len);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(norm_oneTwo, (int32_t x, int32_t *y, int8_t *shift), (x, y, shift))
 
-void *linear_fix(int32_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return NULL;
-        }
-    }
-    void *r = linear_fix_impl(y, x, len);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(log10_vec, (int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in), (out, x, len, bit_frac_in))
 
-int fc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
-            int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
-            int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
-            int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
-            void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = fc_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(my_log10, (int32_t *out, int32_t x), (out, x))
 
-int fc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
-                   int16_t *input, int16_t *input_rec, int32_t *c_state, int16_t dim_output,
-                   int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
-                   int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
-                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = fc_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(FeatureClass_setDefault, (FeatureClass *ps), (ps))
 
-int lstm_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
-              int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
-              int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias,
-              int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
-              void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = lstm_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(FeatureClass_execute, (FeatureClass *ps, int16_t *input), (ps, input))
 
-int lstm_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias,
-                     int16_t *input, int16_t *h_state, int32_t *c_state, int16_t dim_output,
-                     int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
-                     int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
-                     ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = lstm_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, h_state, c_state, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY(int, NNSPClass_reset, (NNSPClass *pt_inst), (pt_inst), G.sticky)
 
-void NeuralNetClass_exe(NeuralNetClass *pt_inst, int16_t *input, int32_t *output, int8_t debug_layer)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    NeuralNetClass_exe_impl(pt_inst, input, output, debug_layer);
-    --G.depth;
-}
+LEGACY_ENTRY(int16_t, NNSPClass_exec, (NNSPClass *pt_inst, int16_t *rawPCM), (pt_inst, rawPCM), 0)
 
-void arm_fft_exec(int32_t *y, int32_t *x)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    arm_fft_exec_impl(y, x);
-    --G.depth;
-}
+LEGACY_ENTRY_VOID(my_argmax, (int32_t *vec, int len, int16_t *Imax), (vec, len, Imax))
 
-int stftModule_analyze_arm(void *ps_, int16_t *x, int32_t *y)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = stftModule_analyze_arm_impl(ps_, x, y);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY(int32_t, ceiling, (int32_t input), (input), 0)
 
-void spec2pspec_arm(int32_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    spec2pspec_arm_impl(y, x, len);
-    --G.depth;
-}
+LEGACY_ENTRY(int32_t, compute_pwr2, (int32_t input), (input), 0)
 
-int stftModule_analyze(stftModule *ps, int16_t *x, int32_t *y)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = stftModule_analyze_impl(ps, x, y);
-    --G.depth;
-    return r;
-}
+LEGACY_ENTRY_VOID(binary_post_proc, (NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger), (pt_inst, pt_nn_est, pt_trigger))
 
-void spec2pspec(int32_t *y, int32_t *x, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    spec2pspec_impl(y, x, len);
-    --G.depth;
-}
+LEGACY_ENTRY_VOID(s2i_post_proc, (NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger), (pt_inst, pt_nn_est, pt_trigger))
 
-void rfft(int num_rfft, int32_t *input, void *output)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    rfft_impl(num_rfft, input, output);
-    --G.depth;
-}
+LEGACY_ENTRY(int, affine_Krows_8x16, (int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias, int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int64_t *pt_accum, int8_t is_out, void *(*act)(void *, int32_t *, int)), (dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act), G.sticky)
 
-void fft(int exp_nfft, void *input, void *output)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    fft_impl(exp_nfft, input, output);
-    --G.depth;
-}
+LEGACY_ENTRY(int, affine_Krows_8x16_acc32b, (int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias, int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int32_t *pt_accum, int8_t is_out, void *(*act)(void *, int32_t *, int)), (dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act), G.sticky)
 
-void melSpecProc(int32_t *specs, int32_t *melSpecs)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    melSpecProc_impl(specs, melSpecs);
-    --G.depth;
-}
+LEGACY_ENTRY(int, rc_Krows_8x16, (int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec, int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int)), (dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act), G.sticky)
 
-void norm_oneTwo(int32_t x, int32_t *y, int8_t *shift)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    norm_oneTwo_impl(x, y, shift);
-    --G.depth;
-}
+LEGACY_ENTRY(int, rc_Krows_8x16_acc32b, (int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec, int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int)), (dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act), G.sticky)
 
-void log10_vec(int32_t *out, int32_t *x, int32_t len, int16_t bit_frac_in)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    log10_vec_impl(out, x, len, bit_frac_in);
-    --G.depth;
-}
+LEGACY_ENTRY(int, rc_8x16, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
 
-void my_log10(int32_t *out, int32_t x)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    my_log10_impl(out, x);
-    --G.depth;
-}
+LEGACY_ENTRY(int, rc_8x16_acc32b, (int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input, int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int)), (p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act), G.sticky)
 
-void FeatureClass_setDefault(FeatureClass *ps)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    FeatureClass_setDefault_impl(ps);
-    --G.depth;
-}
+LEGACY_ENTRY_VOID(shift_64b, (int64_t *x, int8_t shift, int len), (x, shift, len))
 
-void FeatureClass_execute(FeatureClass *ps, int16_t *input)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    FeatureClass_execute_impl(ps, input);
-    --G.depth;
-}
-
-int NNSPClass_reset(NNSPClass *pt_inst)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = NNSPClass_reset_impl(pt_inst);
-    --G.depth;
-    return r;
-}
-
-int16_t NNSPClass_exec(NNSPClass *pt_inst, int16_t *rawPCM)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return 0;
-        }
-    }
-    int16_t r = NNSPClass_exec_impl(pt_inst, rawPCM);
-    --G.depth;
-    return r;
-}
-
-void my_argmax(int32_t *vec, int len, int16_t *Imax)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    my_argmax_impl(vec, len, Imax);
-    --G.depth;
-}
-
-int32_t ceiling(int32_t input)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return 0;
-        }
-    }
-    int32_t r = ceiling_impl(input);
-    --G.depth;
-    return r;
-}
-
-int32_t compute_pwr2(int32_t input)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return 0;
-        }
-    }
-    int32_t r = compute_pwr2_impl(input);
-    --G.depth;
-    return r;
-}
-
-void binary_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    binary_post_proc_impl(pt_inst, pt_nn_est, pt_trigger);
-    --G.depth;
-}
-
-void s2i_post_proc(NNSPClass *pt_inst, int32_t *pt_nn_est, int16_t *pt_trigger)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    s2i_post_proc_impl(pt_inst, pt_nn_est, pt_trigger);
-    --G.depth;
-}
-
-int affine_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
-                      int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
-                      int16_t qbit_input, int64_t *pt_accum, int8_t is_out,
-                      void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = affine_Krows_8x16_impl(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act);
-    --G.depth;
-    return r;
-}
-
-int affine_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int16_t **pp_bias,
-                             int16_t *input, int16_t dim_input, int16_t qbit_kernel, int16_t qbit_bias,
-                             int16_t qbit_input, int32_t *pt_accum, int8_t is_out,
-                             void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = affine_Krows_8x16_acc32b_impl(dim_output, pp_output, pp_kernel, pp_bias, input, dim_input, qbit_kernel, qbit_bias, qbit_input, pt_accum, is_out, act);
-    --G.depth;
-    return r;
-}
-
-int rc_Krows_8x16(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
-                  int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input, int16_t dim_input_rec,
-                  int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
-                  void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = rc_Krows_8x16_impl(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
-    --G.depth;
-    return r;
-}
-
-int rc_Krows_8x16_acc32b(int16_t dim_output, int16_t **pp_output, int8_t **pp_kernel, int8_t **pp_kernel_rec,
-                         int16_t **pp_bias, int16_t *input, int16_t *input_rec, int16_t dim_input,
-                         int16_t dim_input_rec, int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input,
-                         int16_t qbit_input_rec, void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = rc_Krows_8x16_acc32b_impl(dim_output, pp_output, pp_kernel, pp_kernel_rec, pp_bias, input, input_rec, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act);
-    --G.depth;
-    return r;
-}
-
-int rc_8x16(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
-            int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec, int16_t qbit_kernel,
-            int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec, ACTIVATION_TYPE act_type,
-            void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = rc_8x16_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
-
-int rc_8x16_acc32b(int16_t *p_output, int8_t *p_kernel, int8_t *p_kernel_rec, int16_t *p_bias, int16_t *input,
-                   int16_t *input_rec, int16_t dim_output, int16_t dim_input, int16_t dim_input_rec,
-                   int16_t qbit_kernel, int16_t qbit_bias, int16_t qbit_input, int16_t qbit_input_rec,
-                   ACTIVATION_TYPE act_type, void *(*act)(void *, int32_t *, int))
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return G.sticky;
-        }
-    }
-    int r = rc_8x16_acc32b_impl(p_output, p_kernel, p_kernel_rec, p_bias, input, input_rec, dim_output, dim_input, dim_input_rec, qbit_kernel, qbit_bias, qbit_input, qbit_input_rec, act_type, act);
-    --G.depth;
-    return r;
-}
-
-void shift_64b(int64_t *x, int8_t shift, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    shift_64b_impl(x, shift, len);
-    --G.depth;
-}
-
-void shift_32b(int32_t *x, int8_t shift, int len)
-{
-    if (G.depth++ == 0) {
-        if (setjmp(G.jb)) {
-            G.depth = 0;
-            return;
-        }
-    }
-    shift_32b_impl(x, shift, len);
-    --G.depth;
-}
+LEGACY_ENTRY_VOID(shift_32b, (int32_t *x, int8_t shift, int len), (x, shift, len))

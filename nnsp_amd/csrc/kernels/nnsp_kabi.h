@@ -227,6 +227,14 @@ int nnspk_launch_rfft(int32_t *x, int32_t *y, int n, void *stream);
 int nnspk_launch_pspec(int32_t *y, const int32_t *x, int len, int n, int shift, void *stream);
 /* the ARM_OPTIMIZED=0 build's rfft(512) (y [n][514]) or, cfft_only, fft(8) (y [n][512]) */
 int nnspk_launch_rfft_port(const int32_t *x, int32_t *y, int n, int cfft_only, void *stream);
+/* complex.c's helpers (k_cplx) */
+enum {
+    NNSP_CPLX_COPY, NNSP_CPLX_AFFINE, NNSP_CPLX_INTERPROD, NNSP_CPLX_ELMTPROD, NNSP_CPLX_ADD, NNSP_CPLX_ARRY_ADD,
+    NNSP_CPLX_NEG, NNSP_CPLX_SUB, NNSP_CPLX_MUL, NNSP_CPLX_INIT, NNSP_CPLX_ARRY_INIT
+};
+int nnspk_launch_cplx(int op, int32_t *o, int32_t *a, int32_t *b, int shift, int len, void *stream);
+/* fft.c's fft(exp_nfft) / rfft(2^(exp_nfft+1)) for one vector, every size its tables serve */
+int nnspk_launch_fft_dif(int32_t *x, int32_t *y, int exp_nfft, int rfft, void *stream);
 int nnspk_launch_mel(const int32_t *spec, int32_t *mel, int n, void *stream);
 int nnspk_launch_log10(int32_t *out, const int32_t *x, int n, int add, void *stream);
 int nnspk_launch_act(int type, const int32_t *x, void *y, int n, void *stream);

@@ -1303,6 +1303,162 @@ __global__ __launch_bounds__(64) void k_rfft_port(const int32_t* x, int32_t* y, 
     }
 }
 
+// The ARM_OPTIMIZED=0 build's fft(exp_nfft, ...) and rfft(num_rfft, ...) for
+// every size their tables serve (fft.c:27-221): exp_nfft 0..8 (radix-4 DIF
+// stages for 8 and 7, then a radix-2 stage for 7; below that only the
+// bit-reversal copy runs), rfft of 256 or 512 points.  One workgroup per call,
+// butterflies across its 64 lanes, the working array in LDS.  Unlike the
+// front end's register-resident 512-point path (k_rfft_port), this one keeps
+// complex.c's int64 products and int32 clamps literally
+// (complex32_interprod / _complex16_elmtprod), since for other inputs than
+// windowed int16 PCM they can bind.
+//   rfft: x = num_rfft int32 reals (not modified), y = num_rfft / 2 + 1 complex
+//   fft:  x = 2^exp_nfft COMPLEX32, modified in place like fft.c's input; y =
+//         2^exp_nfft COMPLEX32 in natural order
+__device__ __forceinline__ int32_t clamp64(int64_t v) { return sat32(v); }
+__device__ __forceinline__ int2 cmul_tw15(int2 a, int32_t w) {   // complex32_complex16_elmtprod, one element
+    const int64_t wr = (int16_t)(w & 0xffff), wi = (int16_t)(w >> 16);
+    return make_int2(clamp64(((int64_t)a.x * wr - (int64_t)a.y * wi) >> 15),
+                     clamp64(((int64_t)a.x * wi + (int64_t)a.y * wr) >> 15));
+}
+__global__ __launch_bounds__(64) void k_fft_dif(int32_t* x, int32_t* y, int exp_nfft, int rfft) {
+    __shared__ int2 c[256];
+    __shared__ int2 z[256];
+    const int lane = threadIdx.x;
+    const int nfft = 1 << exp_nfft;
+    for (int i = lane; i < nfft; i += 64) c[i] = make_int2(x[2 * i], x[2 * i + 1]);   // cinput (rfft: pairs of reals)
+    __syncthreads();
+    const int stages = exp_nfft == 8 ? 4 : (exp_nfft == 7 ? 3 : 0);
+    int Nf = nfft, Ng = 1, S = 1 << (8 - exp_nfft);
+    for (int st = 0; st < stages; ++st) {
+        const int Nfd4 = Nf >> 2;
+        for (int bf = lane; bf < Ng * Nfd4; bf += 64) {
+            const int g = bf / Nfd4, m = bf - g * Nfd4, s0 = g * Nf + m, k = m * S;
+            const int2 a = c[s0], b = c[s0 + 2 * Nfd4], cc = c[s0 + Nfd4], d = c[s0 + 3 * Nfd4];
+            // ti = {x0, x2, x1, x3} (fft.c:180-187); to = M4 ti (exact sums, clamped, complex32_affine)
+            const int64_t ar = a.x, ai = a.y, br = b.x, bi = b.y, cr = cc.x, ci = cc.y, dr = d.x, di = d.y;
+            int2 to[4];
+            to[0] = make_int2(clamp64(ar + br + cr + dr), clamp64(ai + bi + ci + di));
+            to[1] = make_int2(clamp64(ar + br - cr - dr), clamp64(ai + bi - ci - di));
+            to[2] = make_int2(clamp64(ar - br + ci - di), clamp64(ai - bi - cr + dr));   // row (1, -1, -j, j)
+            to[3] = make_int2(clamp64(ar - br - ci + di), clamp64(ai - bi + cr - dr));   // row (1, -1, j, -j)
+            for (int i = 0; i < 4; ++i) c[s0 + i * Nfd4] = cmul_tw15(to[i], nnsp_tbl_dif_tw[4 * k + i]);
+        }
+        __syncthreads();
+        Nf >>= 2;
+        Ng <<= 2;
+        S <<= 2;
+    }
+    if (exp_nfft == 7) {   // the final radix-2 stage (fft.c:199-211): M2 = [[1, 1], [1, -1]]
+        for (int m = lane; m < nfft / 2; m += 64) {
+            const int2 p0 = c[2 * m], p1 = c[2 * m + 1];
+            c[2 * m] = make_int2(clamp64((int64_t)p0.x + p1.x), clamp64((int64_t)p0.y + p1.y));
+            c[2 * m + 1] = make_int2(clamp64((int64_t)p0.x - p1.x), clamp64((int64_t)p0.y - p1.y));
+        }
+        __syncthreads();
+    }
+    const int Rs = 8 - exp_nfft;
+    for (int m = lane; m < nfft; m += 64) z[m] = c[nnsp_tbl_bitrev8[m] >> Rs];   // br_coeff[m] >> Rs
+    __syncthreads();
+    if (!rfft) {
+        for (int m = lane; m < nfft; m += 64) {
+            y[2 * m] = z[m].x;
+            y[2 * m + 1] = z[m].y;
+            x[2 * m] = c[m].x;   // fft() leaves its stage output in its input
+            x[2 * m + 1] = c[m].y;
+        }
+        return;
+    }
+    // rfft's split (fft.c:62-125): Xe, Xo from Z and conj(Z(N/2 - i)), X = Xe + Xo tw^(R i)
+    const int R = 1 << (8 - exp_nfft), half = nfft;   // num_rfft / 2 complex
+    for (int i = lane; i < half; i += 64) {
+        const int2 po = z[i], pr = z[i ? half - i : 0];
+        const int32_t tr = pr.x, ti = wsub(0, pr.y);
+        const int2 xe = make_int2(wadd(po.x, tr) >> 1, wadd(po.y, ti) >> 1);
+        const int2 xo = make_int2(wsub(po.y, ti) >> 1, wsub(0, wsub(po.x, tr)) >> 1);
+        const int2 o = cmul_tw15(xo, nnsp_tbl_dif_rtw[R * i]);
+        y[2 * i] = wadd(xe.x, o.x);
+        y[2 * i + 1] = wadd(xe.y, o.y);
+        if (i == 0) {
+            y[2 * half] = wsub(xe.x, xo.x);
+            y[2 * half + 1] = wsub(xe.y, xo.y);
+        }
+    }
+}
+
+// complex.c's helpers (the drop-in complex.h), one launch per call: op codes
+// NNSP_CPLX_* (nnsp_kabi.h); a, b: operands, o: result (b is written back by
+// complex32_sub, which negates it in place, complex.c:108-113).  int64
+// products with int32 clamps where complex.c has them, int32 wrap elsewhere.
+__device__ __forceinline__ int64_t cx_re(int64_t ar, int64_t ai, int64_t br, int64_t bi) {
+    return (int64_t)((uint64_t)(ar * br) - (uint64_t)(ai * bi));
+}
+__device__ __forceinline__ int64_t cx_im(int64_t ar, int64_t ai, int64_t br, int64_t bi) {
+    return (int64_t)((uint64_t)(ar * bi) + (uint64_t)(ai * br));
+}
+__global__ __launch_bounds__(64) void k_cplx(int op, int32_t* o, int32_t* a, int32_t* b, int shift, int len, int32_t r,
+                                             int32_t im) {
+    const int n = op == NNSP_CPLX_INTERPROD || op == NNSP_CPLX_COPY || op == NNSP_CPLX_ADD || op == NNSP_CPLX_NEG ||
+                          op == NNSP_CPLX_SUB || op == NNSP_CPLX_MUL || op == NNSP_CPLX_INIT
+                      ? 1 : len;
+    for (int i = threadIdx.x; i < n; i += 64) {
+        switch (op) {
+        case NNSP_CPLX_COPY:
+        case NNSP_CPLX_INIT:         // o = a (complex32_init / real2cmplx: a staged by the host)
+            o[0] = a[0];
+            o[1] = a[1];
+            break;
+        case NNSP_CPLX_AFFINE:       // out[i] = interprod(input, Mat + i * len): a = Mat, b = input
+        case NNSP_CPLX_INTERPROD: {  // out = sum a1[k] * a2[k]: a = arry1, b = arry2
+            const int32_t* m = op == NNSP_CPLX_AFFINE ? a + 2 * (size_t)i * len : a;
+            uint64_t re = 0, ii = 0;
+            for (int k = 0; k < len; ++k) {
+                re += (uint64_t)cx_re(b[2 * k], b[2 * k + 1], m[2 * k], m[2 * k + 1]);
+                ii += (uint64_t)cx_im(b[2 * k], b[2 * k + 1], m[2 * k], m[2 * k + 1]);
+            }
+            o[2 * i] = sat32((int64_t)re >> shift);
+            o[2 * i + 1] = sat32((int64_t)ii >> shift);
+            break;
+        }
+        case NNSP_CPLX_ELMTPROD: {   // a: COMPLEX32, b: COMPLEX16 words
+            const int64_t wr = (int16_t)(b[i] & 0xffff), wi = (int16_t)(b[i] >> 16);
+            o[2 * i] = sat32(cx_re(a[2 * i], a[2 * i + 1], wr, wi) >> 15);
+            o[2 * i + 1] = sat32(cx_im(a[2 * i], a[2 * i + 1], wr, wi) >> 15);
+            break;
+        }
+        case NNSP_CPLX_ADD:
+        case NNSP_CPLX_ARRY_ADD:
+            o[2 * i] = wadd(a[2 * i], b[2 * i]);
+            o[2 * i + 1] = wadd(a[2 * i + 1], b[2 * i + 1]);
+            break;
+        case NNSP_CPLX_NEG:
+            o[0] = wsub(0, a[0]);
+            o[1] = wsub(0, a[1]);
+            break;
+        case NNSP_CPLX_SUB: {        // neg(b, b); add(out, a, b)
+            const int32_t nr = wsub(0, b[0]), ni = wsub(0, b[1]);
+            b[0] = nr;
+            b[1] = ni;
+            o[0] = wadd(a[0], nr);
+            o[1] = wadd(a[1], ni);
+            break;
+        }
+        case NNSP_CPLX_MUL: {        // int32 products (complex.c:115-121), wrapping
+            const uint32_t ar = a[0], ai = a[1], br = b[0], bi = b[1];
+            o[0] = (int32_t)(ar * br - ai * bi);
+            o[1] = (int32_t)(ar * bi + ai * br);
+            break;
+        }
+        case NNSP_CPLX_ARRY_INIT:    // a: reals, b: imags (NULL: zeros, complexArry32_real2cmplx)
+            o[2 * i] = a[i];
+            o[2 * i + 1] = b ? b[i] : 0;
+            break;
+        }
+    }
+    (void)r;
+    (void)im;
+}
+
 // spec2pspec_arm (shift 27) / spec2pspec (shift 15): x [n][1024], y [n][1024]
 __global__ void k_pspec(int32_t* y, const int32_t* x, int len, int n, int shift) {
     const int b = blockIdx.y;
@@ -1657,6 +1813,17 @@ int nnspk_launch_pspec(int32_t* y, const int32_t* x, int len, int n, int shift, 
 int nnspk_launch_rfft_port(const int32_t* x, int32_t* y, int n, int cfft_only, void* stream) {
     if (n <= 0) return 0;
     hipLaunchKernelGGL(k_rfft_port, dim3(n < 4096 ? n : 4096), dim3(64), 0, (hipStream_t)stream, x, y, n, cfft_only);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_fft_dif(int32_t* x, int32_t* y, int exp_nfft, int rfft, void* stream) {
+    if (exp_nfft < 0 || exp_nfft > 8) return ok(hipErrorInvalidValue);
+    hipLaunchKernelGGL(k_fft_dif, dim3(1), dim3(64), 0, (hipStream_t)stream, x, y, exp_nfft, rfft);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_cplx(int op, int32_t* o, int32_t* a, int32_t* b, int shift, int len, void* stream) {
+    hipLaunchKernelGGL(k_cplx, dim3(1), dim3(64), 0, (hipStream_t)stream, op, o, a, b, shift, len, 0, 0);
     return ok(hipGetLastError());
 }
 

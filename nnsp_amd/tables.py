@@ -193,6 +193,7 @@ def header_text() -> str:
         _c_array("int32_t", "nnsp_tbl_melseg", mel_segments(), 4),
         _c_array("int32_t", "nnsp_tbl_dif_tw", dif_twiddles(), 8),
         _c_array("int32_t", "nnsp_tbl_dif_rtw", rfft_dif_twiddles(), 8),
+        _c_array("int16_t", "nnsp_tbl_bitrev8", bitrev8()),
         "#endif\n",
     ]
     return "\n".join(parts)

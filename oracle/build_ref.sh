@@ -29,6 +29,9 @@
 #                              (ARM_OPTIMIZED=0: fft.c, complex.c,
 #                              twiddle_fft_dif.c, spectrogram_module.c,
 #                              feature_module.c, mel, log10, window), row N4.
+#  libnnsp_ref_nnsp_portable.so  the whole portable path: nn_speech.c
+#                              (NNSPClass_init/_reset/_exec) over the portable
+#                              front end and NN files above, same switches.
 #  libnnsp_ref_nets.so         evb/src/def_nn{0_s2i,1_vad,2_kws_galaxy}.c (the
 #                              reference's three nets as data) against the
 #                              reference headers, linked with the portable NN
@@ -72,4 +75,14 @@ gcc -O3 -march=native -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NN
     -I"$API" -I"$CORE" \
     "$SRC/affine.c" "$SRC/affine_acc32b.c" "$SRC/lstm.c" "$SRC/neural_nets.c" "$SRC/activation.c" \
     -Wl,-z,defs -o "$OUT/libnnsp_ref_nn_portable_o3.so"
+
+# the reference's whole portable NNSP path (ARM_OPTIMIZED=0): NNSPClass_init /
+# _reset / _exec of nn_speech.c over the portable front end and NN, for the
+# end-to-end fixture ref_nnsp_portable.npz
+gcc -O2 -fPIC -shared -w -fwrapv -D__AMBIQ_NNSP_DEBUG__ -DAMBIQ_NNSP_DEBUG=0 -DARM_OPTIMIZED=0 \
+    -I"$API" -I"$CORE" \
+    "$SRC/nn_speech.c" "$SRC/feature_module.c" "$SRC/spectrogram_module.c" "$SRC/fft.c" "$SRC/complex.c" \
+    "$SRC/twiddle_fft_dif.c" "$SRC/melSpecProc.c" "$SRC/melSpec_coeff.c" "$SRC/fixlog10.c" \
+    "$SRC/window_stft_coef.c" "$SRC/affine.c" "$SRC/affine_acc32b.c" "$SRC/lstm.c" "$SRC/neural_nets.c" \
+    "$SRC/activation.c" -Wl,-z,defs -o "$OUT/libnnsp_ref_nnsp_portable.so"
 echo "$OUT"

@@ -27,11 +27,26 @@ reference tree).
                    oracle/_ref/libnnsp_ref_fe_portable.so): rfft(512) and
                    FeatureClass_execute over consecutive frames
 
+  ref_fft_complex.npz  the reference's portable fft.c / complex.c
+                   (oracle/_ref/libnnsp_ref_fe_portable.so): rfft(256) and
+                   rfft(512), fft(exp_nfft) for exp_nfft 0..8 (output and the
+                   in-place input), on vectors from small to full int32 range
+                   (complex.c's clamps bind), and every complex32_* helper
+
+  ref_nnsp_portable.npz  the reference's whole portable path end to end
+                   (oracle/_ref/libnnsp_ref_nnsp_portable.so: nn_speech.c over
+                   the ARM_OPTIMIZED=0 front end and NN): NNSPClass_init /
+                   _reset / _exec on each reference net, acc64 and acc32, over
+                   the three test wavs x 1000 frames and 8 synthetic streams x
+                   200 frames with one mid-stream NNSPClass_reset; per frame
+                   the return value, normFeatContext[200:240], outputs[3] and
+                   counts_category, and the final LSTM h / c
+
   test_wavs.npz    python/test_wavs/{speech,galaxy,galaxy_s2i}.wav samples
                    (16 kHz mono int16, 160000 each): the reference's own test
                    inputs, replayed by every 4th synthetic stream
 
-Usage: make_golden.py [stages] [nets] [nn] [wavs]   (default: all)
+Usage: make_golden.py [stages] [nets] [nn] [wavs] [fe_portable] [fft_complex] [nnsp]   (default: all)
 """
 from __future__ import annotations
 
@@ -48,6 +63,7 @@ REF_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_partial.so")
 REF_NN_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nn_portable.so")
 REF_NETS_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nets.so")
 REF_FE_PORT_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_fe_portable.so")
+REF_NNSP_PORT_SO = os.path.join(ROOT, "oracle", "_ref", "libnnsp_ref_nnsp_portable.so")
 REF_PY = "/root/reference/python"
 
 from nnsp_amd._lib import FeatureClass, NeuralNetClass, NNSPClass  # noqa: E402  (ABI mirrors)
@@ -440,6 +456,152 @@ def fe_portable() -> None:
     np.savez_compressed(os.path.join(HERE, "ref_fe_portable.npz"), **out)
 
 
+def fft_complex() -> None:
+    """ref_fft_complex.npz: fft.c's rfft / fft at every size its tables serve,
+    and complex.c's helpers, from the reference's own portable build."""
+    R = C.CDLL(REF_FE_PORT_SO)
+    rng = np.random.default_rng(0x0FF7)
+    out = {}
+    amps = [1 << 15, 1 << 20, 1 << 28, 1 << 31]
+    for num in (256, 512):
+        xs = np.array([rng.integers(-a, a, num) for a in amps for _ in range(4)], np.int64).astype(np.int32)
+        ys = np.zeros((len(xs), num + 2), np.int32)
+        for i, x in enumerate(xs):
+            xi = x.copy()
+            y = np.zeros(1024, np.int32)
+            R.rfft(num, P(xi), P(y))
+            assert np.array_equal(xi, x)
+            ys[i] = y[:num + 2]
+        out[f"rfft{num}_in"], out[f"rfft{num}_out"] = xs, ys
+    for e in range(9):
+        n = 1 << e
+        xs = np.array([rng.integers(-a, a, 2 * n) for a in amps for _ in range(3)], np.int64).astype(np.int32)
+        ys = np.zeros((len(xs), 2 * n), np.int32)
+        xo = np.zeros_like(xs)
+        for i, x in enumerate(xs):
+            xi = x.copy()
+            y = np.zeros(2 * n, np.int32)
+            R.fft(e, P(xi), P(y))
+            ys[i], xo[i] = y, xi
+        out[f"fft{e}_in"], out[f"fft{e}_out"], out[f"fft{e}_in_after"] = xs, ys, xo
+    # complex.c helpers: [case][...] int32 pairs
+    L = 7
+    a = rng.integers(-2**31, 2**31, (12, L, 2)).astype(np.int64).astype(np.int32)
+    b = rng.integers(-2**31, 2**31, (12, L, 2)).astype(np.int64).astype(np.int32)
+    a[:4] >>= 16
+    b[:4] >>= 16
+    m = rng.integers(-2**31, 2**31, (12, L, L, 2)).astype(np.int64).astype(np.int32)
+    m[:6] >>= 12
+    w16 = rng.integers(-2**15, 2**15, (12, L, 2)).astype(np.int16)
+    sh = np.array([0, 1, 15, 31, 0, 3, 15, 20, 0, 7, 30, 2], np.int32)
+    out["cx_a"], out["cx_b"], out["cx_m"], out["cx_w16"], out["cx_shift"] = a, b, m, w16, sh
+    res = {k: [] for k in ("copy", "affine", "interprod", "elmtprod", "add", "arry_add", "neg", "sub", "sub_b",
+                           "mul", "init", "real2cmplx", "arry_real2cmplx", "arry_init")}
+    for c in range(12):
+        A, B, M, W = (np.ascontiguousarray(v[c]) for v in (a, b, m, w16))
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_copy(P(o), P(A)); res["copy"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_affine(P(o), P(M), P(A), int(sh[c]), L); res["affine"].append(o.copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_interprod(P(o), P(A), P(B), int(sh[c]), L); res["interprod"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_complex16_elmtprod(P(o), P(A), P(W), L); res["elmtprod"].append(o.copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_add(P(o), P(A), P(B)); res["add"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complexArry32_add(P(o), P(A), P(B), L); res["arry_add"].append(o.copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_neg(P(o), P(A)); res["neg"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        Bc = B.copy()
+        R.complex32_sub(P(o), P(A), P(Bc)); res["sub"].append(o[0].copy()); res["sub_b"].append(Bc[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_mul(P(o), P(A), P(B)); res["mul"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_init(P(o), C.c_int32(int(A[0, 0])), C.c_int32(int(A[0, 1]))); res["init"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complex32_real2cmplx(P(o), C.c_int32(int(B[0, 0]))); res["real2cmplx"].append(o[0].copy())
+        o = np.zeros((L, 2), np.int32)
+        re_ = np.ascontiguousarray(A[:, 0]); im_ = np.ascontiguousarray(B[:, 1])
+        R.complexArry32_real2cmplx(P(o), P(re_), L); res["arry_real2cmplx"].append(o.copy())
+        o = np.zeros((L, 2), np.int32)
+        R.complexArry32_init(P(o), P(re_), P(im_), L); res["arry_init"].append(o.copy())
+    for k, v in res.items():
+        out[f"cx_{k}"] = np.array(v, np.int32)
+    np.savez_compressed(os.path.join(HERE, "ref_fft_complex.npz"), **out)
+
+
+# end-to-end NNSPClass_exec fixture: streams and where each is reset
+NNSP_NOISE = [(4096, 0x4E4E5350), (4096, 17), (30000, 5), (30000, 6), (300, 7), (1200, 8), (12000, 9), (64, 10)]
+NNSP_WAV_T, NNSP_WAV_RESET = 1000, 611      # a reset on an odd frame: slides restarts at 1
+NNSP_NOISE_T, NNSP_NOISE_RESET = 200, 97
+
+
+def nnsp_streams():
+    """[(pcm [T][160] int16, reset frame)]: the three wavs from sample 0, then
+    SplitMix64 streams (oracle.synthetic_pcm, one amplitude and seed each)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import synthetic_pcm
+    wz = np.load(os.path.join(HERE, "test_wavs.npz"))
+    out = [(wz[w][:NNSP_WAV_T * 160].reshape(NNSP_WAV_T, 160), NNSP_WAV_RESET) for w in WAVS]
+    for amp, seed in NNSP_NOISE:
+        out.append((synthetic_pcm(1, NNSP_NOISE_T, seed=seed, amp=amp)[0], NNSP_NOISE_RESET))
+    return out
+
+
+def nnsp() -> None:
+    """ref_nnsp_portable.npz: NNSPClass_exec (nn_speech.c:74-127) of the
+    reference's own portable build, frame by frame."""
+    R = C.CDLL(REF_NNSP_PORT_SO)
+    R.NNSPClass_exec.restype = C.c_int16
+    R.NeuralNetClass_exe.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int8]
+    streams = nnsp_streams()
+    out = {"noise_cfg": np.array(NNSP_NOISE, np.int64),
+           "cfg": np.array([NNSP_WAV_T, NNSP_WAV_RESET, NNSP_NOISE_T, NNSP_NOISE_RESET], np.int32)}
+    for name in ("vad", "kws", "s2i"):
+        data = N.ref_net(name)
+        for acc32 in (0, 1):
+            tag = f"{name}_{32 if acc32 else 64}"
+            pn = PortableNet(R, data, acc32)
+            mean = np.ascontiguousarray(data.mean, np.int32)
+            stdR = np.ascontiguousarray(data.stdR, np.int32)
+            thr, cnt = C.c_int16(N.THRESH_PROB), C.c_int16(N.THRESH_CNTS)
+            trig, feats, outs, counts, hs, cs = [], [], [], [], [], []
+            for pcm, reset_at in streams:
+                feat, inst = FeatureClass(), NNSPClass()
+                assert R.NNSPClass_init(C.byref(inst), C.byref(pn.net), C.byref(feat), C.c_char(bytes([N.NN_ID[name]])),
+                                        P(mean), P(stdR), C.byref(thr), C.byref(cnt)) == 0
+                R.NNSPClass_reset(C.byref(inst))
+                T = len(pcm)
+                tr = np.zeros(T, np.int16)
+                ft = np.zeros((T, 40), np.int16)
+                o3 = np.zeros((T, 3), np.int16)
+                ct = np.zeros((T, 8), np.int16)
+                for t in range(T):
+                    if t == reset_at:
+                        R.NNSPClass_reset(C.byref(inst))
+                    fr = np.ascontiguousarray(pcm[t], np.int16)
+                    tr[t] = R.NNSPClass_exec(C.byref(inst), P(fr))
+                    ft[t] = np.array(feat.normFeatContext[200:240], np.int16)
+                    o3[t] = list(inst.outputs)
+                    ct[t] = list(inst.counts_category)
+                trig.append(tr)
+                feats.append(ft)
+                outs.append(o3)
+                counts.append(ct)
+                hs.append(np.concatenate(pn.h) if pn.h else np.zeros(0, np.int16))
+                cs.append(np.concatenate(pn.c) if pn.c else np.zeros(0, np.int32))
+            cat = lambda a: np.concatenate(a, 0)   # noqa: E731  (streams back to back, frames of the wavs first)
+            out[f"{tag}_trig"], out[f"{tag}_outputs"], out[f"{tag}_counts"] = cat(trig), cat(outs), cat(counts)
+            out[f"{tag}_h"], out[f"{tag}_c"] = np.stack(hs), np.stack(cs)
+            if acc32:
+                assert np.array_equal(cat(feats), out[f"{name}_feats"])
+            else:
+                out[f"{name}_feats"] = cat(feats)
+    np.savez_compressed(os.path.join(HERE, "ref_nnsp_portable.npz"), **out)
+
+
 def wavs() -> None:
     import wave
     out = {}
@@ -454,9 +616,10 @@ def main() -> None:
     for so in (REF_SO, REF_NN_SO, REF_NETS_SO):
         if not os.path.exists(so):
             sys.exit("build oracle/_ref first (oracle/build_ref.sh)")
-    which = sys.argv[1:] or ["stages", "nets", "nn", "wavs", "fe_portable"]
+    which = sys.argv[1:] or ["stages", "nets", "nn", "wavs", "fe_portable", "fft_complex", "nnsp"]
     for w in which:   # nets before nn: nn re-packs the dumped reference nets
-        {"stages": stages, "nets": nets, "nn": nn, "wavs": wavs, "fe_portable": fe_portable}[w]()
+        {"stages": stages, "nets": nets, "nn": nn, "wavs": wavs, "fe_portable": fe_portable, "fft_complex": fft_complex,
+         "nnsp": nnsp}[w]()
     print("wrote", sorted(os.listdir(HERE)))
 
 

@@ -256,3 +256,85 @@ def test_nnsp_exec_portable(name):
         assert L.NNSPClass_exec(C.byref(inst), O.p(frame)) == o_trig[0, t], f"frame {t}"
         np.testing.assert_array_equal(np.ctypeslib.as_array(feat.normFeatContext)[200:240], o_feat[0, t])
     assert L.nnsp_legacy_status() == 0
+
+
+@pytest.fixture(scope="module")
+def gfc():
+    return np.load(os.path.join(GOLD, "ref_fft_complex.npz"))
+
+
+@pytest.mark.parametrize("num", [256, 512])
+def test_rfft_sizes_vs_reference(gfc, num):
+    """rfft(256) and rfft(512) on vectors up to the full int32 range, where
+    complex.c's clamps and the split's int32 wraps bind (fft.c:27-126)."""
+    L = _lib.lib()
+    for x, y in zip(gfc[f"rfft{num}_in"], gfc[f"rfft{num}_out"]):
+        xi = np.ascontiguousarray(x, np.int32)
+        keep = xi.copy()
+        out = np.zeros(num + 2, np.int32)
+        L.rfft(num, O.p(xi), O.p(out))
+        np.testing.assert_array_equal(out, y)
+        np.testing.assert_array_equal(xi, keep)
+    assert L.nnsp_legacy_status() == 0
+
+
+@pytest.mark.parametrize("e", range(9))
+def test_fft_every_size_vs_reference(gfc, e):
+    """fft(exp_nfft) for 0..8: radix-4 stages (8, 7), the radix-2 stage (7),
+    the bit-reversal copy alone (< 7); output and the in-place input."""
+    L = _lib.lib()
+    for x, y, xa in zip(gfc[f"fft{e}_in"], gfc[f"fft{e}_out"], gfc[f"fft{e}_in_after"]):
+        xi = np.ascontiguousarray(x, np.int32).copy()
+        out = np.zeros(2 << e, np.int32)
+        L.fft(e, O.p(xi), O.p(out))
+        np.testing.assert_array_equal(out, y, err_msg=f"fft({e}) output")
+        np.testing.assert_array_equal(xi, xa, err_msg=f"fft({e}) input afterwards")
+    assert L.nnsp_legacy_status() == 0
+
+
+def test_fft_rfft_unsupported_sizes_report():
+    L = _lib.lib()
+    x = np.zeros(2048, np.int32)
+    y = np.zeros(2048, np.int32)
+    L.rfft(1024, O.p(x), O.p(y))
+    assert L.nnsp_legacy_status() == -2   # NNSP_EUNSUPPORTED
+    L.nnsp_legacy_clear()
+    L.fft(9, O.p(x), O.p(y))
+    assert L.nnsp_legacy_status() == -2
+    L.nnsp_legacy_clear()
+
+
+def test_complex_helpers_vs_reference(gfc):
+    """complex.c's helpers (the drop-in complex.h), full-range operands."""
+    L = _lib.lib()
+    a, b, m, w, sh = gfc["cx_a"], gfc["cx_b"], gfc["cx_m"], gfc["cx_w16"], gfc["cx_shift"]
+    n = a.shape[1]
+    for c in range(len(a)):
+        A, B, M, W = (np.ascontiguousarray(v[c]) for v in (a, b, m, w))
+
+        def o():
+            return np.zeros((n, 2), np.int32)
+        r = o(); L.complex32_copy(O.p(r), O.p(A)); np.testing.assert_array_equal(r[0], gfc["cx_copy"][c])
+        r = o(); L.complex32_affine(O.p(r), O.p(M), O.p(A), int(sh[c]), n)
+        np.testing.assert_array_equal(r, gfc["cx_affine"][c])
+        r = o(); L.complex32_interprod(O.p(r), O.p(A), O.p(B), int(sh[c]), n)
+        np.testing.assert_array_equal(r[0], gfc["cx_interprod"][c])
+        r = o(); L.complex32_complex16_elmtprod(O.p(r), O.p(A), O.p(W), n)
+        np.testing.assert_array_equal(r, gfc["cx_elmtprod"][c])
+        r = o(); L.complex32_add(O.p(r), O.p(A), O.p(B)); np.testing.assert_array_equal(r[0], gfc["cx_add"][c])
+        r = o(); L.complexArry32_add(O.p(r), O.p(A), O.p(B), n); np.testing.assert_array_equal(r, gfc["cx_arry_add"][c])
+        r = o(); L.complex32_neg(O.p(r), O.p(A)); np.testing.assert_array_equal(r[0], gfc["cx_neg"][c])
+        Bc = B.copy()
+        r = o(); L.complex32_sub(O.p(r), O.p(A), O.p(Bc)); np.testing.assert_array_equal(r[0], gfc["cx_sub"][c])
+        np.testing.assert_array_equal(Bc[0], gfc["cx_sub_b"][c])   # b negated in place (complex.c:108-113)
+        r = o(); L.complex32_mul(O.p(r), O.p(A), O.p(B)); np.testing.assert_array_equal(r[0], gfc["cx_mul"][c])
+        r = o(); L.complex32_init(O.p(r), C.c_int32(int(A[0, 0])), C.c_int32(int(A[0, 1])))
+        np.testing.assert_array_equal(r[0], gfc["cx_init"][c])
+        r = o(); L.complex32_real2cmplx(O.p(r), C.c_int32(int(B[0, 0])))
+        np.testing.assert_array_equal(r[0], gfc["cx_real2cmplx"][c])
+        re_, im_ = np.ascontiguousarray(A[:, 0]), np.ascontiguousarray(B[:, 1])
+        r = o(); L.complexArry32_real2cmplx(O.p(r), O.p(re_), n)
+        np.testing.assert_array_equal(r, gfc["cx_arry_real2cmplx"][c])
+        r = o(); L.complexArry32_init(O.p(r), O.p(re_), O.p(im_), n)
+        np.testing.assert_array_equal(r, gfc["cx_arry_init"][c])
+    assert L.nnsp_legacy_status() == 0

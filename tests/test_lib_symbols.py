@@ -135,3 +135,54 @@ def test_reference_def_nets_compile_and_link_unchanged(tmp_path, acc32):
             rows = 4 * N if lstm else N
             kern = np.ctypeslib.as_array((C.c_int8 * (rows * K)).from_address(n.pt_kernel[i]))
             np.testing.assert_array_equal(kern, z[f"{name}_kernel{i}"])
+
+
+PORTABLE_APP = r"""
+#include <stdint.h>
+#include "fft.h"
+#include "complex.h"
+#include "spectrogram_module.h"
+/* a portable (ARM_OPTIMIZED=0) caller of the reference's fft.h / complex.h
+ * API: compiles against include/ and links; nothing is run (no GPU here) */
+int use(int32_t *x, void *y)
+{
+    COMPLEX32 a = {1, 2}, b = {3, 4}, o;
+    COMPLEX16 w = {5, 6};
+    rfft(512, x, y);
+    fft(7, x, y);
+    complex32_add(&o, &a, &b);
+    complex32_sub(&o, &a, &b);
+    complex32_mul(&o, &a, &b);
+    complex32_complex16_elmtprod(&o, &a, &w, 1);
+    complex32_interprod(&o, &a, &b, 0, 1);
+    complexArry32_print(&o, 1);
+    spec2pspec((int32_t *)y, x, 257);
+    return o.real;
+}
+"""
+
+
+def test_portable_fft_complex_headers_compile_and_link(tmp_path):
+    """include/fft.h and include/complex.h stand in for ns-nnsp/includes-api's
+    (fft.h:4-5, complex.h): a portable application compiles and links."""
+    import subprocess
+    src = tmp_path / "app.c"
+    src.write_text(PORTABLE_APP)
+    so = str(tmp_path / "libapp.so")
+    subprocess.check_call(["gcc", "-Wall", "-Werror", "-fPIC", "-shared", "-I", os.path.join(ROOT, "include"), str(src),
+                           "-L", os.path.dirname(_lib.LIB_PATH), "-lnnsp_mi355x", "-Wl,-z,defs",
+                           "-Wl,--allow-shlib-undefined", "-o", so])
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/ns-nnsp"), reason="reference absent")
+def test_complex_types_match_reference_header(tmp_path):
+    import subprocess
+    probe = ('#include <stdio.h>\n#include <stddef.h>\n#include "complex.h"\nint main(void){printf("%zu %zu %zu %zu\\n",'
+             ' sizeof(COMPLEX32), offsetof(COMPLEX32, imag), sizeof(COMPLEX16), offsetof(COMPLEX16, imag));}\n')
+    (tmp_path / "p.c").write_text(probe)
+    outs = []
+    for inc in (os.path.join(ROOT, "include"), "/root/reference/ns-nnsp/includes-api"):
+        exe = str(tmp_path / "p")
+        subprocess.check_call(["gcc", "-I", inc, str(tmp_path / "p.c"), "-o", exe])
+        outs.append(subprocess.check_output([exe]))
+    assert outs[0] == outs[1] == b"8 4 4 2\n"
