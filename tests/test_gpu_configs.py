@@ -176,15 +176,19 @@ def test_full_scale_batch_mode(name):
     eng.close()
 
 
-@pytest.mark.parametrize("window", [-1, 8])
-def test_full_scale_cascade_shared_and_cold(window):
+@pytest.mark.parametrize("weights,window", [("synth", -1), ("synth", 8), ("ref", -1)])
+def test_full_scale_cascade_shared_and_cold(weights, window):
+    """The cascade's shared and cold front ends on full-scale input.  With the
+    reference nets the full-scale input makes VAD and KWS alternate (KWS never
+    triggers, so S2I never runs); the seeded synthetic nets of the same shapes
+    run all three nets."""
     S, chunks = 64, [100, 37, 100]
     th = {"vad": (3000, 1), "kws": (6000, 1), "s2i": (9000, 1)}   # low thresholds: frequent resets
     pcm = _full_scale(S, sum(chunks), seed=9)
-    gnets = {n: NNSPBatch(ref_net(n), S, 100, thresh_prob=th[n][0], th_count=th[n][1]) for n in th}
+    gnets = {n: NNSPBatch(get_net(n, weights), S, 100, thresh_prob=th[n][0], th_count=th[n][1]) for n in th}
     gc = NNSPCascade(gnets, (1, 2, 0), 20, 15, 30, 12)
     gc.set_window(window)
-    oc = OracleCascade({n: OracleNet(ref_net(n), thresh_prob=th[n][0], th_count=th[n][1]) for n in th},
+    oc = OracleCascade({n: OracleNet(get_net(n, weights), thresh_prob=th[n][0], th_count=th[n][1]) for n in th},
                        (1, 2, 0), 20, 15, 30, 12)
     o_ran, o_det, o_o3, _ = oc.run(pcm)
     t0 = 0
@@ -195,7 +199,9 @@ def test_full_scale_cascade_shared_and_cold(window):
         np.testing.assert_array_equal(o3, o_o3[:, t0:t0 + Tc], err_msg=f"outputs3 chunk@{t0}")
         t0 += Tc
     gc.close()
-    # the cold mode ran: every net ran, and the nets switched many times
-    assert set(np.unique(o_ran)) == {0, 1, 2}, "not every net ran: vacuous"
+    # the cold mode ran: the nets switched many times (every switch resets the
+    # departing net; its next segment starts with cold frames)
+    want = {0, 1, 2} if weights == "synth" else {1, 2}
+    assert want <= set(np.unique(o_ran).tolist()), "nets did not switch: vacuous"
     switches = (np.diff(o_ran.astype(np.int16), axis=1) != 0).sum()
     assert switches > S, f"only {switches} net switches: the cold front end barely ran"
