@@ -214,6 +214,7 @@ class NetHandle:
         names = {0: "relu6_fix", 1: "tanh_fix", 2: "sigmoid_fix", 3: "linear_fix"}
         self.h, self.c = [None] * spec.nl, [None] * spec.nl
         for i, t in enumerate(spec.types):
+            a32 = acc32 or bool(spec.accs and spec.accs[i])   # per-layer layer_func (mixed nets)
             n.net_layer_type[i] = t
             n.qbit_kernel[i] = spec.qk[i]
             n.qbit_input[i] = spec.qi[i]
@@ -221,14 +222,14 @@ class NetHandle:
             n.activation_type[i] = {0: 0, 1: 1, 2: 2, 3: 3}[spec.acts[i]]
             n.act_func[i] = fn_addr(names[spec.acts[i]])
             if t == LSTM:
-                lf = "lstm_8x16_acc32b" if acc32 else "lstm_8x16"
+                lf = "lstm_8x16_acc32b" if a32 else "lstm_8x16"
                 N = spec.sizes[i + 1]
                 self.h[i] = np.zeros(N, np.int16)
                 self.c[i] = np.zeros(N, np.int32)
                 n.pt_hstate[i] = ptr(self.h[i])
                 n.pt_cstate[i] = ptr(self.c[i])
             else:
-                lf = "fc_8x16_acc32b" if acc32 else "fc_8x16"
+                lf = "fc_8x16_acc32b" if a32 else "fc_8x16"
             n.layer_func[i] = fn_addr(lf)
             w = np.ascontiguousarray(Wp[i]).view(np.int8)
             b = np.ascontiguousarray(Bp[i]).astype(np.int16)

@@ -85,10 +85,17 @@ static void plan_fast(nnsp_batch *b)
     const NnImage *g = &b->im.img;
     b->fast = 0;
     if (getenv("NNSP_FUSED_NN")) return;
-    if (g->n_lstm != 1) return;
+    /* the split kernels: one accumulator width (template), one LSTM of width
+     * <= NN_MAX_W (its state rows), prefix layers of <= 4 k-tiles and <= 256
+     * rows, suffix layers <= 128 wide (their LDS rows); anything else the
+     * reference runs goes to the fused nn_kernel */
+    if (g->n_lstm != 1 || g->mixed_acc) return;
     int li = -1;
     for (int i = 0; i < g->nl; ++i)
         if (g->L[i].type == NN_LSTM) li = i;
+    if (g->L[li].N > NN_MAX_W || g->L[li].K > 256) return;
+    for (int i = 0; i < li; ++i)
+        if (g->L[i].N > 256 || g->L[i].K > 256) return;
     for (int i = li + 1; i < g->nl; ++i)
         if (g->L[i].N > 128 || g->L[i].K > 128) return;
     const int shape = getenv("NNSP_GENERIC_SHAPE") ? NN_SHAPE_GENERIC : net_shape(g);
@@ -204,35 +211,27 @@ int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
     int e = nnsp_image_build(&b->im, L, nl, nn_id, thresh_prob, th_count, 0);
     if (e) goto fail;
     b->nout = b->im.img.nout;
-    /* NNSP_NET_STREAM_PRIO=1: the batch's stream at the device's highest
-     * priority (cascade experiments: the nets' rounds ahead of the look-ahead
-     * front end) */
-    int hi = getenv("NNSP_NET_STREAM_PRIO") != NULL;
-    {   /* NNSP_PRIO_NETS="0,2": only the batches of these NNSP_IDs at high priority */
-        const char *pn = getenv("NNSP_PRIO_NETS");
-        if (pn) {
-            hi = 0;
-            for (const char *q = pn; *q; ++q)
-                if (*q >= '0' && *q <= '9' && *q - '0' == nn_id) hi = 1;
-        }
-    }
-    if ((e = hi ? nnspk_stream_create_prio(&b->stream, 1) : nnspk_stream_create(&b->stream))) goto fail;
+    if ((e = nnspk_stream_create(&b->stream))) goto fail;
     for (int i = 0; i < 3; ++i)
         if ((e = nnspk_event_create(&b->ev[i]))) goto fail;
     if ((e = nnsp_image_upload(&b->im, b->stream))) goto fail;
     const size_t S = (size_t)n_streams, T = (size_t)max_frames;
     const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
+    /* h / c row stride: NN_MAX_W, or the widest LSTM rounded up to 8 */
+    b->hs = NN_MAX_W;
+    for (int i = 0; i < b->im.img.n_lstm; ++i)
+        if (b->im.img.lstm_n[i] > b->hs) b->hs = (b->im.img.lstm_n[i] + 7) / 8 * 8;
     if ((e = nnspk_malloc((void **)&b->d_mean, 40 * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_stdR, 40 * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_tail, S * 320 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_prev5, S * 200 * 2))) goto fail;
-    if ((e = nnspk_malloc((void **)&b->d_h, S * nls * NN_MAX_W * 2))) goto fail;
-    if ((e = nnspk_malloc((void **)&b->d_c, S * nls * NN_MAX_W * 4))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_h, S * nls * (size_t)b->hs * 2))) goto fail;
+    if ((e = nnspk_malloc((void **)&b->d_c, S * nls * (size_t)b->hs * 4))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_post, S * sizeof(NnPost)))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_feats, S * T * 40 * 2))) goto fail;
     if ((e = nnspk_malloc((void **)&b->d_mask, S))) goto fail;
     plan_fast(b);
-    b->ep32 = !b->im.img.acc32 && !getenv("NNSP_NO_EP32") && fits_int32(b, L, nl);
+    b->ep32 = !b->im.img.acc32 && !b->im.img.mixed_acc && !getenv("NNSP_NO_EP32") && fits_int32(b, L, nl);
     if (b->fast) {
         if ((e = nnspk_set_lds_limit())) goto fail;
         if (b->shape != NN_SHAPE_GENERIC) { /* x rows: int16, 16 * ceil(N / 16) per (stream, step) */
@@ -283,7 +282,7 @@ int nnsp_batch_reset(nnsp_batch *b, const uint8_t *mask)
     /* FeatureClass_setDefault + NeuralNetClass_setDefault + NNSPClass fields */
     TRY(nnspk_launch_fe_default(b->d_prev5, b->d_tail, b->d_mean, b->d_stdR, b->norm_shift, dm, b->S,
                                 b->stream));
-    TRY(nnspk_launch_nn_default(b->d_h, b->d_c, b->d_post, b->im.img.n_lstm ? b->im.img.n_lstm : 1,
+    TRY(nnspk_launch_nn_default(b->d_h, b->d_c, b->d_post, (b->im.img.n_lstm ? b->im.img.n_lstm : 1) * b->hs,
                                 dm, b->S, b->stream));
     return nnspk_sync(b->stream);
 }
@@ -388,11 +387,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
             if (need < blocks) blocks = (int)need;
         }
-        if (seg->phase != 2) TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
-        if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
-        if (seg->phase == 1) return 0;
-        for (int i = 0; i < 2; ++i)
-            if (seg->recur_wait[i]) TRY(nnspk_stream_wait(stream, seg->recur_wait[i]));
+        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
         f.a_off = b->rec_a_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;
@@ -409,6 +404,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         r.prev5 = b->d_prev5;
         r.h = b->d_h;
         r.c = b->d_c;
+        r.hs = b->hs;
         r.post = b->d_post;
         r.trig = trig;
         r.logits = logits;
@@ -475,7 +471,7 @@ int nnsp_batch_post_state(nnsp_batch *b, nnsp_post_state *out)
 size_t nnsp_batch_state_bytes(const nnsp_batch *b)
 {
     const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
-    return 320 * 2 + 200 * 2 + (size_t)nls * NN_MAX_W * 6 + sizeof(NnPost);
+    return 320 * 2 + 200 * 2 + (size_t)nls * b->hs * 6 + sizeof(NnPost);
 }
 
 static int state_xfer(nnsp_batch *b, void *host, int first, int count, int to_dev)
@@ -490,8 +486,8 @@ static int state_xfer(nnsp_batch *b, void *host, int first, int count, int to_de
         struct { void *dev; size_t n; } seg[5] = {
             {b->d_tail + s * 320, 640},
             {b->d_prev5 + s * 200, 400},
-            {b->d_h + s * nls * NN_MAX_W, (size_t)nls * NN_MAX_W * 2},
-            {b->d_c + s * nls * NN_MAX_W, (size_t)nls * NN_MAX_W * 4},
+            {b->d_h + s * nls * b->hs, (size_t)nls * b->hs * 2},
+            {b->d_c + s * nls * b->hs, (size_t)nls * b->hs * 4},
             {b->d_post + s, sizeof(NnPost)},
         };
         for (int k = 0; k < 5; ++k) {

@@ -79,20 +79,9 @@ struct nnsp_cascade {
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation) */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
-    /* XCD partition for chunks with a look-ahead front end: it runs on the
-     * CUs [0, part) of fe_stream while the nets' rounds run on the other
-     * CUs (own_ns); other chunks use the unmasked streams */
-    int part;                       /* CUs of the front end's partition (0: off) */
-    void *fe_stream;                /* look-ahead front end, CU-masked */
-    void *own_ns[3];                /* the nets' CU-masked streams */
-    int netpart;                    /* experiment NNSP_NET_CUS: own_ns for every chunk */
-    void *ev_fe_dep;                /* fe_stream waits for the cascade's stream there */
-    int ahead_on_fe;                /* the last look-ahead ran on fe_stream */
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
-    void *ev_pj[3];                 /* per net: its proj of the round done (proj join) */
-    int proj_join;                  /* rounds < proj_join: every net's recur waits for all three projs */
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
@@ -104,11 +93,6 @@ struct nnsp_cascade {
     int ahead_pending[2];
     float ahead_ms[2];
     int sfe_ahead;                  /* last chunk's shared front end ran in the previous call */
-    int ahead_blocks;               /* grid cap of the look-ahead front end (0: full) */
-    int ahead_fpw;                  /* its frames per wave (0: persistent grid) */
-    int ahead_after;                /* it starts after this many rounds of the nets */
-    int cold_first;                 /* all nets' cold front ends of a round before their NN kernels */
-    int vad_last;                   /* VAD's recurrence after S2I's and KWS's in each round */
     int window;                     /* frames per stream and round (0: to the chunk end) */
     int auto_window;                /* pick window per chunk from the last chunk's switch rate */
     int last_cuts;                  /* last chunk: segments cut by a net switch */
@@ -186,46 +170,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
     c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
-    {   /* experiment: NNSP_FE_FREE_CUS=N: the cascade's stream leaves N CUs to the nets */
-        const char *fc = getenv("NNSP_FE_FREE_CUS");
-        const char *fs = getenv("NNSP_FE_FREE_SPREAD");
-        e = fc ? nnspk_stream_create_cumask(&c->stream, atoi(fc), fs ? atoi(fs) : 1) : nnspk_stream_create(&c->stream);
-        if (e) goto fail;
-    }
-    {   /* experiment (off unless NNSP_PART_FE=F): the XCD partition of
-         * look-ahead chunks -- the look-ahead front end on F CUs (MI355X: 256
-         * CUs in 8 XCDs of 32, CU i on XCD i % 8; F = 192: 6 XCDs), the nets'
-         * rounds on the others.  With the cascade's own stream masked as well it
-         * measured +2.4 % (paired A/B); in this form, with the front end on a
-         * stream of its own so that the call returns before it ends, -7 %
-         * (profiles/r02/sched).  A partition that splits an XCD: -15 %. */
-        int cus = 0, clk = 0;
-        char arch[64];
-        if (nnspk_device_info(&cus, &clk, arch, (int)sizeof arch)) cus = 0;
-        const char *pf = getenv("NNSP_PART_FE");
-        c->part = pf ? atoi(pf) : 0;
-        if (c->part > 0 && c->part < cus) {
-            if ((e = nnspk_stream_create_cupart(&c->fe_stream, 0, c->part, 1))) goto fail;
-            for (int n = 0; n < 3; ++n)
-                if ((e = nnspk_stream_create_cupart(&c->own_ns[n], c->part, cus, 1))) goto fail;
-            if ((e = nnspk_event_create(&c->ev_fe_dep))) goto fail;
-        } else {
-            c->part = 0;
-        }
-        /* experiment (off unless NNSP_NET_CUS="lo:hi,lo:hi,lo:hi", nets in id
-         * order s2i, vad, kws; CU index space XCD-major, 32 per XCD): every
-         * round of each net on its own CUs (the front end stays unmasked) */
-        const char *nc = getenv("NNSP_NET_CUS");
-        c->netpart = 0;
-        if (!c->part && nc && cus > 0) {
-            int lo[3], hi[3];
-            if (sscanf(nc, "%d:%d,%d:%d,%d:%d", &lo[0], &hi[0], &lo[1], &hi[1], &lo[2], &hi[2]) == 6) {
-                for (int n = 0; n < 3; ++n)
-                    if ((e = nnspk_stream_create_cupart(&c->own_ns[n], lo[n], hi[n], 1))) goto fail;
-                c->netpart = 1;
-            }
-        }
-    }
+    if ((e = nnspk_stream_create(&c->stream))) goto fail;
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
@@ -236,9 +181,9 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
          * one stream (c->stream) to the three, so on a device with four
          * hardware queues (HIP's default) the look-ahead front end on
          * c->stream never shares an in-order queue with a net's rounds */
-        c->ns[n] = nets[n]->stream;   /* per chunk: own_ns[n] when partitioned */
-        if ((e = nnspk_event_create(&c->ev_join[n])) || (e = nnspk_event_create(&c->ev_pj[n])) ||
-            (e = nnspk_event_create(&c->ev_rnd[0][n])) || (e = nnspk_event_create(&c->ev_rnd[1][n])))
+        c->ns[n] = nets[n]->stream;
+        if ((e = nnspk_event_create(&c->ev_join[n])) || (e = nnspk_event_create(&c->ev_rnd[0][n])) ||
+            (e = nnspk_event_create(&c->ev_rnd[1][n])))
             goto fail;
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i)
@@ -340,18 +285,6 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
         c->debug = getenv("NNSP_CASCADE_DEBUG") != NULL;
-        const char *ab = getenv("NNSP_AHEAD_FE_BLOCKS");
-        c->ahead_blocks = ab ? atoi(ab) : 0;
-        const char *af = getenv("NNSP_AHEAD_FE_FPW");
-        c->ahead_fpw = af ? atoi(af) : 0;
-        const char *aa = getenv("NNSP_AHEAD_AFTER_ROUND");
-        c->ahead_after = aa ? atoi(aa) : (c->part ? 0 : 1);
-        const char *cf = getenv("NNSP_COLD_FIRST");
-        c->cold_first = cf ? atoi(cf) != 0 : 0;   /* measured: +1 % reference nets, -5 % synthetic */
-        const char *pj = getenv("NNSP_PROJ_JOIN");
-        c->proj_join = pj ? atoi(pj) : 0;
-        const char *vl = getenv("NNSP_VAD_LAST");
-        c->vad_last = vl ? atoi(vl) != 0 : 0;   /* measured: -2 % reference nets, -7 % synthetic */
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
             c->window = atoi(w);
@@ -389,18 +322,12 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     }
     for (int n = 0; n < 3; ++n) {
         nnspk_event_destroy(c->ev_join[n]);
-        nnspk_event_destroy(c->ev_pj[n]);
         nnspk_event_destroy(c->ev_rnd[0][n]);
         nnspk_event_destroy(c->ev_rnd[1][n]);
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
         c->ns[n] = NULL; /* the batch's stream, owned by the batch */
-        nnspk_stream_destroy(c->own_ns[n]);
-        c->own_ns[n] = NULL;
     }
-    if (c->fe_stream) nnspk_sync(c->fe_stream);
-    nnspk_stream_destroy(c->fe_stream);
-    nnspk_event_destroy(c->ev_fe_dep);
     nnspk_stream_destroy(c->stream);
     nnspk_event_destroy(c->ev_book);
     nnspk_host_free(c->h_book);
@@ -411,8 +338,6 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
-    if (c->fe_stream) TRY(nnspk_sync(c->fe_stream)); /* a look-ahead front end writes ring slots */
-    c->ahead_on_fe = 0;
     TRY(book_take(c));
     for (int i = 0; i < 3; ++i) TRY(nnsp_batch_reset(c->net[i], mask)); /* synchronous */
     const uint8_t *dm = NULL;
@@ -485,13 +410,9 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
 
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
-static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
-                    int wait_cold, void *const recur_wait[2], int phase)
+static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st)
 {
     const int timed = c->timing && r < MAX_TIMED;
-    if (wait_cold)
-        for (int m = 0; m < 3; ++m)
-            if (m != n) TRY(nnspk_stream_wait(st, c->ev_join[m]));
     nnsp_segment seg;
     memset(&seg, 0, sizeof seg);
     seg.list = c->d_list[r & 1][n];
@@ -508,14 +429,7 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
     seg.fs = a->fs[n];
     seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
     seg.ctl = c->fused ? a : NULL;
-    if (recur_wait) {
-        seg.recur_wait[0] = recur_wait[0];
-        seg.recur_wait[1] = recur_wait[1];
-    }
-    seg.phase = phase;
-    if (phase == 1) seg.proj_done = c->ev_pj[n];
     TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
-    if (phase == 1) return 0;
     DBG(st, "proj + recur", n, r);
     if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
     if (c->fused) {
@@ -543,21 +457,10 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         a->cold_list[n] = c->d_cold_list[(r + 1) & 1][n];
     }
     if (!c->serial && !c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
-    /* cold frames first: every net's cold front end is queued before any
-     * net's NN kernels may start (ev_join as the cold-done event), so the tiny
-     * cold launches do not wait behind the other nets' proj workgroups */
-    const int cold_first = c->fused && !c->serial && c->cold_first;
-    /* VAD last (experiment, NNSP_VAD_LAST=1): its recurrence waits for the
-     * S2I and KWS recurrences of the round, so that their 12-wave workgroups
-     * find whole CUs.  Measured slower: S2I and KWS alone still take 0.4-0.5 ms
-     * in round 0 (396 whole-CU workgroups on 256 CUs), and VAD's then follows. */
-    const int vad_last = c->fused && !c->serial && c->vad_last;
-    static const int order_vad_last[3] = {0, 2, 1}, order_plain[3] = {0, 1, 2};
-    const int *order = vad_last ? order_vad_last : order_plain;
-    /* proj join (NNSP_PROJ_JOIN=R: rounds < R): measured below */
-    const int pjoin = c->fused && !c->serial && !cold_first && !vad_last && r < c->proj_join;
-    for (int i = 0; i < 3; ++i) {
-        const int n = order[i];
+    /* (measured and dropped, profiles/r02/sched: every net's cold front end
+     * of a round before any net's NN kernels, VAD's recurrence after S2I's
+     * and KWS's, every recur behind all three projs -- each -2..-7 %) */
+    for (int n = 0; n < 3; ++n) {
         void *st = c->serial ? c->stream : c->ns[n];
         const int timed = c->timing && r < MAX_TIMED;
         if (c->fused) {
@@ -574,36 +477,8 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
-        if (cold_first) TRY(nnspk_event_record(c->ev_join[n], st));
-        else {
-            void *w[2] = {NULL, NULL};
-            if (vad_last && n == 1) {
-                w[0] = c->ev_rnd[r & 1][0];
-                w[1] = c->ev_rnd[r & 1][2];
-            }
-            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w, pjoin ? 1 : 0));
-        }
+        TRY(round_nn(c, a, r, n, T, cur, hist, st));
     }
-    if (pjoin)   /* every net's recur after all three projs of the round (they then run on a GPU of their own) */
-        for (int i = 0; i < 3; ++i) {
-            const int n = order[i];
-            void *st = c->ns[n];
-            void *w[2] = {NULL, NULL};
-            int k = 0;
-            for (int m = 0; m < 3; ++m)
-                if (m != n) w[k++] = c->ev_pj[m];
-            TRY(round_nn(c, a, r, n, T, cur, hist, st, 0, w, 2));
-        }
-    if (cold_first)
-        for (int i = 0; i < 3; ++i) {
-            const int n = order[i];
-            void *w[2] = {NULL, NULL};
-            if (vad_last && n == 1) {
-                w[0] = c->ev_rnd[r & 1][0];
-                w[1] = c->ev_rnd[r & 1][2];
-            }
-            TRY(round_nn(c, a, r, n, T, cur, hist, c->ns[n], 1, w, 0));
-        }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
 }
@@ -625,10 +500,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
 {
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
-    if (ahead) {
-        fa.max_blocks = c->ahead_blocks;
-        fa.wave_frames = c->ahead_fpw;
-    }
+    (void)ahead;
     fa.pcm = pcm;
     fa.tail = tail;
     fa.tail_stride = tail_stride;
@@ -745,19 +617,10 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
     TRY(nnspk_event_record(c->ev[0], c->stream)); /* the counters (d_zero) were cleared by the last chunk */
-    /* a look-ahead front end of the last call on fe_stream: this chunk's work
-     * (its features, or, if it was not used, its ring slots) comes after it */
-    if (c->ahead_on_fe) {
-        TRY(nnspk_stream_wait(c->stream, c->ev_ahead[k & 1][1]));
-        c->ahead_on_fe = 0;
-    }
     /* look-ahead: the next chunk's shared front end runs while this chunk's
      * rounds run (it writes ring slots and a history buffer this chunk does not
-     * read; its STFT tail is this chunk's last two frames).  With the XCD
-     * partition it runs on fe_stream's CUs and the nets on theirs. */
+     * read; its STFT tail is this chunk's last two frames) */
     const int ahead = next_pcm && T >= 2 && T >= c->H && next_T >= c->H && c->fused && !c->serial;
-    const int part = ahead && c->part > 0;
-    for (int n = 0; n < 3; ++n) c->ns[n] = part || c->netpart ? c->own_ns[n] : c->net[n]->stream;
     /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
@@ -783,36 +646,24 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     DBG(c->stream, "casc_begin", -1, -1);
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
     int ahead_launched = 0;
-    /* the look-ahead front end starts once the nets' first ahead_after rounds
-     * (the bulk of the chunk's NN work) are queued behind: running beside
-     * them from the start it slowed them more than it gained */
-#define LAUNCH_AHEAD()                                                                                         \
-    do {                                                                                                       \
-        const int q_ = (int)((k + 1) & 1);                                                                     \
-        TRY(ahead_read(c, q_, 1)); /* slot q_'s last front end (two chunks ago) is long done */               \
-        void *fs_ = part ? c->fe_stream : c->stream;                                                           \
-        if (part) {                                                                                            \
-            TRY(nnspk_event_record(c->ev_fe_dep, c->stream));                                                  \
-            TRY(nnspk_stream_wait(fs_, c->ev_fe_dep));                                                         \
-        }                                                                                                      \
-        TRY(nnspk_event_record(c->ev_ahead[q_][0], fs_));                                                      \
-        TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring,     \
-                      k + 1, 1, fs_));                                                                         \
-        TRY(nnspk_event_record(c->ev_ahead[q_][1], fs_));                                                      \
-        c->ahead_pending[q_] = 1;                                                                              \
-        c->ahead_on_fe = part;                                                                                 \
-        ahead_launched = 1;                                                                                    \
-    } while (0)
-    if (ahead && c->ahead_after <= 0) LAUNCH_AHEAD();
-    /* rounds run without host round trips: launch as many as the last chunk
-     * needed, then check the next round's list lengths (one read-back) */
+    /* the look-ahead front end starts once the nets' first round (the bulk of
+     * the chunk's NN work) is done: running beside it from the start, or with
+     * its workgroups capped or short-lived, or on a CU partition, it slowed
+     * the rounds more than it gained (profiles/r02/sched) */
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
         for (; r < R; ++r) {
             TRY(launch_round(c, &a, r, pcm, T, hist));
-            if (ahead && !ahead_launched && r + 1 >= c->ahead_after) {
+            if (ahead && !ahead_launched) {
                 for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[r & 1][n]));
-                LAUNCH_AHEAD();
+                const int q = (int)((k + 1) & 1);
+                TRY(ahead_read(c, q, 1)); /* slot q's last front end (two chunks ago) is long done */
+                TRY(nnspk_event_record(c->ev_ahead[q][0], c->stream));
+                TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring,
+                              k + 1, 1, c->stream));
+                TRY(nnspk_event_record(c->ev_ahead[q][1], c->stream));
+                c->ahead_pending[q] = 1;
+                ahead_launched = 1;
             }
         }
         TRY(join_rounds(c, r));
@@ -907,7 +758,6 @@ int nnsp_cascade_sync(nnsp_cascade *c)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
-    if (c->fe_stream) TRY(nnspk_sync(c->fe_stream));
     TRY(book_take(c));
     for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
     return 0;

@@ -68,6 +68,7 @@ struct nnsp_batch {
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int shape;                        /* NN_SHAPE_* compiled split-path shape */
     int ep32;                         /* acc64 net that provably fits int32 accumulators */
+    int hs;                           /* h / c elements per LSTM row of the state (NN_MAX_W or wider) */
     int32_t *d_gx;                    /* generic shape: proj -> recur exact Wx.x sums */
     int16_t *d_xg;                    /* compiled shapes: proj -> recur LSTM inputs x */
     long long rec_a_off;              /* first byte of the image recur stages into LDS */
@@ -91,9 +92,6 @@ typedef struct {
     int16_t *detected, *outputs3;
     int net_id;
     const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
-    void *recur_wait[2];       /* events the stream waits for between proj and recur (NULL: none) */
-    int phase;                 /* split path: 0 proj + recur, 1 proj only, 2 recur only */
-    void *proj_done;           /* non-NULL: recorded on the stream after proj */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

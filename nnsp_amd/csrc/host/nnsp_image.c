@@ -275,9 +275,13 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
     for (int i = 0; i < nl; ++i) {
         const nnsp_layer_desc *d = &L[i];
         NnLayer *y = &g->L[i];
-        if (d->K <= 0 || d->N <= 0 || d->K > NN_MAX_K) {
-            nnsp_set_error("layer %d: width %d->%d outside the engine's 1..%d", i, d->K, d->N,
-                           NN_MAX_K);
+        /* the reference runs any stack whose widths fit its 300-element
+         * int16 activation buffers (neural_nets.c:9-10); a linear layer
+         * writes int32, 150 of them */
+        const int lin = d->type == NN_FC && d->act == 3;
+        if (d->K <= 0 || d->N <= 0 || d->K > NN_MAX_WIDTH || d->N > (lin ? NN_MAX_LIN : NN_MAX_WIDTH)) {
+            nnsp_set_error("layer %d: width %d->%d outside the reference's activation buffers (1..%d int16, "
+                           "%d int32 for a linear layer)", i, d->K, d->N, NN_MAX_WIDTH, NN_MAX_LIN);
             return NNSP_EUNSUPPORTED;
         }
         if (i > 0 && d->K != L[i - 1].N) {
@@ -290,11 +294,12 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
         y->act = d->act;
         y->nkt = (d->K + 63) / 64;
         y->has_bias = d->B != NULL;
+        y->acc32 = d->acc32;
         y->ep_off = rows_total;
         y->a_off = (int64_t)a_bytes;
         if (d->type == NN_LSTM) {
-            if (d->N > NN_MAX_W || n_lstm >= NN_MAX_LSTM) {
-                nnsp_set_error("layer %d: LSTM width %d / count over engine limits", i, d->N);
+            if (n_lstm >= NN_MAX_LSTM) {
+                nnsp_set_error("layer %d: more than %d LSTM layers", i, NN_MAX_LSTM);
                 return NNSP_EUNSUPPORTED;
             }
             g->lstm_n[n_lstm++] = d->N;
@@ -314,10 +319,6 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
             y->bias_sh = qs2 - d->qb;
             y->out_sh = 15 - qs2;
         } else {
-            if (d->N > 256) {
-                nnsp_set_error("layer %d: FC width %d > 256", i, d->N);
-                return NNSP_EUNSUPPORTED;
-            }
             y->nrt = (d->N + 15) / 16;
             y->rows = d->N;
             a_bytes += (size_t)y->nrt * y->nkt * 1024;
@@ -335,22 +336,20 @@ int nnsp_image_build(nnsp_image *im, const nnsp_layer_desc *L, int nl, int nn_id
     }
     g->n_lstm = n_lstm;
     g->nout = L[nl - 1].N;
-    g->acc32 = L[0].acc32;
-    for (int i = 1; i < nl; ++i)
-        if (L[i].acc32 != g->acc32) {
-            nnsp_set_error("mixed acc32 / acc64 layers are not supported");
-            return NNSP_EUNSUPPORTED;
-        }
-    /* streaming engines keep the last layer's row per stream (<= NN_MAX_OUT);
-     * a direct image (one NeuralNetClass_exe / fc_8x16 call) returns the raw
-     * activation row: 256 int16 or 128 int32 (linear) */
-    for (int i = 0; i < nl; ++i)
-        if (L[i].type == NN_FC && L[i].act == 3 && L[i].N > NN_MAX_K / 2) {
-            nnsp_set_error("layer %d: linear FC width %d > %d (int32 outputs)", i, L[i].N, NN_MAX_K / 2);
-            return NNSP_EUNSUPPORTED;
-        }
-    if (!direct && L[nl - 1].type == NN_FC && g->nout > NN_MAX_OUT) {
-        nnsp_set_error("output width %d > %d", g->nout, NN_MAX_OUT);
+    /* every layer its own accumulator width (layer_func[i]); acc32 = all
+     * layers _acc32b, mixed_acc = both kinds (the fused path only) */
+    g->acc32 = 1;
+    g->mixed_acc = 0;
+    for (int i = 0; i < nl; ++i) {
+        g->acc32 &= L[i].acc32 != 0;
+        if (L[i].acc32 != L[0].acc32) g->mixed_acc = 1;
+    }
+    /* NNSPClass_exec copies the last layer into its static int32_t
+     * output[50] (nn_speech.c:78, neural_nets.c:152-167): 50 int32 or 100
+     * int16; a direct image (one NeuralNetClass_exe / fc_8x16 call) returns
+     * the whole activation row */
+    if (!direct && g->nout > (L[nl - 1].type == NN_FC && L[nl - 1].act == 3 ? NN_MAX_OUT_LIN : NN_MAX_OUT)) {
+        nnsp_set_error("output width %d exceeds NNSPClass_exec's output buffer (50 int32 / 100 int16)", g->nout);
         return NNSP_EUNSUPPORTED;
     }
     im->a_bytes = a_bytes;

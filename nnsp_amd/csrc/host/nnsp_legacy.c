@@ -259,38 +259,52 @@ static img_node *net_image(const NeuralNetClass *net)
     return img_add(net, NULL, NULL, NULL, ik, bytes, L, nl, lin);
 }
 
-/* LSTM h/c of a NeuralNetClass <-> device rows [l][NN_MAX_W] */
-static void net_state_up(const NeuralNetClass *net, int16_t **dh, int32_t **dc)
+/* LSTM h/c of a NeuralNetClass <-> device rows [l][hs] (hs: the widest
+ * LSTM rounded up to 8; NnRun.hs) */
+static int net_hs(const NeuralNetClass *net)
 {
-    int16_t hs[NN_MAX_LSTM][NN_MAX_W];
-    int32_t cs[NN_MAX_LSTM][NN_MAX_W];
-    memset(hs, 0, sizeof hs);
-    memset(cs, 0, sizeof cs);
+    int hs = 8;
+    for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i)
+        if (net->net_layer_type[i] == lstm && net->size_layer[i + 1] > hs) hs = (net->size_layer[i + 1] + 7) / 8 * 8;
+    return hs;
+}
+
+static void net_state_up(const NeuralNetClass *net, int hs, int16_t **dh, int32_t **dc)
+{
+    static int16_t h[NN_MAX_LSTM * (NN_MAX_WIDTH + 8)];
+    static int32_t c[NN_MAX_LSTM * (NN_MAX_WIDTH + 8)];
+    memset(h, 0, sizeof h);
+    memset(c, 0, sizeof c);
     int l = 0;
     for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
         if (net->net_layer_type[i] == lstm) {
             const int N = net->size_layer[i + 1];
-            memcpy(hs[l], net->pt_hstate[i], (size_t)N * 2);
-            memcpy(cs[l], net->pt_cstate[i], (size_t)N * 4);
+            memcpy(h + (size_t)l * hs, net->pt_hstate[i], (size_t)N * 2);
+            memcpy(c + (size_t)l * hs, net->pt_cstate[i], (size_t)N * 4);
             ++l;
         }
-    *dh = (int16_t *)up(hs, sizeof hs);
-    *dc = (int32_t *)up(cs, sizeof cs);
+    *dh = (int16_t *)up(h, (size_t)(l ? l : 1) * hs * 2);
+    *dc = (int32_t *)up(c, (size_t)(l ? l : 1) * hs * 4);
 }
 
-static void net_state_down(NeuralNetClass *net, const int16_t *dh, const int32_t *dc)
+static void net_state_down(NeuralNetClass *net, int hs, const int16_t *dh, const int32_t *dc)
 {
-    int16_t hs[NN_MAX_LSTM][NN_MAX_W];
-    int32_t cs[NN_MAX_LSTM][NN_MAX_W];
-    down(hs, dh, sizeof hs);
-    down(cs, dc, sizeof cs);
+    static int16_t h[NN_MAX_LSTM * (NN_MAX_WIDTH + 8)];
+    static int32_t c[NN_MAX_LSTM * (NN_MAX_WIDTH + 8)];
+    int nls = 0;
+    for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i) nls += net->net_layer_type[i] == lstm;
+    if (nls > NN_MAX_LSTM) nls = NN_MAX_LSTM;
+    if (nls) {
+        down(h, dh, (size_t)nls * hs * 2);
+        down(c, dc, (size_t)nls * hs * 4);
+    }
     fin();
     int l = 0;
     for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
         if (net->net_layer_type[i] == lstm) {
             const int N = net->size_layer[i + 1];
-            memcpy(net->pt_hstate[i], hs[l], (size_t)N * 2);
-            memcpy(net->pt_cstate[i], cs[l], (size_t)N * 4);
+            memcpy(net->pt_hstate[i], h + (size_t)l * hs, (size_t)N * 2);
+            memcpy(net->pt_cstate[i], c + (size_t)l * hs, (size_t)N * 4);
             ++l;
         }
 }
@@ -346,8 +360,8 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
     memset(in_pad, 0, sizeof in_pad);
     memcpy(in_pad, input, (size_t)dim_input * 2);
     int16_t *din = (int16_t *)up(in_pad, sizeof in_pad);
-    int16_t hs[NN_MAX_W];
-    int32_t cs[NN_MAX_W];
+    int16_t hs[NN_MAX_K];
+    int32_t cs[NN_MAX_K];
     memset(hs, 0, sizeof hs);
     memset(cs, 0, sizeof cs);
     if (type == NN_LSTM) {
@@ -361,6 +375,7 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
     memset(&r, 0, sizeof r);
     r.S = 1; r.T = 1; r.mode = NN_MODE_DIRECT; r.nl_run = 1;
     r.direct_in = din; r.h = dh; r.c = dc; r.logits = dout; r.out_stride = NN_MAX_K;
+    r.hs = NN_MAX_K;
     CK(nnspk_launch_nn(&n->im.img, &r, G.stream));
     down(p_output, dout, (size_t)dim_output * (n->out_linear ? 4 : 2));
     if (type == NN_LSTM) {
@@ -448,16 +463,18 @@ static void NeuralNetClass_exe_impl(NeuralNetClass *pt_inst, int16_t *input, int
     int16_t *din = (int16_t *)up(in_pad, sizeof in_pad);
     int16_t *dh;
     int32_t *dc;
-    net_state_up(pt_inst, &dh, &dc);
+    const int hs = net_hs(pt_inst);
+    net_state_up(pt_inst, hs, &dh, &dc);
     int32_t *dout = (int32_t *)up(NULL, NN_MAX_K * 4);
     NnRun r;
     memset(&r, 0, sizeof r);
     r.S = 1; r.T = 1; r.mode = NN_MODE_DIRECT; r.nl_run = nl;
     r.direct_in = din; r.h = dh; r.c = dc; r.logits = dout; r.out_stride = NN_MAX_K;
+    r.hs = hs;
     CK(nnspk_launch_nn(&n->im.img, &r, G.stream));
     const int lin = pt_inst->activation_type[nl - 1] == linear;
     down(output, dout, (size_t)pt_inst->size_layer[nl] * (lin ? 4 : 2));
-    net_state_down(pt_inst, dh, dc);
+    net_state_down(pt_inst, hs, dh, dc);
 }
 
 /* ---------------------------------------------------------------------------
@@ -816,7 +833,8 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     r.S = 1; r.T = 1; r.mode = NN_MODE_STREAM; r.nl_run = img.nl;
     r.feats = a.feats;
     r.prev5 = (const int16_t *)up(fe->normFeatContext + 40, 400);
-    net_state_up(net, &r.h, &r.c);
+    r.hs = net_hs(net);
+    net_state_up(net, r.hs, &r.h, &r.c);
     r.post = up(&ps, sizeof ps);
     r.trig = (int16_t *)up(NULL, 2);
     CK(nnspk_launch_nn(&img, &r, G.stream));
@@ -824,7 +842,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     down(f5, a.feats, 80);
     down(fe->feature, a.dbg_log, 160);
     down(&ps, r.post, sizeof ps);
-    net_state_down(net, r.h, r.c); /* syncs */
+    net_state_down(net, r.hs, r.h, r.c); /* syncs */
     memmove(fe->normFeatContext, fe->normFeatContext + 40, 200 * 2);
     memcpy(fe->normFeatContext + 200, f5, 80);
     memmove(fe->state_stftModule.dataBuffer, fe->state_stftModule.dataBuffer + 160, 320 * 2);

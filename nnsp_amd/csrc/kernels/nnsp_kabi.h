@@ -10,10 +10,13 @@ extern "C" {
 #endif
 
 #define NN_MAX_LAYERS 10
-#define NN_MAX_LSTM 2   /* LSTM layers per net */
-#define NN_MAX_W 128    /* LSTM width; also the h/c row stride in device state */
-#define NN_MAX_K 256    /* FC / LSTM input width (4 MFMA k-tiles) */
-#define NN_MAX_OUT 64   /* width of the last layer */
+#define NN_MAX_LSTM 10   /* LSTM layers per net (any layer may be one) */
+#define NN_MAX_WIDTH 300 /* layer widths in int16: neural_nets.c's input0/1[300] (:9-10) */
+#define NN_MAX_LIN 150   /* a linear layer's int32 outputs in those buffers */
+#define NN_MAX_K 320     /* padded widths: 5 MFMA k-tiles of 64 */
+#define NN_MAX_W 128     /* the split path's LSTM width and h/c row stride (fused path: NnRun.hs) */
+#define NN_MAX_OUT 100   /* NNSPClass_exec's last layer: static int32_t output[50] (nn_speech.c:78) */
+#define NN_MAX_OUT_LIN 50
 #define NN_FC 0
 #define NN_LSTM 1
 /* compiled shapes of the split NN path (nnsp_fast.hip): FC(tanh, K 240) ->
@@ -65,9 +68,6 @@ typedef struct {
     int16_t *hist_out;
     int32_t tail_stride;      /* samples between streams' tails (0: 320, a [S][320] buffer; a chunk's
                                  last two frames: T * 160) */
-    int32_t max_blocks;       /* > 0: cap on the grid */
-    int32_t wave_frames;      /* > 0: frames per wave (short-lived workgroups: a look-ahead front end
-                                 yields CU slots to the nets' kernels as it goes); 0: persistent grid */
     int32_t port;             /* 1: the ARM_OPTIMIZED=0 build's front end (row N4): Frac15 window,
                                  fft.c's rfft, spec2pspec >> 15 */
     long long *dbg_clk;       /* development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0 of
@@ -116,7 +116,7 @@ typedef struct {
     int32_t has_bias, bias_sh, out_sh; /* affine_Krows epilogue */
     int32_t xs_sh;       /* LSTM: shift_64b(acc, qi_rec - qi) on the input part */
     int32_t ep_off;      /* row offset into wsum / wsum_r / bias */
-    int32_t pad;
+    int32_t acc32;       /* this layer's layer_func is the _acc32b twin (int32 wrap, shift_32b) */
     int64_t a_off, ar_off; /* byte offsets of the MFMA A fragments */
 } NnLayer;
 
@@ -125,8 +125,8 @@ typedef struct {
     const int32_t *wsum;   /* per row: 128 * sum_k W (hi/lo split correction) */
     const int32_t *wsum_r; /* per row: 128 * sum_k W_rec */
     const int16_t *bias;   /* per row (re-tiled order for LSTM) */
-    int32_t nl, acc32, nout, n_lstm;
-    int32_t nn_id, thresh_prob, th_count, pad;
+    int32_t nl, acc32, nout, n_lstm;   /* acc32: every layer is an _acc32b layer */
+    int32_t nn_id, thresh_prob, th_count, mixed_acc; /* mixed_acc: fc_8x16 and _acc32b layers mixed */
     int32_t lstm_n[NN_MAX_LSTM];
     NnLayer L[NN_MAX_LAYERS];
 } NnImage;
@@ -136,12 +136,13 @@ typedef struct {
     const int16_t *feats;     /* [S][T][40] */
     const int16_t *prev5;     /* [S][5][40] */
     const int16_t *direct_in; /* [S][NN_MAX_K] (DIRECT mode) */
-    int16_t *h;               /* [S][n_lstm][NN_MAX_W] */
-    int32_t *c;               /* [S][n_lstm][NN_MAX_W] */
+    int16_t *h;               /* [S][n_lstm][hs] */
+    int32_t *c;               /* [S][n_lstm][hs] */
     void *post;               /* [S] post-processing state (32 B each) */
     int16_t *trig;            /* [S][T] NNSPClass_exec return value per frame */
     int32_t *logits;          /* STREAM: [S][T][nout] (NN frames only); DIRECT: [S][out_stride] */
-    int32_t out_stride, pad;
+    int32_t out_stride;
+    int32_t hs;               /* h / c elements per LSTM row (>= the widest LSTM, multiple of 8) */
 } NnRun;
 
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
@@ -244,7 +245,7 @@ int nnspk_launch_post(int nn_id, int thresh_prob, int th_count, void *post, int3
 int nnspk_launch_fe_default(int16_t *prev5, int16_t *tail, const int32_t *mean,
                             const int32_t *stdR, int norm_shift, const uint8_t *mask, int n,
                             void *stream);
-int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int n_lstm, const uint8_t *mask,
+int nnspk_launch_nn_default(int16_t *h, int32_t *c, void *post, int row, const uint8_t *mask,
                             int n, void *stream);
 size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape);
 int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, int waves, void *stream);
@@ -271,9 +272,6 @@ const char *nnspk_error_string(int e);
 int nnspk_stream_create(void **s);
 /* high != 0: the device's greatest stream priority (its kernels' workgroups
  * are dispatched ahead of normal-priority streams' when both wait) */
-int nnspk_stream_create_prio(void **s, int high);
-int nnspk_stream_create_cumask(void **s, int free_cus, int spread);
-int nnspk_stream_create_cupart(void **s, int lo, int hi, int spread);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);

@@ -928,16 +928,17 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
 }
 
 // ============================================================================
-// NN: generic fc / lstm stack on int8 MFMA
+// NN: generic fc / lstm stack on int8 MFMA (the fused path: any stack the
+// reference's NeuralNetClass_exe runs -- widths up to its 300-element
+// activation buffers, neural_nets.c:9-10, any number of LSTM layers, each
+// layer with its own accumulator width)
 // ============================================================================
-#define NN_ASTRIDE 264   // int16 per stream row of an activation buffer (256 + pad)
-#define NN_HSTRIDE 136   // int16 per stream row of an LSTM h buffer (128 + pad)
-#define NN_CW 128        // int32 per stream row of an LSTM c buffer
+#define NN_KT (NN_MAX_K / 64)         // k tiles of the widest layer input
+#define NN_ASTRIDE (NN_MAX_K + 8)     // int16 per stream row of an activation / h buffer (+pad)
 
 struct alignas(16) NnLds {
-    int16_t act[2][16][NN_ASTRIDE];
-    int16_t h[NN_MAX_LSTM][16][NN_HSTRIDE];
-    int32_t c[NN_MAX_LSTM][16][NN_CW];
+    int16_t act[2][16][NN_ASTRIDE];   // layer input / output, ping-pong (the reference's input0/1)
+    int16_t h[16][NN_ASTRIDE];        // the current LSTM layer's h (its B operand), staged per step
     int16_t tanh_tbl[384];
     int32_t slides[16];
     int32_t active[16];
@@ -945,14 +946,14 @@ struct alignas(16) NnLds {
 
 __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
                               int16_t* out, const int16_t* tt, int lane) {
-    v4i bh[4], bl[4];
-    load_b<4>(in, NN_ASTRIDE, Ly.nkt, lane, bh, bl);
+    v4i bh[NN_KT], bl[NN_KT];
+    load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bh, bl);
     const int sc = lane & 15, q = lane >> 4;
     const uint8_t* A = img.A + Ly.a_off;
     for (int rt = 0; rt < Ly.nrt; ++rt) {
         v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < NN_KT; ++kt)
             if (kt < Ly.nkt) {
                 const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
                 ah = mfma8(w, bh[kt], ah);
@@ -963,7 +964,7 @@ __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16
             const int row = 16 * rt + 4 * q + i;
             if (row >= Ly.rows) continue;
             const int32_t sum = (ah[i] << 8) + al[i] + img.wsum[Ly.ep_off + row];
-            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, img.acc32);
+            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, Ly.acc32);
             if (Ly.act == ACT_LINEAR)
                 reinterpret_cast<int32_t*>(out + sc * NN_ASTRIDE)[row] = v;
             else
@@ -975,27 +976,29 @@ __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16
 // lstm_8x16 (lstm.c:15-214): per 4-unit group, gates i,j,f,o; every group
 // reads the previous h (T6).  Rows are re-tiled so that lane group q of row
 // tile rt holds gates i,j,f,o of unit 4*rt+q in its 4 accumulator registers.
+// h comes staged in hbuf; the cell state row of the lane's stream (cg, NULL
+// for a padding stream) stays in HBM: lane (sc, q) owns units 4*rt + q.
 __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
-                                int16_t* out, int16_t* hbuf, int32_t* cbuf, const int16_t* tt,
+                                int16_t* out, const int16_t* hbuf, int32_t* cg, const int16_t* tt,
                                 int lane, bool commit) {
-    v4i bxh[4], bxl[4], bhh[2], bhl[2];
-    load_b<4>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
-    load_b<2>(hbuf, NN_HSTRIDE, Ly.nkt_r, lane, bhh, bhl);
+    v4i bxh[NN_KT], bxl[NN_KT], bhh[NN_KT], bhl[NN_KT];
+    load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
+    load_b<NN_KT>(hbuf, NN_ASTRIDE, Ly.nkt_r, lane, bhh, bhl);
     const int sc = lane & 15, q = lane >> 4;
     const uint8_t* A = img.A + Ly.a_off;
     const uint8_t* Ar = img.A + Ly.ar_off;
-    const int acc32 = img.acc32;
+    const int acc32 = Ly.acc32;
     for (int rt = 0; rt < Ly.nrt; ++rt) {
         v4i xh = {0, 0, 0, 0}, xl = {0, 0, 0, 0}, hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
 #pragma unroll
-        for (int kt = 0; kt < 4; ++kt)
+        for (int kt = 0; kt < NN_KT; ++kt)
             if (kt < Ly.nkt) {
                 const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
                 xh = mfma8(w, bxh[kt], xh);
                 xl = mfma8(w, bxl[kt], xl);
             }
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
+        for (int kt = 0; kt < NN_KT; ++kt)
             if (kt < Ly.nkt_r) {
                 const v4i w = load_frag(Ar + (size_t)(rt * Ly.nkt_r + kt) * 1024, lane);
                 hh = mfma8(w, bhh[kt], hh);
@@ -1019,10 +1022,10 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
             const int32_t v = affine_out(pre, img.bias[Ly.ep_off + row], Ly, acc32);
             g[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
         }
-        const int32_t c_old = cbuf[sc * NN_CW + u];
+        const int32_t c_old = cg ? cg[u] : 0;
         const int32_t c_new = sat32(((int64_t)g[0] * g[1] + (int64_t)g[2] * c_old) >> 15);
         const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
-        if (commit) cbuf[sc * NN_CW + u] = c_new;
+        if (commit && cg) cg[u] = c_new;
         out[sc * NN_ASTRIDE + u] = hv;
     }
 }
@@ -1035,16 +1038,9 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
     const int s = s0 + sc;
     const bool valid = s < r.S;
     for (int i = lane; i < 384; i += 64) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
-    // ---- LSTM state in (neural_nets.c:27-42 layout: h int16[N], c int32[N])
-    for (int l = 0; l < img.n_lstm; ++l) {
-        const int N = img.lstm_n[l];
-        for (int idx = lane; idx < 16 * N; idx += 64) {
-            const int st = idx / N, u = idx - st * N, gs = s0 + st;
-            const bool ok = gs < r.S;
-            sm.h[l][st][u] = ok ? r.h[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] : (int16_t)0;
-            sm.c[l][st][u] = ok ? r.c[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] : 0;
-        }
-    }
+    // LSTM state rows (neural_nets.c:27-42 layout: h int16[N], c int32[N]) of
+    // stream gs, layer l: r.h / r.c + (gs * n_lstm + l) * hs
+    const size_t hs = (size_t)r.hs;
     PostState ps = {};
     if (lane < 16 && valid && r.post) ps = reinterpret_cast<const PostState*>(r.post)[s];
     if (lane < 16) sm.slides[lane] = (valid && r.post) ? ps.slides : 1;
@@ -1087,13 +1083,19 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
             const int16_t* in = &sm.act[i & 1][0][0];
             int16_t* out = &sm.act[(i + 1) & 1][0][0];
             if (Ly.type == NN_LSTM) {
-                lstm_layer_mfma(img, Ly, in, out, &sm.h[lst][0][0], &sm.c[lst][0][0], sm.tanh_tbl,
-                                lane, active);
+                const int N = Ly.N;
+                for (int idx = lane; idx < 16 * N; idx += 64) {   // stage h (the previous step's)
+                    const int st = idx / N, u = idx - st * N, gs = s0 + st;
+                    sm.h[st][u] = gs < r.S ? r.h[((size_t)gs * img.n_lstm + lst) * hs + u] : (int16_t)0;
+                }
+                wave_lds_sync();
+                int32_t* cg = valid ? r.c + ((size_t)s * img.n_lstm + lst) * hs : nullptr;
+                lstm_layer_mfma(img, Ly, in, out, &sm.h[0][0], cg, sm.tanh_tbl, lane, active);
                 wave_lds_sync();
                 // h_state := output after all groups (lstm.c:205-206)
-                for (int idx = lane; idx < 16 * Ly.N; idx += 64) {
-                    const int st = idx / Ly.N, u = idx - st * Ly.N;
-                    if (sm.active[st]) sm.h[lst][st][u] = sm.act[(i + 1) & 1][st][u];
+                for (int idx = lane; idx < 16 * N; idx += 64) {
+                    const int st = idx / N, u = idx - st * N, gs = s0 + st;
+                    if (sm.active[st]) r.h[((size_t)gs * img.n_lstm + lst) * hs + u] = out[st * NN_ASTRIDE + u];
                 }
                 ++lst;
             } else {
@@ -1130,17 +1132,6 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
             }
         }
         wave_lds_sync();
-    }
-    // ---- state out
-    for (int l = 0; l < img.n_lstm; ++l) {
-        const int N = img.lstm_n[l];
-        for (int idx = lane; idx < 16 * N; idx += 64) {
-            const int st = idx / N, u = idx - st * N, gs = s0 + st;
-            if (gs < r.S) {
-                r.h[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] = sm.h[l][st][u];
-                r.c[((size_t)gs * img.n_lstm + l) * NN_MAX_W + u] = sm.c[l][st][u];
-            }
-        }
     }
     if (r.mode != NN_MODE_DIRECT && lane < 16 && valid && r.post) {
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
@@ -1552,12 +1543,13 @@ __global__ void k_fe_default(int16_t* prev5, int16_t* tail, const int32_t* mean,
 }
 
 // NNSPClass_reset post/NN part (nn_speech.c:57-72, neural_nets.c:27-42)
-__global__ void k_nn_default(int16_t* h, int32_t* c, void* post, int n_lstm, const uint8_t* mask, int n) {
+// (row: h / c elements per stream, n_lstm * hs)
+__global__ void k_nn_default(int16_t* h, int32_t* c, void* post, int row, const uint8_t* mask, int n) {
     const int s = blockIdx.x;
     if (s >= n || (mask && !mask[s])) return;
-    for (int i = threadIdx.x; i < n_lstm * NN_MAX_W; i += blockDim.x) {
-        h[(size_t)s * n_lstm * NN_MAX_W + i] = 0;
-        c[(size_t)s * n_lstm * NN_MAX_W + i] = 0;
+    for (int i = threadIdx.x; i < row; i += blockDim.x) {
+        h[(size_t)s * row + i] = 0;
+        c[(size_t)s * row + i] = 0;
     }
     if (threadIdx.x == 0 && post) {
         PostState* p = reinterpret_cast<PostState*>(post) + s;
@@ -1690,33 +1682,25 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // whole multiples of the resident workgroups (256 CUs x 6 at 80 VGPRs):
     // each wave runs a contiguous frame range, so a partial last wave of
     // workgroups is pure tail
-    static const long long cap = [] {
-        const char* e = getenv("NNSP_FE_BLOCKS");
-        return e && atoll(e) > 0 ? atoll(e) : 256LL * 6 * 4;
-    }();
+    // (grid sweep, profiles/fe_sweep.sh: 3072 -> 454 M, 6144 -> 460 M cascade frames/s)
+    const long long cap = 256LL * 6 * 4;
     if (blocks > cap) blocks = cap;
-    if (a->wave_frames > 0) blocks = (nfr + 4LL * a->wave_frames - 1) / (4LL * a->wave_frames);
-    if (a->max_blocks > 0 && blocks > a->max_blocks) blocks = a->max_blocks;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
     const dim3 g((unsigned)blocks), blk(256);
     hipStream_t st = (hipStream_t)stream;
-    // two frames per wave (fe_kernel2): NNSP_FE_PAIR = 0 off, 1 the batch mode
-    // only (default), 2 the shared mode too.  Measured (A/B on one box): batch
-    // FE 0.55 -> 0.52 ms (VAD, 8192 streams); shared FE 2.18 -> 2.34 ms (fewer
-    // waves per SIMD keep its VALU less busy: SQ_ACTIVE_INST_VALU 95 -> 88 %)
-    static const int pair = [] {
-        const char* e = getenv("NNSP_FE_PAIR");
-        return e ? atoi(e) : FE_PAIR_DEFAULT;
-    }();
+    // two frames per wave (fe_kernel2): FE_PAIR_DEFAULT = 0 off, 1 the batch
+    // mode only (default), 2 the shared mode too.  Measured (A/B on one box):
+    // batch FE 0.55 -> 0.52 ms (VAD, 8192 streams); shared FE 2.18 -> 2.34 ms
+    // (fewer waves per SIMD keep its VALU less busy: SQ_ACTIVE_INST_VALU 95 -> 88 %)
+    constexpr int pair = FE_PAIR_DEFAULT;
     const bool use_pair = a->mode == FE_MODE_BATCH ? pair >= 1 : (a->mode == FE_MODE_SHARED && pair >= 2);
     // (no segments: every frame of a listed row is inside the chunk)
-    if (use_pair && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk && a->wave_frames <= 0) {
+    if (use_pair && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk) {
         // whole multiples of the resident workgroups at four per CU
         long long b2 = (nfr + 7) / 8;
         if (b2 > 256LL * 4 * 4) b2 = 256LL * 4 * 4;
-        if (a->max_blocks > 0 && b2 > a->max_blocks) b2 = a->max_blocks;
         const dim3 g2((unsigned)b2);
         if (a->mode == FE_MODE_SHARED) {
             if (a->port) hipLaunchKernelGGL((fe_kernel2<FE_MODE_SHARED, true>), g2, blk, 0, st, *a);
@@ -1768,6 +1752,7 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
 
 int nnspk_launch_nn(const NnImage* img, const NnRun* r, void* stream) {
     if (r->S <= 0) return 0;
+    if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);   // h / c row stride unset
     hipLaunchKernelGGL(nn_kernel, dim3((r->S + 15) / 16), dim3(64), 0, (hipStream_t)stream, *img, *r);
     return ok(hipGetLastError());
 }
@@ -1864,10 +1849,10 @@ int nnspk_launch_fe_default(int16_t* prev5, int16_t* tail, const int32_t* mean, 
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_nn_default(int16_t* h, int32_t* c, void* post, int n_lstm, const uint8_t* mask, int n,
+int nnspk_launch_nn_default(int16_t* h, int32_t* c, void* post, int row, const uint8_t* mask, int n,
                             void* stream) {
     if (n <= 0) return 0;
-    hipLaunchKernelGGL(k_nn_default, dim3(n), dim3(64), 0, (hipStream_t)stream, h, c, post, n_lstm, mask, n);
+    hipLaunchKernelGGL(k_nn_default, dim3(n), dim3(64), 0, (hipStream_t)stream, h, c, post, row, mask, n);
     return ok(hipGetLastError());
 }
 
@@ -1894,42 +1879,6 @@ int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
 const char* nnspk_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 int nnspk_stream_create(void** s) { return ok(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); }
-int nnspk_stream_create_prio(void** s, int high) {
-    int least = 0, greatest = 0;
-    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
-    if (e != hipSuccess) return (int)e;
-    return ok(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
-}
-// a stream on the CUs [lo, hi) of the device's n (spread 1: CU i counts as
-// i' = (i % 8) * (n / 8) + i / 8, i.e. the partition takes the same share of
-// every 8th CU)
-int nnspk_stream_create_cupart(void** s, int lo, int hi, int spread) {
-    int n = 0;
-    hipError_t e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
-    if (e != hipSuccess) return (int)e;
-    if (n <= 0 || n > 1024 || lo < 0 || hi > n || lo >= hi) return nnspk_stream_create(s);
-    uint32_t m[32] = {0};
-    for (int i = 0; i < n; ++i) {
-        const int ip = spread ? (i % 8) * (n / 8) + i / 8 : i;
-        if (ip >= lo && ip < hi) m[i / 32] |= 1u << (i % 32);
-    }
-    return ok(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)((n + 31) / 32), m));
-}
-int nnspk_stream_create_cumask(void** s, int free_cus, int spread) {
-    // a stream whose kernels leave free_cus CUs to the others: the top ones
-    // (spread 0) or every (n / free_cus)-th (spread 1)
-    int n = 0;
-    hipError_t e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
-    if (e != hipSuccess) return (int)e;
-    if (n <= 0 || n > 1024 || free_cus <= 0 || free_cus >= n) return nnspk_stream_create(s);
-    uint32_t m[32] = {0};
-    const int step = n / free_cus;
-    for (int i = 0; i < n; ++i) {
-        const bool off = spread ? (i % step == 0 && i / step < free_cus) : (i >= n - free_cus);
-        if (!off) m[i / 32] |= 1u << (i % 32);
-    }
-    return ok(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)((n + 31) / 32), m));
-}
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }

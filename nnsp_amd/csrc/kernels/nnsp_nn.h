@@ -89,7 +89,13 @@ __device__ __forceinline__ const int16_t* feat8_ptr(const FeatSrc& fs, const int
     slot = slot >= rg ? slot - rg : slot;
     const size_t row = cold ? (size_t)s * T + t : (size_t)s * fs.ring + slot;
     const uintptr_t base = cold ? (uintptr_t)feats : (uintptr_t)fs.nring;
-    return reinterpret_cast<const int16_t*>(base + (row * 40 + 8 * part) * sizeof(int16_t));
+    uintptr_t addr = base + (row * 40 + 8 * part) * sizeof(int16_t);
+    // the address is opaque and lives in a VGPR pair: no compiler can
+    // re-derive a wave-uniform (SGPR) base from the select above and merge
+    // this load with another -- the hazard stays closed under a new hipcc, not
+    // only under the ROCm 7.2 codegen it was found with
+    asm volatile("" : "+v"(addr));
+    return reinterpret_cast<const int16_t*>(addr);
 }
 __device__ __forceinline__ int4 feat8(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t, int part) {
     return *reinterpret_cast<const int4*>(feat8_ptr(fs, feats, s, T, b, t, part));

@@ -41,6 +41,7 @@ class NetSpec:
     # synthetic-weight spreads per layer: (std of W, std of Wrec, bias mean, bias std)
     spread: list[tuple] = field(default_factory=list)
     nid: int | None = None   # NNSP_ID of a net not named vad/kws/s2i (post-processing kind)
+    accs: list[int] | None = None   # per layer 1: fc_8x16_acc32b / lstm_8x16_acc32b (mixed nets)
 
     @property
     def nl(self) -> int:
@@ -306,11 +307,42 @@ GEN_SPECS = {
     "wide": NetSpec("wide", [240, 256, 28, 256, 2], [FC, LSTM, FC, FC], [7, 5, 5, 7], [8, 15, 15, 12],
                     [14, 13, 15, 15], [TANH, TANH, RELU6, LINEAR],
                     [(10, 0, 500, 6000), (3, 12, 300, 7000), (15, 0, 2000, 5000), (8, 0, 0, 6000)], nid=1),
+    # the reference's own limits (neural_nets.c:9-10: 300-element activation
+    # buffers): a 300-wide FC, a 300-wide LSTM (K = 300), then 300 -> 41
+    "wide300": NetSpec("wide300", [240, 300, 300, 300, 41], [FC, LSTM, FC, FC], [7, 6, 5, 6], [8, 15, 15, 12],
+                       [14, 14, 15, 14], [TANH, TANH, RELU6, LINEAR],
+                       [(8, 0, 500, 6000), (1.5, 2, 300, 7000), (4, 0, 2000, 5000), (5, 0, -8000, 9000)], nid=0),
+    # three LSTM layers, the first straight on the 240-wide context
+    "lstm3": NetSpec("lstm3", [240, 96, 64, 40, 2], [LSTM, LSTM, LSTM, FC], [5, 5, 5, 7], [8, 15, 15, 15],
+                     [13, 13, 13, 15], [TANH, TANH, TANH, LINEAR],
+                     [(4, 6, 300, 7000), (5, 8, 300, 7000), (6, 9, 300, 7000), (20, 0, 0, 6000)], nid=1),
+    # fc_8x16 and fc_8x16_acc32b / lstm_8x16 layers mixed in one net (per-layer layer_func)
+    "mixacc": NetSpec("mixacc", [240, 28, 28, 28, 28, 2], [FC, LSTM, FC, FC, FC],
+                      [7, 5, 5, 5, 7], [8, 15, 15, 12, 12], [14, 13, 15, 15, 15],
+                      [TANH, TANH, RELU6, RELU6, LINEAR],
+                      [(14, 0, 1700, 10000), (7, 15, 500, 8300), (12, 0, -2800, 8300),
+                       (19, 0, 5000, 4300), (30, 0, 0, 7000)], nid=1, accs=[1, 0, 1, 0, 1]),
+    # a linear layer inside the stack: its int32 outputs sit in the int16
+    # buffer, and the next layer reads size_layer int16 of them (neural_nets.c:131-149)
+    "midlin": NetSpec("midlin", [240, 48, 64, 2], [FC, FC, FC], [7, 5, 7], [8, 15, 12], [14, 15, 15],
+                      [LINEAR, RELU6, LINEAR], [(6, 0, 500, 6000), (3, 0, 2000, 5000), (20, 0, 0, 6000)], nid=2),
 }
+
+# Shapes only NeuralNetClass_exe takes (not NNSPClass_exec: its context is 240
+# wide and its static int32_t output[50], nn_speech.c:78, holds 50 int32 or
+# 100 int16): a 300-wide input, the widest linear layer (150 int32), a
+# 300-wide int16 output.
+DIRECT_SPECS = {
+    "direct300": NetSpec("direct300", [300, 300, 150], [LSTM, FC], [5, 6], [12, 15], [13, 14], [TANH, LINEAR],
+                         [(2, 2, 300, 7000), (4, 0, -2000, 9000)], nid=1),
+    "int16out": NetSpec("int16out", [300, 200, 300], [FC, FC], [6, 6], [12, 15], [14, 15], [TANH, RELU6],
+                        [(5, 0, 500, 6000), (6, 0, 2000, 5000)], nid=1),
+}
+ALL_GEN_SPECS = {**GEN_SPECS, **DIRECT_SPECS}
 
 
 def synth_net(name: str | NetSpec, seed: int = 1234) -> NetData:
-    spec = name if isinstance(name, NetSpec) else (SPECS.get(name) or GEN_SPECS[name])
+    spec = name if isinstance(name, NetSpec) else (SPECS.get(name) or ALL_GEN_SPECS[name])
     rng = np.random.default_rng([seed, spec.nn_id] + ([] if spec.name in SPECS else [len(spec.types)]))
 
     def i8(shape, std):

@@ -577,13 +577,14 @@ void or_net_forward(const or_net *net, or_stream *st, const int16_t *in, int32_t
     for (int i = 0; i < nl; ++i) {
         const int K = net->size[i], N = net->size[i + 1];
         const int qir = i + 1 < OR_MAX_LAYERS ? net->qi[i + 1] : 0;
+        const int acc32 = net->acc32 || net->acc32_layer[i]; /* layer_func[i] (neural_nets.c:111-129) */
         if (net->type[i] == OR_LSTM) {
             lstm_layer(nxt, net->W[i], net->Wr[i], net->B[i], cur, st->h[l], st->c[l], N, K,
-                       net->qk[i], net->qb[i], net->qi[i], qir, net->acc32, net->portable);
+                       net->qk[i], net->qb[i], net->qi[i], qir, acc32, net->portable);
             ++l;
         } else {
             fc_layer((char *)nxt, net->W[i], net->B[i], cur, N, K, net->qk[i], net->qb[i],
-                     net->qi[i], net->act[i], net->acc32, net->portable);
+                     net->qi[i], net->act[i], acc32, net->portable);
         }
         i16 *t = cur; cur = nxt; nxt = t;
     }
@@ -684,7 +685,13 @@ int16_t or_nnsp_exec(const or_net *net, or_stream *st, const or_cfg *cfg, const 
     if (st->slides == 1) {
         i32 out[50];
         or_net_forward(net, st, st->ctx, out, -1);
-        if (logits) memcpy(logits, out, (size_t)net->size[net->nl] * sizeof(i32));
+        if (logits) { /* the last layer's outputs, int16 ones widened */
+            const int nout = net->size[net->nl];
+            if (net->act[net->nl - 1] == OR_LINEAR)
+                memcpy(logits, out, (size_t)nout * sizeof(i32));
+            else
+                for (int o = 0; o < nout; ++o) logits[o] = ((const i16 *)out)[o];
+        }
         if (cfg->nn_id == 0)
             or_s2i_post(st, cfg, out);
         else

@@ -32,8 +32,8 @@ extern "C" {
 #endif
 
 #define OR_MAX_LAYERS 10
-#define OR_MAX_LSTM 2
-#define OR_MAX_WIDTH 128
+#define OR_MAX_LSTM 10   /* any layer of a NeuralNetClass may be an LSTM */
+#define OR_MAX_WIDTH 304 /* >= neural_nets.c's 300-element activation buffers (:9-10) */
 
 enum { OR_RELU6 = 0, OR_TANH = 1, OR_SIGMOID = 2, OR_LINEAR = 3 };
 enum { OR_FC = 0, OR_LSTM = 1 };
@@ -53,6 +53,7 @@ typedef struct {
     const int8_t *Wr[OR_MAX_LAYERS];
     const int16_t *B[OR_MAX_LAYERS];
     int32_t portable; /* 1: the ARM_OPTIMIZED=0 build's live align shift (affine.c:311-313), 0: shipped (T1) */
+    int32_t acc32_layer[OR_MAX_LAYERS]; /* per layer: its layer_func is the _acc32b twin (ORed with acc32) */
 } or_net;
 
 /* Per-stream state of one NNSPClass + FeatureClass + LSTM h/c. */

@@ -18,13 +18,15 @@ LIB = os.environ.get("NNSP_ORACLE_LIB") or os.path.join(HERE, "liboracle.so")
 REF = os.path.join(HERE, "_ref", "libnnsp_ref_partial.so")
 
 MAXL = 10
+MAX_LSTM, MAX_WIDTH = 10, 304   # nnsp_oracle.h OR_MAX_LSTM / OR_MAX_WIDTH
 
 
 class or_net(C.Structure):
     _fields_ = [("nl", C.c_int32), ("size", C.c_int32 * (MAXL + 1)), ("type", C.c_int32 * MAXL),
                 ("qk", C.c_int32 * MAXL), ("qi", C.c_int32 * MAXL), ("qb", C.c_int32 * MAXL),
                 ("act", C.c_int32 * MAXL), ("acc32", C.c_int32), ("W", C.c_void_p * MAXL),
-                ("Wr", C.c_void_p * MAXL), ("B", C.c_void_p * MAXL), ("portable", C.c_int32)]
+                ("Wr", C.c_void_p * MAXL), ("B", C.c_void_p * MAXL), ("portable", C.c_int32),
+                ("acc32_layer", C.c_int32 * MAXL)]
 
 
 class or_cfg(C.Structure):
@@ -91,6 +93,8 @@ class OracleNet:
                 self.keep.append(wr)
                 n.Wr[i] = wr.ctypes.data
         n.acc32 = int(acc32)
+        for i, a in enumerate(spec.accs or []):   # mixed fc_8x16 / _acc32b layers (NetSpec.accs)
+            n.acc32_layer[i] = int(a)
         n.portable = int(portable)   # the ARM_OPTIMIZED=0 build's live align shift (pinning only)
         self.net = n
         self.mean = np.ascontiguousarray(data.mean, np.int32)
@@ -249,8 +253,8 @@ def load_wavs() -> np.ndarray:
 
 
 class or_stream(C.Structure):
-    _fields_ = [("buf", C.c_int16 * 480), ("ctx", C.c_int16 * 240), ("h", (C.c_int16 * 128) * 2),
-                ("c", (C.c_int32 * 128) * 2), ("slides", C.c_int16), ("trigger", C.c_int16),
+    _fields_ = [("buf", C.c_int16 * 480), ("ctx", C.c_int16 * 240), ("h", (C.c_int16 * MAX_WIDTH) * MAX_LSTM),
+                ("c", (C.c_int32 * MAX_WIDTH) * MAX_LSTM), ("slides", C.c_int16), ("trigger", C.c_int16),
                 ("argmax_last", C.c_int16), ("pad0", C.c_int16), ("counts", C.c_int16 * 8),
                 ("outputs", C.c_int16 * 3), ("pad1", C.c_int16)]
 

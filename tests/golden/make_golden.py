@@ -21,7 +21,7 @@ reference tree).
                    into its byte order: fc_8x16 / lstm_8x16 / rc_8x16 and their
                    _acc32b twins called directly, and NeuralNetClass_exe over
                    consecutive calls (LSTM state carried) on the three reference
-                   nets and on the N3 shapes of nnsp_amd.nets.GEN_SPECS
+                   nets and on the N3 shapes of nnsp_amd.nets.ALL_GEN_SPECS
 
   ref_fe_portable.npz  the reference's ARM_OPTIMIZED=0 front end (row N4,
                    oracle/_ref/libnnsp_ref_fe_portable.so): rfft(512) and
@@ -286,7 +286,8 @@ class PortableNet:
             n.qbit_kernel[i], n.qbit_input[i], n.qbit_bias[i] = spec.qk[i], spec.qi[i], spec.qb[i]
             n.activation_type[i] = spec.acts[i]
             n.act_func[i] = C.cast(getattr(R, acts[spec.acts[i]]), C.c_void_p).value
-            fn = ("lstm_8x16" if t == N.LSTM else "fc_8x16") + ("_acc32b" if acc32 else "")
+            a32 = acc32 or bool(spec.accs and spec.accs[i])   # mixed nets: per-layer layer_func
+            fn = ("lstm_8x16" if t == N.LSTM else "fc_8x16") + ("_acc32b" if a32 else "")
             n.layer_func[i] = C.cast(getattr(R, fn), C.c_void_p).value
             w, b = np.ascontiguousarray(Wp[i], np.int8), np.ascontiguousarray(Bp[i], np.int16)
             self.keep += [w, b]
@@ -386,11 +387,11 @@ def nn() -> None:
     # ---- NeuralNetClass_exe over consecutive calls: the reference nets (their
     #      own tables, re-packed) and the N3 shapes (synthetic weights)
     cases = [("vad", N.ref_net("vad")), ("kws", N.ref_net("kws")), ("s2i", N.ref_net("s2i"))]
-    cases += [(g, N.synth_net(g, 77)) for g in N.GEN_SPECS]
+    cases += [(g, N.synth_net(g, 77)) for g in N.ALL_GEN_SPECS]
     for name, data in cases:
         x = nn_inputs(rng, 24, data.spec.sizes[0])
         out[f"net_{name}_x"] = x
-        if name in N.GEN_SPECS:
+        if name in N.ALL_GEN_SPECS:
             for i in range(data.spec.nl):
                 out[f"net_{name}_W{i}"], out[f"net_{name}_B{i}"] = data.W[i], data.B[i]
                 if data.Wr[i] is not None:

@@ -208,8 +208,8 @@ def test_lstm_vs_reference(gnn, acc):
 
 
 def _net_data(g, name):
-    if name in nets.GEN_SPECS:
-        spec = nets.GEN_SPECS[name]
+    if name in nets.ALL_GEN_SPECS:
+        spec = nets.ALL_GEN_SPECS[name]
         W = [g[f"net_{name}_W{i}"] for i in range(spec.nl)]
         Wr = [g[f"net_{name}_Wr{i}"] if f"net_{name}_Wr{i}" in g else None for i in range(spec.nl)]
         B = [g[f"net_{name}_B{i}"] for i in range(spec.nl)]
@@ -218,7 +218,7 @@ def _net_data(g, name):
 
 
 @pytest.mark.parametrize("acc", [64, 32])
-@pytest.mark.parametrize("name", ["vad", "kws", "s2i"] + list(nets.GEN_SPECS))
+@pytest.mark.parametrize("name", ["vad", "kws", "s2i"] + list(nets.ALL_GEN_SPECS))
 def test_neural_net_exe_vs_reference(gnn, name, acc):
     L = _lib.lib()
     data = _net_data(gnn, name)

@@ -232,3 +232,43 @@ def test_cascade_rejects_nets_out_of_nnsp_id_order():
     sq = np.array([1, 2, 0], np.int8)
     rc = _lib.lib().nnsp_cascade_create(C.byref(h), C.addressof(arr), O.p(sq), 3, C.addressof(prm))
     assert rc != 0 and not h.value
+
+
+def _spec_like(name, sizes, types, acts, nid=1):
+    """A synthetic NetSpec of the given shape (qbits of the VAD net's layers)."""
+    from nnsp_amd.nets import NetSpec
+    n = len(types)
+    return NetSpec(name, sizes, types, [6] * n, [8] + [15] * (n - 1), [14] * n, acts,
+                   [(4, 4, 300, 6000)] * n, nid=nid)
+
+
+def test_n3_beyond_the_reference_limits_is_refused():
+    """What the reference cannot run is refused with NNSP_EUNSUPPORTED and a
+    message, never truncated: a layer wider than neural_nets.c's 300-element
+    buffers (:9-10), a linear layer past 150 int32, and -- for NNSPClass_exec,
+    whose static int32_t output[50] holds 50 int32 (nn_speech.c:78) -- a
+    51-wide linear output."""
+    from nnsp_amd.nets import FC, LINEAR, RELU6, TANH
+    cases = [("w301", [240, 301, 2], [FC, FC], [TANH, LINEAR]),
+             ("lin151", [240, 151, 2], [FC, FC], [LINEAR, LINEAR]),
+             ("out51", [240, 64, 51], [FC, FC], [TANH, LINEAR])]
+    for name, sizes, types, acts in cases:
+        data = synth_net(_spec_like(name, sizes, types, acts), 3)
+        with pytest.raises(RuntimeError, match="nnsp_batch_create") as ei:
+            NNSPBatch(data, 16, 8)
+        assert "EUNSUPPORTED" in str(ei.value) or "outside" in str(ei.value) or "exceeds" in str(ei.value), ei.value
+    # the widest the reference allows is accepted: 300 int16 / 100 int16 output
+    ok = synth_net(_spec_like("ok300", [240, 300, 100], [FC, FC], [TANH, RELU6]), 3)
+    NNSPBatch(ok, 16, 8).close()
+
+
+def test_cascade_refuses_nets_without_one_lstm():
+    """The batched cascade runs nets of the split path (exactly one LSTM, the
+    shape of def_nn*.c); a three-LSTM net is refused with a message (the
+    single-net engine runs it, test_batch_n3_shapes)."""
+    S = 16
+    gnets = {"vad": NNSPBatch(synth_net("lstm3", 3), S, 16), "kws": NNSPBatch(ref_net("kws"), S, 16),
+             "s2i": NNSPBatch(ref_net("s2i"), S, 16)}
+    with pytest.raises(RuntimeError, match="nnsp_cascade_create") as ei:
+        NNSPCascade(gnets)
+    assert "one LSTM" in str(ei.value), ei.value

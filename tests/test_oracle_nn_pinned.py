@@ -77,8 +77,8 @@ def test_lstm_layers(g, acc):
 
 
 def _net_data(g, name):
-    if name in nets.GEN_SPECS:
-        spec = nets.GEN_SPECS[name]
+    if name in nets.ALL_GEN_SPECS:
+        spec = nets.ALL_GEN_SPECS[name]
         W = [g[f"net_{name}_W{i}"] for i in range(spec.nl)]
         Wr = [g[f"net_{name}_Wr{i}"] if f"net_{name}_Wr{i}" in g else None for i in range(spec.nl)]
         B = [g[f"net_{name}_B{i}"] for i in range(spec.nl)]
@@ -86,7 +86,7 @@ def _net_data(g, name):
     return nets.ref_net(name)
 
 
-NETS = ["vad", "kws", "s2i"] + list(nets.GEN_SPECS)
+NETS = ["vad", "kws", "s2i"] + list(nets.ALL_GEN_SPECS)
 
 
 @pytest.mark.parametrize("acc", [64, 32])
@@ -113,8 +113,8 @@ def test_neural_net_exe(g, name, acc):
             np.testing.assert_array_equal(got, y[r], err_msg=f"{name} acc{acc} portable={portable} call {r}")
         ost = O.or_stream.from_buffer(st)
         lstm_w = [sp.sizes[i + 1] for i in range(sp.nl) if sp.types[i] == nets.LSTM]
-        h = np.concatenate([np.array(ost.h[k][:n], np.int16) for k, n in enumerate(lstm_w)])
-        c = np.concatenate([np.array(ost.c[k][:n], np.int32) for k, n in enumerate(lstm_w)])
+        h = np.concatenate([np.array(ost.h[k][:n], np.int16) for k, n in enumerate(lstm_w)] + [np.zeros(0, np.int16)])
+        c = np.concatenate([np.array(ost.c[k][:n], np.int32) for k, n in enumerate(lstm_w)] + [np.zeros(0, np.int32)])
         np.testing.assert_array_equal(h, g[f"net_{name}_h{acc}"])
         np.testing.assert_array_equal(c, g[f"net_{name}_c{acc}"])
 
