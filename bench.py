@@ -80,6 +80,9 @@ WORKLOADS = {  # BASELINE.json configs
 # CPU baseline: the oracle ("port"), one process per usable core
 # ---------------------------------------------------------------------------
 def host_cpu() -> dict:
+    """The host's CPU share, each limit recorded on its own: the affinity mask,
+    the cgroup v2 quota and the job-size variables the box exports; ``usable``
+    is the smallest of them."""
     model = "unknown"
     try:
         with open("/proc/cpuinfo") as f:
@@ -90,21 +93,19 @@ def host_cpu() -> dict:
     except OSError:
         pass
     host = os.cpu_count() or 1
-    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
-    quota = None
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else host
+    cgroup = None
     try:   # cgroup v2 CPU quota: the share of the host this job may use
         with open("/sys/fs/cgroup/cpu.max") as f:
             q, per = f.read().split()
             if q != "max":
-                quota = max(1, int(int(q) / int(per)))
+                cgroup = max(1, int(int(q) / int(per)))
     except (OSError, ValueError):
         pass
-    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):   # the box exports the job's CPU share
-        if os.environ.get(k, "").isdigit():
-            quota = min(quota or 10**9, int(os.environ[k]))
-    if quota:
-        usable = min(usable, quota)
-    return {"model": model, "host_cores": host, "usable_cores": usable, "cgroup_or_env_quota": quota}
+    env = {k: int(os.environ[k]) for k in ("OMP_NUM_THREADS", "MAX_JOBS") if os.environ.get(k, "").isdigit()}
+    usable = min([affinity] + ([cgroup] if cgroup else []) + list(env.values()))
+    return {"model": model, "host_cores": host, "affinity_cores": affinity, "cgroup_quota": cgroup,
+            "env_quota": env, "usable_cores": usable}
 
 
 def native_oracle() -> tuple[str | None, str]:
@@ -120,22 +121,29 @@ def native_oracle() -> tuple[str | None, str]:
         return None, "prebuilt oracle/liboracle.so (-O3; gcc -march=native build unavailable)"
 
 
-def cpu_baseline(net: str, acc32: bool, weights: str, mix: bool, seconds: float, procs: int | None = None,
+def cpu_pool():
+    """The CPU-baseline worker processes, forked before this process touches
+    the GPU (a fork of a process holding a HIP context is unsafe); they idle
+    until the GPU legs are done."""
+    import multiprocessing as mp
+
+    cpu = host_cpu()
+    cpu["lib"], cpu["build"] = native_oracle()   # gcc runs before the GPU is touched too
+    return mp.get_context("fork").Pool(cpu["usable_cores"]), cpu
+
+
+def cpu_baseline(pool, cpu: dict, net: str, acc32: bool, weights: str, mix: bool, seconds: float,
                  portable: bool = False) -> dict:
     """The C oracle timed on the host cores, one process per core (the
     reference library keeps global scratch and is not re-entrant, so it scales
     by processes -- SURVEY 8(d))."""
-    import multiprocessing as mp
-
-    cpu = host_cpu()
-    procs = procs or cpu["usable_cores"]
-    lib, flags = native_oracle()
-    with mp.get_context("fork").Pool(procs) as pool:
-        res = pool.starmap(_cpu_worker, [(net, acc32, weights, mix, seconds, i, lib, portable) for i in range(procs)])
+    procs, lib = cpu["usable_cores"], cpu["lib"]
+    res = pool.starmap(_cpu_worker, [(net, acc32, weights, mix, seconds, i, lib, portable) for i in range(procs)])
     rate = sum(f / t for f, t in res)   # the processes run concurrently: their rates add
     return {"value": rate, "unit": "frames/s", "cores": procs, "kind": "port",
-            "cpu_model": cpu["model"], "host_cores": cpu["host_cores"], "quota": cpu["cgroup_or_env_quota"],
-            "build": flags,
+            "cpu_model": cpu["model"], "host_cores": cpu["host_cores"], "affinity_cores": cpu["affinity_cores"],
+            "cgroup_quota": cpu["cgroup_quota"], "env_quota": cpu["env_quota"],
+            "build": cpu["build"],
             "sample": f"{procs} concurrent processes x ~{seconds:.0f} s each of 32 continuous streams in 100-frame "
                       f"chunks (the bench's input mix and weights, inputs generated before the timed loop), "
                       f"{net}, {'32' if acc32 else '64'}b accumulator"
@@ -383,6 +391,8 @@ def main() -> None:
     args = ap.parse_args()
 
     rank, world, local, launched = dist_env()
+    # the CPU baseline runs on rank 0 at N=1 only; its pool exists before the GPU does
+    pool, cpu = cpu_pool() if rank == 0 and world == 1 and not args.no_cpu_baseline else (None, None)
     import torch
 
     dist = None
@@ -456,9 +466,11 @@ def main() -> None:
                 out["cascade_synthetic_weights"] = stress
         else:
             out["nn_ms_per_step"] = res["nn_ms"]
-        if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.net, args.acc32, args.weights, args.input == "mix",
-                                               args.cpu_seconds, portable=args.build == "portable")
+        if pool is not None:
+            with pool:
+                out["cpu_baseline"] = cpu_baseline(pool, cpu, args.net, args.acc32, args.weights,
+                                                   args.input == "mix", args.cpu_seconds,
+                                                   portable=args.build == "portable")
         print(json.dumps(out))
     if dist:
         dist.destroy_process_group()

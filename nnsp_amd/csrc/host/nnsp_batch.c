@@ -144,10 +144,8 @@ static void plan_fast(nnsp_batch *b)
     b->fast = 1;
 }
 
-/* NNSP_RECUR_CLOCKS probe buffer: 2048 longs of phase clocks, then
- * fe_kernel's per-wave records (4 longs per wave, 32768 waves), then
- * proj_kernel's (8192 waves) */
-#define DCLK_LONGS (2048 + 4 * 32768 + 4 * 8192)
+/* NNSP_RECUR_CLOCKS probe buffer (layout: nnsp_kabi.h NNSP_DCLK_*) */
+#define DCLK_LONGS NNSP_DCLK_LONGS
 
 #define TRY(x)                 \
     do {                       \
@@ -365,7 +363,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.n_list = seg->n_list;
         f.seg_begin = seg->seg_begin;
         f.seg_len = seg->seg_len;
-        f.dbg_clk = b->d_clk;
+        f.dbg_clk = seg->ctl && seg->ctl->round ? NULL : b->d_clk; /* probes: a cascade's round 0 */
         f.shape = b->shape;
         f.ep32 = b->ep32;
         const NnLayer *LL = &b->im.img.L[b->li];
@@ -388,6 +386,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             if (need < blocks) blocks = (int)need;
         }
         TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
+        if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
         f.a_off = b->rec_a_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;
@@ -409,6 +408,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         r.trig = trig;
         r.logits = logits;
         TRY(nnspk_launch_nn(&b->im.img, &r, stream));
+        if (seg && seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
         /* carry the feature context (slots 1..5); recur_kernel does it on the split path */
         TRY(nnspk_launch_ctx_roll(b->d_prev5, b->d_feats, b->S, T, seg->list, seg->n_list, seg->seg_begin,
                                   seg->seg_len, stream));
@@ -517,6 +517,14 @@ int nnsp_batch_debug_clocks(nnsp_batch *b, long long *out)
 {
     if (!b || !out || !b->d_clk) return NNSP_EINVAL;
     TRY(nnspk_d2h(out, b->d_clk, 64 * 32 * 8, b->stream));
+    return nnspk_sync(b->stream);
+}
+
+/* development probe: zero the clock buffer (before an instrumented chunk) */
+int nnsp_batch_debug_clocks_clear(nnsp_batch *b)
+{
+    if (!b || !b->d_clk) return NNSP_EINVAL;
+    TRY(nnspk_memset(b->d_clk, 0, DCLK_LONGS * 8, b->stream));
     return nnspk_sync(b->stream);
 }
 

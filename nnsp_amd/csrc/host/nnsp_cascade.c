@@ -82,6 +82,7 @@ struct nnsp_cascade {
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
+    void *ev_vad_proj;              /* VAD's round-0 prefix FC layers done */
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
@@ -176,6 +177,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
     for (int q = 0; q < 2; ++q)
         if ((e = nnspk_event_create(&c->ev_ahead[q][0])) || (e = nnspk_event_create(&c->ev_ahead[q][1]))) goto fail;
+    if ((e = nnspk_event_create(&c->ev_vad_proj))) goto fail;
     for (int n = 0; n < 3; ++n) {
         /* each net's rounds run on its batch's own stream: the cascade adds
          * one stream (c->stream) to the three, so on a device with four
@@ -316,6 +318,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         nnspk_event_destroy(c->ev_fe[i]);
     }
     nnspk_event_destroy(c->ev_fork);
+    nnspk_event_destroy(c->ev_vad_proj);
     for (int q = 0; q < 2; ++q) {
         nnspk_event_destroy(c->ev_ahead[q][0]);
         nnspk_event_destroy(c->ev_ahead[q][1]);
@@ -410,11 +413,13 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
 
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
-static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st)
+static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
+                    void *proj_done)
 {
     const int timed = c->timing && r < MAX_TIMED;
     nnsp_segment seg;
     memset(&seg, 0, sizeof seg);
+    seg.proj_done = proj_done;
     seg.list = c->d_list[r & 1][n];
     seg.n_list_dev = cur + n;
     seg.seg_begin = c->d_seg_begin;
@@ -460,12 +465,22 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
     /* (measured and dropped, profiles/r02/sched: every net's cold front end
      * of a round before any net's NN kernels, VAD's recurrence after S2I's
      * and KWS's, every recur behind all three projs -- each -2..-7 %) */
-    for (int n = 0; n < 3; ++n) {
+    /* round 0 with fused control: VAD (net 1) is launched first and S2I's
+     * and KWS's cold front ends wait for VAD's proj -- every stream starts
+     * with VAD's round, so VAD's cold frames and prefix layers are the
+     * longest chain of the round and get the whole device (paired A/B over
+     * 6 runs, profiles/r03: +1 % cascade frames/s over the plain order) */
+    static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2};
+    const int vad_first = r == 0 && c->fused && !c->serial;
+    const int *order = vad_first ? o_vad : o_plain;
+    for (int i = 0; i < 3; ++i) {
+        const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];
         const int timed = c->timing && r < MAX_TIMED;
         if (c->fused) {
             if (r == 0) {
                 TRY(nnspk_stream_wait(st, c->ev_fork)); /* casc_begin */
+                if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
             } else {
                 for (int m = 0; m < 3; ++m)
                     if (m != n) TRY(nnspk_stream_wait(st, c->ev_rnd[(r - 1) & 1][m]));
@@ -477,7 +492,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
-        TRY(round_nn(c, a, r, n, T, cur, hist, st));
+        TRY(round_nn(c, a, r, n, T, cur, hist, st, vad_first && n == 1 ? c->ev_vad_proj : NULL));
     }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
@@ -509,6 +524,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     fa.mean = c->net[0]->d_mean; /* unused in FE_MODE_SHARED */
     fa.stdR = c->net[0]->d_stdR;
     fa.mode = FE_MODE_SHARED;
+    fa.dbg_clk = c->net[1]->d_clk; /* development probe (NNSP_RECUR_CLOCKS): per-wave records in VAD's buffer */
     fa.port = c->net[0]->port;
     fa.norm32 = c->net[0]->norm32 && c->net[1]->norm32 && c->net[2]->norm32;
     fa.ring = c->ring;

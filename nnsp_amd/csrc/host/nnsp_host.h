@@ -92,6 +92,8 @@ typedef struct {
     int16_t *detected, *outputs3;
     int net_id;
     const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
+    void *proj_done;           /* non-NULL: recorded on the stream once the prefix FC layers are done
+                                  (split path: between proj and recur; fused kernel: after it) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

@@ -246,6 +246,16 @@ __device__ __forceinline__ int16_t relu6_q12(int32_t x) {   // :6-17
     return (int16_t)(v < 0 ? 0 : v);
 }
 
+// development probes (NNSP_RECUR_CLOCKS): where a wave runs, packed as
+// xcc << 12 | se << 8 | sh << 7 | cu << 3 | simd (HW_REG_HW_ID, HW_REG_XCC_ID)
+__device__ __forceinline__ long long nnsp_hw_where() {
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    const unsigned simd = (hw >> 4) & 3, cu = (hw >> 8) & 15, sh = (hw >> 12) & 1, se = (hw >> 13) & 7;
+    return (long long)(((xcc & 15) << 12) | (se << 8) | (sh << 7) | (cu << 3) | simd);
+}
+
 enum { ACT_RELU6 = 0, ACT_TANH = 1, ACT_SIGMOID = 2, ACT_LINEAR = 3 };
 
 // shift_64b / shift_32b (affine.c:565-591, affine_acc32b.c:566-592)

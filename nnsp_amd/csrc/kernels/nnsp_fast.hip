@@ -281,12 +281,19 @@ __device__ __forceinline__ void put_frame(const FastRun& r, int s, int T, int f,
 // Per-wave LDS of proj.  The compiled shapes keep one activation buffer as
 // wide as the LSTM input's K tiles (+8: rows 16 B apart modulo 256 B); the
 // generic shape ping-pongs two full-width buffers across its prefix layers.
+//
+// Compiled shapes: two union buffers, the next tile's features loading into
+// one (LDS-DMA) while the current tile computes from the other; a tile's
+// activations overwrite its own union once the FC layer has read it (the
+// B operand is loaded before the first output store), so the act rows need
+// no buffer of their own.
 template <class SH>
 struct alignas(16) ProjWave {
     static constexpr int AS = SH::generic ? P_ASTRIDE : 64 * SH::NKR + 8;
     static constexpr int NA = SH::generic ? 2 : 1;
-    int16_t uni[P_UNION + 32];
-    int16_t act[NA][16][AS];
+    static constexpr int UNI = (P_UNION + 32) > 16 * AS ? (P_UNION + 32) : 16 * AS;   // int16 per union buffer
+    int16_t uni[SH::generic ? 1 : 2][SH::generic ? P_UNION + 32 : UNI];
+    int16_t act[SH::generic ? NA : 0][16][AS];
 };
 
 // 16 zero bytes: the source of union elements outside a segment (proj_kernel)
@@ -304,9 +311,6 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     PW& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
-    if constexpr (!GEN)   // x rows carry zeros past the LSTM input width N (fc_layer writes 0..N-1)
-        for (int c = lane; c < 16 * (PW::AS - SH::NW); c += 64)
-            P.act[0][c / (PW::AS - SH::NW)][SH::NW + c % (PW::AS - SH::NW)] = 0;
     const NnLayer& LL = img.L[r.li];
     const int nrt = GEN ? LL.nrt : SH::NRT;
     const int nkt = GEN ? LL.nkt : SH::NKR;
@@ -368,6 +372,142 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
         return g;
     };
     long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+    if constexpr (!GEN) {
+        // ---- compiled shapes: the next tile's features (LDS-DMA into the
+        //      other union buffer) and descriptors load while this tile
+        //      computes; one vmcnt(0) per tile then waits only for what was
+        //      issued a whole tile earlier (and the x stores of the last one)
+        constexpr int XC = SH::XS / 8;   // 8-element chunks of an x row
+        // the union of tile t (descriptor m) into buffer bf; false: no row of
+        // the tile has a frame (wave-uniform), nothing issued
+        auto union_issue = [&](const Seg& m, long long t, int bf) -> bool {
+            const int j0 = j0_of(t);
+            if (!__any(lane < G && m.ok && 2 * j0 + m.ph < m.L)) return false;
+            const Seg g1 = {__builtin_amdgcn_readfirstlane(m.s), __builtin_amdgcn_readfirstlane(m.b),
+                            __builtin_amdgcn_readfirstlane(m.L), __builtin_amdgcn_readfirstlane(m.ph),
+                            __builtin_amdgcn_readfirstlane((int)m.ok) != 0};
+            auto union_g = [&](auto GC) {
+                constexpr int GG = decltype(GC)::value, FRG = 2 * (16 / GG) + 4, NU = GG * FRG * 5;
+#pragma unroll
+                for (int mm = 0; mm < (NU + 63) / 64; ++mm) {
+                    int c = lane + 64 * mm;
+                    asm volatile("" : "+v"(c));
+                    if (mm < NU / 64 || c < NU) {
+                        const int k = c / (FRG * 5), rem = c - k * (FRG * 5), fr = rem / 5, part = rem - 5 * fr;
+                        Seg g = g1;
+                        if (GG > 1) {
+                            g.s = __shfl(m.s, k);
+                            g.b = __shfl(m.b, k);
+                            g.L = __shfl(m.L, k);
+                            g.ph = __shfl(m.ph, k);
+                            g.ok = __shfl((int)m.ok, k) != 0;
+                        }
+                        const int idx = 2 * j0 + g.ph + fr;
+                        const int16_t* src = reinterpret_cast<const int16_t*>(&nnsp_proj_zero16);
+                        if (g.ok) {
+                            if (idx < 5)
+                                src = r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part;
+                            else if (idx - 5 < g.L)
+                                src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+                        }
+                        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                         (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
+                                                         16, 0, 0);
+                    }
+                }
+            };
+            if (G == 1)
+                union_g(std::integral_constant<int, 1>{});
+            else if (G == 2)
+                union_g(std::integral_constant<int, 2>{});
+            else
+                union_g(std::integral_constant<int, 4>{});
+            return true;
+        };
+        // descriptors in flight are held packed (3 VGPRs instead of 5; the
+        // kernel sits at 128): s (-1: none), b, L | phase << 16
+        struct SegP { int s, b, lp; };
+        auto pack = [](const Seg& g) { return SegP{g.ok ? g.s : -1, g.b, g.L | (g.ph << 16)}; };
+        auto unpack = [](const SegP& p) { return Seg{p.s < 0 ? 0 : p.s, p.b, p.lp & 0xffff, p.lp >> 16, p.s >= 0}; };
+        Seg mine = seg_from(list_at(tile));
+        SegP mine_n = pack(seg_from(list_at(tile + tstride)));
+        int s_nn = list_at(tile + 2 * tstride);
+        bool have = tile < ntiles && union_issue(mine, tile, 0);
+        int cb = 0;
+        for (; tile < ntiles; tile += tstride, ++it) {
+            PCLK(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's union landed
+            wave_lds_sync();
+            // descriptors two tiles ahead, then the next tile's union into the
+            // other buffer (its previous contents, the last tile's x rows, were
+            // stored before the wait above)
+            const SegP mine_nn = pack(seg_from(s_nn));
+            s_nn = list_at(tile + 3 * tstride);
+            const bool have_n = tile + tstride < ntiles && union_issue(unpack(mine_n), tile + tstride, cb ^ 1);
+            if (have) {
+                ++ntile_run;
+                PCLK(1);
+                const int j0 = j0_of(tile);
+                auto seg_k = [&](int k) {
+                    Seg g;
+                    g.s = __shfl(mine.s, k);
+                    g.b = __shfl(mine.b, k);
+                    g.L = __shfl(mine.L, k);
+                    g.ph = __shfl(mine.ph, k);
+                    g.ok = __shfl((int)mine.ok, k) != 0;
+                    return g;
+                };
+                // ---- the prefix FC layer, K = 240, tanh (row (k, j)'s context =
+                //      uni[k*FR*40 + 80j .. +239]; the per-lane base makes in +
+                //      sc * 80 that row); its output rows overwrite the union
+                const int kr = sc / SPT, jr = sc - kr * SPT;
+                int16_t* U = &P.uni[cb][0];
+                const int16_t* in = U + kr * FR * 40 + 80 * jr - 80 * sc;
+                const NnLayer& L0 = img.L[0];
+                fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
+                                                              in, 80, U, PW::AS, tt, lane);
+                wave_lds_sync();
+                PCLK(2);
+                // ---- the LSTM's input x of every row to HBM, already in the
+                //      MFMA B operand's split form (split_hilo): per row xs high
+                //      bytes, then xs low bytes ^ 0x80; columns N..xs-1 (not
+                //      written by the layer) are stored as zeros
+                for (int c = lane; c < 16 * XC; c += 64) {
+                    const int row = c / XC, part = c - row * XC;
+                    const int kx = row / SPT, jx = row - kx * SPT;
+                    const Seg g = seg_k(kx);
+                    const int j = j0 + jx;
+                    if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L) {
+                        int4 v = *reinterpret_cast<const int4*>(U + row * PW::AS + 8 * part);
+                        if (8 * XC > SH::NW && part == XC - 1) {   // mask the columns past N
+                            int32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) {
+                                const int col = 8 * part + 2 * e;
+                                w4[e] = col + 1 < SH::NW ? w4[e] : (col < SH::NW ? (w4[e] & 0xffff) : 0);
+                            }
+                            v = make_int4(w4[0], w4[1], w4[2], w4[3]);
+                        }
+                        uint8_t* dst = reinterpret_cast<uint8_t*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS) +
+                                       8 * part;
+                        const uint32_t HS = 0x07050301u, LS = 0x06040200u;
+                        *reinterpret_cast<uint2*>(dst) =
+                            make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, HS),
+                                       __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, HS));
+                        *reinterpret_cast<uint2*>(dst + SH::XS) =
+                            make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, LS) ^ 0x80808080u,
+                                       __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, LS) ^ 0x80808080u);
+                    }
+                }
+                PCLK(3);
+            }
+            mine = unpack(mine_n);
+            mine_n = mine_nn;
+            have = have_n;
+            cb ^= 1;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
     Seg mine_n = seg_from(list_at(tile));
     int s_nn = list_at(tile + tstride);
     for (; tile < ntiles; tile += tstride, ++it) {
@@ -416,7 +556,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                             src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
                     }
                     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                     (__attribute__((address_space(3))) void*)&P.uni[512 * m], 16, 0, 0);
+                                                     (__attribute__((address_space(3))) void*)&P.uni[0][512 * m], 16, 0, 0);
                 }
             }
         };
@@ -434,40 +574,9 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
         const Seg me = seg_k(kr);
         // ---- prefix FC layers (row (k, j)'s context = uni[k*FR*40 + 80j .. +239];
         //      the per-lane base makes in + sc * in_stride that row)
-        const int16_t* in = P.uni + kr * FR * 40 + 80 * jr - 80 * sc;
+        const int16_t* in = &P.uni[0][0] + kr * FR * 40 + 80 * jr - 80 * sc;
         int in_stride = 80;
-        if constexpr (!GEN) {   // one tanh FC layer, K = 240
-            const NnLayer& L0 = img.L[0];
-            fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
-                                                          in, in_stride, &P.act[0][0][0], PW::AS, tt, lane);
-            wave_lds_sync();
-            PCLK(2);
-            // ---- the LSTM's input x of every row to HBM, already in the MFMA
-            //      B operand's split form (split_hilo): per row xs high bytes,
-            //      then xs low bytes ^ 0x80 (columns N..xs-1: the zeros set at
-            //      kernel start) -- split here once instead of by each of
-            //      recur's LSTM waves every step
-            constexpr int XC = SH::XS / 8;   // 8-element chunks per row
-            for (int c = lane; c < 16 * XC; c += 64) {
-                const int row = c / XC, part = c - row * XC;
-                const int kx = row / SPT, jx = row - kx * SPT;
-                const Seg g = seg_k(kx);
-                const int j = j0 + jx;
-                if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L) {
-                    const int4 v = *reinterpret_cast<const int4*>(&P.act[0][row][8 * part]);
-                    uint8_t* dst = reinterpret_cast<uint8_t*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS) + 8 * part;
-                    const uint32_t HS = 0x07050301u, LS = 0x06040200u;
-                    *reinterpret_cast<uint2*>(dst) = make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, HS),
-                                                                __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, HS));
-                    *reinterpret_cast<uint2*>(dst + SH::XS) =
-                        make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, LS) ^ 0x80808080u,
-                                   __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, LS) ^ 0x80808080u);
-                }
-            }
-            wave_lds_sync();
-            PCLK(3);
-            continue;
-        } else {
+        {
             for (int i = 0; i < r.li; ++i) {
                 const NnLayer& Ly = img.L[i];
                 int16_t* out = &P.act[i & (PW::NA - 1)][0][0];
@@ -506,10 +615,11 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
             PCLK(3);
         }
     }
+    }
 #undef PCLK
     if (pwc) {
         pwc[2] = (long long)__builtin_amdgcn_s_memrealtime();
-        pwc[3] = ntile_run;
+        pwc[3] = (long long)ntile_run | (nnsp_hw_where() << 32);
     }
 }
 
@@ -886,6 +996,13 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     if ((int)blockIdx.x * TPW * 16 >= nrow) return;
     // the workgroup's tiles share the staged weights and tables; everything
     // else below is per tile (tid / TD instead of threadIdx / blockDim)
+    // development probe (NNSP_RECUR_CLOCKS, the cascade's round 0 / a batch):
+    // per workgroup, wall clock (100 MHz) at the start, after staging and at
+    // the end, and where it ran (nnsp_hw_where)
+    long long* wgc = (r.dbg_clk && (!ctl || ca.round == 0) && threadIdx.x == 0 && blockIdx.x < 8192u)
+                         ? r.dbg_clk + NNSP_DCLK_RECUR + 4 * blockIdx.x
+                         : nullptr;
+    if (wgc) wgc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     const int sub = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / CF::NWV;
     const int tid = (int)threadIdx.x - sub * TD;
     const int i0 = ((int)blockIdx.x * TPW + sub) * 16;   // tile = 16 consecutive entries of the stream list
@@ -897,6 +1014,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
     for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    if (wgc) wgc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - sub * CF::NWV;   // < RGP: LSTM wave; then stages
     const int sc = lane & 15, q = lane >> 4;
@@ -1300,6 +1418,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
 #pragma unroll
     for (int k = 0; k < 2; ++k)
         if (ci[k] >= 0) reinterpret_cast<int4*>(r.prev5)[ci[k]] = cv[k];
+    if (wgc) {
+        wgc[2] = (long long)__builtin_amdgcn_s_memrealtime();
+        wgc[3] = (long long)nsteps | (nnsp_hw_where() << 32);
+    }
     if (ctl && post_w) {
         // ---- controller bookkeeping (casc_control_kernel's tail): frames since
         //      the reset of the net the stream runs next (its feat8 reads above

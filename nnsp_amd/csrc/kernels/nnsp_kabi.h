@@ -28,6 +28,14 @@ extern "C" {
 #define NN_MODE_STREAM 0 /* NNSPClass_exec over a chunk: FE features in, post-proc */
 #define NN_MODE_DIRECT 1 /* NeuralNetClass_exe: 240-wide input in, raw output */
 
+/* development probe buffer (NNSP_RECUR_CLOCKS), in longs: recur phase
+ * clocks [0, 2048); fe_kernel per wave 4 each (32768 waves); proj_kernel
+ * per wave 4 each (8192 waves); recur_pipe_kernel per workgroup 4 each (8192) */
+#define NNSP_DCLK_FE 2048
+#define NNSP_DCLK_PROJ (NNSP_DCLK_FE + 4 * 32768)
+#define NNSP_DCLK_RECUR (NNSP_DCLK_PROJ + 4 * 8192)
+#define NNSP_DCLK_LONGS (NNSP_DCLK_RECUR + 4 * 8192)
+
 typedef struct {
     const int16_t *pcm;  /* [S][T][160] */
     const int16_t *tail; /* [S][320]: samples of the two frames before the chunk */

@@ -620,7 +620,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     flush();
     if (wclk) {
         wclk[2] = (long long)__builtin_amdgcn_s_memrealtime();
-        wclk[3] = (long long)(fend - fbeg);
+        wclk[3] = (long long)(fend - fbeg) | (nnsp_hw_where() << 32);
     }
 #undef FCLK
 }
@@ -1683,6 +1683,9 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // each wave runs a contiguous frame range, so a partial last wave of
     // workgroups is pure tail
     // (grid sweep, profiles/fe_sweep.sh: 3072 -> 454 M, 6144 -> 460 M cascade frames/s)
+    // (also measured in round 3, paired A/B: 1536 blocks -- one generation --
+    // 882 M, 3072 951 M, 6144 965 M, 12288 965 M, 24576 954 M cascade frames/s:
+    // the later generations' workgroup turnover lets the nets' rounds in)
     const long long cap = 256LL * 6 * 4;
     if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
