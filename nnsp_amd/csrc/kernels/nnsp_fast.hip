@@ -299,7 +299,9 @@ struct alignas(16) ProjWave {
 // 16 zero bytes: the source of union elements outside a segment (proj_kernel)
 __device__ __attribute__((aligned(16))) int4 nnsp_proj_zero16;
 
-template <class SH, bool ACC32>
+// GT: streams per 16-row tile (compiled shapes: 1, 2 or 4, FastRun.gpt; one
+// instantiation each, so a G = 1 tile's descriptors are wave-uniform scalars)
+template <class SH, bool ACC32, int GT>
 __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) {   // <= 128 VGPRs: 4 waves per SIMD
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
@@ -308,7 +310,10 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     using PW = ProjWave<SH>;
     PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
     constexpr bool GEN = SH::generic;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // wave-uniform tile arithmetic (32-bit, scalar): with the wave index in a
+    // VGPR every tile paid three 64-bit divisions on the VALU (~250 VALU per tile)
+    const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nwv = blockDim.x >> 6;
     PW& P = pw[wv];
     const int sc = lane & 15, q = lane >> 4;
     const NnLayer& LL = img.L[r.li];
@@ -319,17 +324,17 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     // a 16-row MFMA tile is G streams x SPT consecutive NN steps: G = 1 tiles
     // a stream's steps 16 at a time; short segments (cascade rounds, host:
     // SPT >= the segment's steps) pack G = 2 or 4 streams into one tile
-    const int G = GEN ? 1 : r.gpt;
-    const int SPT = 16 / G;
-    const int FR = 2 * SPT + 4;                       // context frames of one stream's rows
+    constexpr int G = GEN ? 1 : GT;
+    constexpr int SPT = 16 / G;
+    constexpr int FR = 2 * SPT + 4;                   // context frames of one stream's rows
     const int ntps = G > 1 ? 1 : (wsteps + 15) / 16;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
     if (r.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *r.n_list_rec = nrow;
-    const long long ngrp = (nrow + G - 1) / G;
-    const long long ntiles = ngrp * ntps;
+    const int ngrp = (nrow + G - 1) / G;
+    const int ntiles = ngrp * ntps;   // < 2^31: S * T < 2^31 (host)
     // device-sized lists (cascade rounds): workgroups with no tile exit
     // before staging anything
-    if ((long long)blockIdx.x * (blockDim.x >> 6) >= ntiles) return;
+    if ((int)blockIdx.x * nwv >= ntiles) return;
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after staging, at the end, and the tiles it ran
     const unsigned pwid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
@@ -355,11 +360,13 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     // loaded two tiles ahead and the segment descriptors one tile ahead, so a
     // tile waits only for its features.  (Prefetching the features as well
     // took 16 more VGPRs per lane held across the FC layer: past 128, spills.)
-    const long long tstride = (long long)gridDim.x * (blockDim.x >> 6);
-    auto j0_of = [&](long long t) { return 16 * (int)(t - (t / ntps) * ntps); };
+    const int tstride = (int)gridDim.x * nwv;
+    auto grp_of = [&](int t) { return ntps == 1 ? t : (ntps == 4 ? t >> 2 : (ntps == 2 ? t >> 1 : t / ntps)); };
+    auto j0_of = [&](int t) { return 16 * (t - grp_of(t) * ntps); };
     // lanes 0..G-1: the tile's stream k = lane (the others read by shuffle); -1: none
-    auto list_at = [&](long long t) {
-        const long long i = (t / ntps) * G + (lane < G ? lane : 0);
+    auto list_at = [&](int t) {
+        if (t >= ntiles) return -1;
+        const int i = G == 1 ? grp_of(t) : grp_of(t) * G + (lane < G ? lane : 0);
         return i < nrow ? (r.list ? r.list[i] : (int)i) : -1;
     };
     auto seg_from = [&](int st) {
@@ -371,7 +378,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
         g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
         return g;
     };
-    long long tile = (long long)blockIdx.x * (blockDim.x >> 6) + wv;
+    int tile = (int)blockIdx.x * nwv + wv;
     if constexpr (!GEN) {
         // ---- compiled shapes: the next tile's features (LDS-DMA into the
         //      other union buffer) and descriptors load while this tile
@@ -380,48 +387,82 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
         constexpr int XC = SH::XS / 8;   // 8-element chunks of an x row
         // the union of tile t (descriptor m) into buffer bf; false: no row of
         // the tile has a frame (wave-uniform), nothing issued
-        auto union_issue = [&](const Seg& m, long long t, int bf) -> bool {
+        auto union_issue = [&](const Seg& m, int t, int bf) -> bool {
             const int j0 = j0_of(t);
             if (!__any(lane < G && m.ok && 2 * j0 + m.ph < m.L)) return false;
             const Seg g1 = {__builtin_amdgcn_readfirstlane(m.s), __builtin_amdgcn_readfirstlane(m.b),
                             __builtin_amdgcn_readfirstlane(m.L), __builtin_amdgcn_readfirstlane(m.ph),
                             __builtin_amdgcn_readfirstlane((int)m.ok) != 0};
-            auto union_g = [&](auto GC) {
-                constexpr int GG = decltype(GC)::value, FRG = 2 * (16 / GG) + 4, NU = GG * FRG * 5;
-#pragma unroll
-                for (int mm = 0; mm < (NU + 63) / 64; ++mm) {
-                    int c = lane + 64 * mm;
-                    asm volatile("" : "+v"(c));
-                    if (mm < NU / 64 || c < NU) {
-                        const int k = c / (FRG * 5), rem = c - k * (FRG * 5), fr = rem / 5, part = rem - 5 * fr;
-                        Seg g = g1;
-                        if (GG > 1) {
-                            g.s = __shfl(m.s, k);
-                            g.b = __shfl(m.b, k);
-                            g.L = __shfl(m.L, k);
-                            g.ph = __shfl(m.ph, k);
-                            g.ok = __shfl((int)m.ok, k) != 0;
-                        }
-                        const int idx = 2 * j0 + g.ph + fr;
-                        const int16_t* src = reinterpret_cast<const int16_t*>(&nnsp_proj_zero16);
-                        if (g.ok) {
-                            if (idx < 5)
-                                src = r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part;
-                            else if (idx - 5 < g.L)
-                                src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
-                        }
-                        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                         (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
-                                                         16, 0, 0);
+            constexpr int NU = G * FR * 5;   // 16-byte chunks (8 features) of the union
+            if constexpr (G == 1) {
+                // one stream whose window V[t0 .. t0 + FR) lies past prev5 and
+                // past the segment's (possibly cold) first two frames: its
+                // features are consecutive frames of the ring (or of feats),
+                // chunk c = 5d + part at frame t0 + d.  Frames past the
+                // segment feed only rows that are not stored: they re-read the
+                // segment's last frame (in bounds) instead of a zero row.
+                const int t0 = 2 * j0 + g1.ph;
+                if (t0 >= 7) {
+                    const int dmax = g1.L + 4 - t0;             // V index L + 4: the segment's last frame
+                    const int f0 = g1.b + t0 - 5;               // chunk frame of V[t0]
+                    const bool ring = r.fs.nring != nullptr;
+                    const unsigned rg = ring ? (unsigned)r.fs.ring : 0u;
+                    unsigned slot0 = 0;
+                    if (ring) {   // (abs0 + f0 - lookback) mod ring, as feat8_ptr
+                        slot0 = (unsigned)(r.fs.abs0 + f0 - r.fs.lookback) + rg;
+                        slot0 = slot0 >= rg ? slot0 - rg : slot0;
+                        slot0 = slot0 >= rg ? slot0 - rg : slot0;
                     }
+                    const char* base = ring ? reinterpret_cast<const char*>(r.fs.nring) + (size_t)g1.s * rg * 80
+                                            : reinterpret_cast<const char*>(r.feats) + ((size_t)g1.s * r.T + f0) * 80;
+#pragma unroll
+                    for (int mm = 0; mm < (NU + 63) / 64; ++mm) {
+                        const int c = lane + 64 * mm;
+                        if (mm < NU / 64 || c < NU) {
+                            const int d0 = (c * 52429) >> 18;   // c / 5 (c < 2^14)
+                            const int part = c - 5 * d0;
+                            const unsigned d = (unsigned)min(d0, dmax);
+                            unsigned row = d;
+                            if (ring) {
+                                row = slot0 + d;
+                                row = row >= rg ? row - rg : row;
+                            }
+                            const char* src = base + (row * 80u + 16u * (unsigned)part);
+                            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                             (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
+                                                             16, 0, 0);
+                        }
+                    }
+                    return true;
                 }
-            };
-            if (G == 1)
-                union_g(std::integral_constant<int, 1>{});
-            else if (G == 2)
-                union_g(std::integral_constant<int, 2>{});
-            else
-                union_g(std::integral_constant<int, 4>{});
+            }
+#pragma unroll
+            for (int mm = 0; mm < (NU + 63) / 64; ++mm) {
+                int c = lane + 64 * mm;
+                asm volatile("" : "+v"(c));
+                if (mm < NU / 64 || c < NU) {
+                    const int k = c / (FR * 5), rem = c - k * (FR * 5), fr = rem / 5, part = rem - 5 * fr;
+                    Seg g = g1;
+                    if (G > 1) {
+                        g.s = __shfl(m.s, k);
+                        g.b = __shfl(m.b, k);
+                        g.L = __shfl(m.L, k);
+                        g.ph = __shfl(m.ph, k);
+                        g.ok = __shfl((int)m.ok, k) != 0;
+                    }
+                    const int idx = 2 * j0 + g.ph + fr;
+                    const int16_t* src = reinterpret_cast<const int16_t*>(&nnsp_proj_zero16);
+                    if (g.ok) {
+                        if (idx < 5)
+                            src = r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part;
+                        else if (idx - 5 < g.L)
+                            src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+                    }
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                                     (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
+                                                     16, 0, 0);
+                }
+            }
             return true;
         };
         // descriptors in flight are held packed (3 VGPRs instead of 5; the
@@ -475,7 +516,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                 for (int c = lane; c < 16 * XC; c += 64) {
                     const int row = c / XC, part = c - row * XC;
                     const int kx = row / SPT, jx = row - kx * SPT;
-                    const Seg g = seg_k(kx);
+                    const Seg g = G == 1 ? mine : seg_k(kx);
                     const int j = j0 + jx;
                     if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L) {
                         int4 v = *reinterpret_cast<const int4*>(U + row * PW::AS + 8 * part);
@@ -1452,8 +1493,13 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
 namespace {
 
 template <class SH>
-const void* proj_fn(bool acc32) {
-    return acc32 ? (const void*)proj_kernel<SH, true> : (const void*)proj_kernel<SH, false>;
+const void* proj_fn(bool acc32, int gpt) {
+    if constexpr (SH::generic) {
+        return acc32 ? (const void*)proj_kernel<SH, true, 1> : (const void*)proj_kernel<SH, false, 1>;
+    }
+    if (gpt == 4) return acc32 ? (const void*)proj_kernel<SH, true, 4> : (const void*)proj_kernel<SH, false, 4>;
+    if (gpt == 2) return acc32 ? (const void*)proj_kernel<SH, true, 2> : (const void*)proj_kernel<SH, false, 2>;
+    return acc32 ? (const void*)proj_kernel<SH, true, 1> : (const void*)proj_kernel<SH, false, 1>;
 }
 
 template <class SH, int RPW>
@@ -1461,12 +1507,12 @@ const void* recur_fn(bool acc32) {
     return acc32 ? (const void*)recur_kernel<SH, RPW, true> : (const void*)recur_kernel<SH, RPW, false>;
 }
 
-const void* pick_proj(int shape, bool acc32) {
+const void* pick_proj(int shape, bool acc32, int gpt) {
     switch (shape) {
-        case NN_SHAPE_VAD: return proj_fn<ShapeVad>(acc32);
-        case NN_SHAPE_KWS: return proj_fn<ShapeKws>(acc32);
-        case NN_SHAPE_S2I: return proj_fn<ShapeS2i>(acc32);
-        default: return proj_fn<ShapeGen>(acc32);
+        case NN_SHAPE_VAD: return proj_fn<ShapeVad>(acc32, gpt);
+        case NN_SHAPE_KWS: return proj_fn<ShapeKws>(acc32, gpt);
+        case NN_SHAPE_S2I: return proj_fn<ShapeS2i>(acc32, gpt);
+        default: return proj_fn<ShapeGen>(acc32, gpt);
     }
 }
 
@@ -1525,7 +1571,8 @@ size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int 
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, int waves, void* stream) {
     const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, waves, r->ep_n, r->shape);
-    return launch(pick_proj(r->shape, img->acc32 || r->ep32), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
+    if (r->shape != NN_SHAPE_GENERIC && r->gpt != 1 && r->gpt != 2 && r->gpt != 4) return (int)hipErrorInvalidValue;
+    return launch(pick_proj(r->shape, img->acc32 || r->ep32, r->gpt), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
 }
 
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const CascArgs_* ctl, void* stream) {
@@ -1558,9 +1605,10 @@ int nnspk_set_lds_limit(void) {
             int wv = 0;
             size_t tb = 0;
             const void* pipe = pick_pipe(shapes[i], a, &wv, &tb);
-            const void* fns[4] = {pick_proj(shapes[i], a), pick_recur(shapes[i], nrts[i], a),
-                                  pick_recur(NN_SHAPE_GENERIC, nrts[i], a), pipe};
-            for (int k = 0; k < 4; ++k) {
+            const void* fns[6] = {pick_proj(shapes[i], a, 1), pick_recur(shapes[i], nrts[i], a),
+                                  pick_recur(NN_SHAPE_GENERIC, nrts[i], a), pipe, pick_proj(shapes[i], a, 2),
+                                  pick_proj(shapes[i], a, 4)};
+            for (int k = 0; k < 6; ++k) {
                 if (!fns[k]) continue;
                 hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (e != hipSuccess) return (int)e;
