@@ -35,15 +35,20 @@ __device__ __forceinline__ int64_t mad_i64_i32(int32_t a, int32_t b, int64_t acc
     return r;
 }
 
-// sat32(((int64)a * b + (int64)c * d) >> 15) for int16 a, b, c and int32 d
-// (lstm.c's cell update): one v_mad_i64_i32, the shifted low word from one
-// funnel shift, and the range check on the high word in 32-bit compares
-// (|x| < 2^47: x >> 15 fits int32 iff x >> 46 is 0 or -1)
-__device__ __forceinline__ int32_t cell_q15(int32_t a, int32_t b, int32_t c, int32_t d) {
-    const int64_t x = mad_i64_i32(c, d, (int64_t)(a * b));
+// sat32(x >> 15) for any int64 x: the shifted low word from one funnel shift,
+// and the range check on the high word in 32-bit compares (x >> 15 fits int32
+// iff x >> 46 = hi >> 14 is 0 or -1) -- no 64-bit compares (v_cmp_*_i64 issue
+// at ~5x an add, profiles/microbench/valu_rates2)
+__device__ __forceinline__ int32_t sat32_shr15(int64_t x) {
     const int32_t hi = (int32_t)(x >> 32);
     const int32_t y = (int32_t)__builtin_amdgcn_alignbit((uint32_t)hi, (uint32_t)x, 15);
     return (uint32_t)((hi >> 14) + 1) < 2u ? y : ((hi >> 31) ^ INT32_MAX);
+}
+
+// sat32(((int64)a * b + (int64)c * d) >> 15) for int16 a, b, c and int32 d
+// (lstm.c's cell update): one v_mad_i64_i32 and sat32_shr15
+__device__ __forceinline__ int32_t cell_q15(int32_t a, int32_t b, int32_t c, int32_t d) {
+    return sat32_shr15(mad_i64_i32(c, d, (int64_t)(a * b)));
 }
 
 // SMMLAR / SMMULR contribution: floor((x*c + 2^31) / 2^32)

@@ -40,6 +40,10 @@ using namespace nnsp;
 #define FE_PAIR_DEFAULT 1   // fe_kernel2 (two frames per wave) for the batch mode
 #endif
 #define FE_X_DW 512   // dwords of one frame's complex buffer (256 complex)
+#define FE_P_DW 260   // dwords of the power spectrum P: bins 0..256 and the Mel segments' zero-coefficient
+                      // reads past them (segment start + 11 <= 257; tests/test_tables.py).  fe_kernel's
+                      // LDS is 27136 B = 53 x 512 B: six workgroups per CU (LDS is granted in 512-B
+                      // blocks -- at 264 the kernel took 27200 B, 54 blocks, five workgroups, -3 %)
 __device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (FE_MODE_COLD)
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
 
@@ -50,17 +54,18 @@ struct FeLane {
 // Block-shared constant tables (LDS).
 struct FeTables {
     int2 tw[3][3][64];    // per stage, twiddle (k, 2k, 3k) of each lane's butterfly: (cos, sin)
-    int4 split[256];      // per bin k: (A_re, A_im, B_re, nv) of realCoefA/BQ31 at 16k; nv: in
-                          // FE_MODE_SHARED, k < 120 net k/40's mean of Mel bank k%40,
-                          // 120 <= k < 240 its stdR (fe_norm_word); otherwise 0
+    int4 split[256];      // per bin k: (A_re, A_im, B_re, -) of realCoefA/BQ31 at 16k (PORT: rfft's twiddle)
+    int32_t norm[240];    // FE_MODE_SHARED: k < 120 net k/40's mean of Mel bank k%40, 120 <= k < 240 its
+                          // stdR (fe_norm_word) -- dense, so that 40 lanes read 40 banks
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
     uint4 win[64];        // per lane: window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
-    uint2 mc[3][64];      // per lane: Mel segment coefficients as int16 pairs (LDS, not VGPRs:
+    int16_t mc[12][64];   // per lane: its Mel segment's 12 coefficients, zero-padded, read with
+                          // sign-extending ds_read_i16 (no VALU unpacking; LDS, not VGPRs:
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
 };   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
 
-// the per-net normalisation constants ride in split[].w: a separate table
-// would push fe_kernel's LDS past 160 KB / 6 and cost a workgroup per CU
+// the per-net normalisation constants (norm[]; with the Mel pad at 264 the
+// tables and buffers stay within 160 KB / 6)
 __device__ __forceinline__ int32_t fe_norm_word(const FeArgs& a, int k) {
     if (a.mode != FE_MODE_SHARED || k >= 240) return 0;
     const int n = (k % 120) / 40, b = k % 40;
@@ -85,7 +90,7 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
                                       (uint32_t)nnsp_tbl_dif_tw[4 * k + 2], (uint32_t)nnsp_tbl_dif_tw[4 * k + 3]);
         }
         for (int k = threadIdx.x; k < 256; k += blockDim.x)   // rfft's twiddle of bin k (fft.c:103-105)
-            T.split[k] = make_int4(nnsp_tbl_dif_rtw[k], 0, 0, fe_norm_word(a, k));
+            T.split[k] = make_int4(nnsp_tbl_dif_rtw[k], 0, 0, 0);
     } else {
         for (int i = threadIdx.x; i < 576; i += blockDim.x) {
             const int s = i / 192, j = (i / 64) % 3, l = i % 64;
@@ -93,14 +98,14 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
             T.tw[s][j][l] = make_int2(nnsp_tbl_tw256[2 * (j + 1) * k], nnsp_tbl_tw256[2 * (j + 1) * k + 1]);
         }
         for (int k = threadIdx.x; k < 256; k += blockDim.x)
-            T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2],
-                                   fe_norm_word(a, k));
+            T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
     }
+    for (int k = threadIdx.x; k < 240; k += blockDim.x) T.norm[k] = fe_norm_word(a, k);
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        uint32_t w[4], c[6];
+        uint32_t w[4];
         for (int m = 0; m < 4; ++m) {
             const int i = 128 * m + 2 * lane;
             w[m] = i < 480 ? ((uint32_t)(uint16_t)nnsp_tbl_window[i] | ((uint32_t)(uint16_t)nnsp_tbl_window[i + 1] << 16))
@@ -108,13 +113,8 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
         }
         const int* sg = nnsp_tbl_melseg + 4 * lane;
         const int mn = sg[2];
-        for (int i = 0; i < 6; ++i) {
-            const int lo = 2 * i < mn ? nnsp_tbl_mel[sg[3] + 2 * i] : 0;
-            const int hi = 2 * i + 1 < mn ? nnsp_tbl_mel[sg[3] + 2 * i + 1] : 0;
-            c[i] = (uint32_t)(uint16_t)lo | ((uint32_t)(uint16_t)hi << 16);
-        }
+        for (int i = 0; i < 12; ++i) T.mc[i][lane] = (int16_t)(i < mn ? nnsp_tbl_mel[sg[3] + i] : 0);
         T.win[lane] = make_uint4(w[0], w[1], w[2], w[3]);
-        for (int j = 0; j < 3; ++j) T.mc[j][lane] = make_uint2(c[2 * j], c[2 * j + 1]);
     }
 }
 
@@ -320,8 +320,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
     // contiguous so that the padded T1 transpose may use both
-    __shared__ __attribute__((aligned(16))) int32_t XPs[4][FE_X_DW + 272];
-    __shared__ int64_t Ms[4][64];
+    __shared__ __attribute__((aligned(16))) int32_t XPs[4][FE_X_DW + FE_P_DW];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
     const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
@@ -342,7 +341,9 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = XPs[wv];
     int32_t* P = XPs[wv] + FE_X_DW;
-    int64_t* Mp = Ms[wv];
+    // the Mel partial sums go to X, dead once the split has read it (the next
+    // frame's cFFT writes X only after the frame's last wave_lds_sync)
+    int64_t* Mp = reinterpret_cast<int64_t*>(X);
     FeLane L;
     fe_lane_init(L, lane);
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
@@ -567,17 +568,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         {
             int64_t mac = 0;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint2 c2 = TB.mc[j][lane];
-                const uint32_t cc[2] = {c2.x, c2.y};
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int i = 2 * j + h;
-                    const int2 pv = make_int2(P[L.mj0 + 2 * i], P[L.mj0 + 2 * i + 1]);
-                    mac = mad_i64_i32((int32_t)(int16_t)(cc[h] & 0xffff), pv.x, mac);
-                    mac = mad_i64_i32((int32_t)cc[h] >> 16, pv.y, mac);
-                }
-            }
+            for (int i = 0; i < 12; ++i) mac = mad_i64_i32((int32_t)TB.mc[i][lane], P[L.mj0 + i], mac);
             Mp[lane] = mac;
         }
         wave_lds_sync();
@@ -590,7 +581,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
 #pragma unroll
             for (int k = 0; k < FE_MEL_MAXSEG; ++k)
                 if (k < L.mcnt) mac += Mp[L.mfirst + k];
-            const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
+            const int32_t lg = log10_q15_lds(sat32_shr15(mac), TB.logp);
             if (MODE == FE_MODE_BATCH && a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
             if constexpr (shared) {
                 // (abs0 + t) % ring with t < T <= ring: one conditional subtract
@@ -603,7 +594,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
                 int16_t nv[3];
 #pragma unroll
                 for (int n = 0; n < 3; ++n) {   // each net's normalisation (feature_module.c:67-73)
-                    const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
+                    const int32_t mn = TB.norm[40 * n + lane], sr = TB.norm[120 + 40 * n + lane];
                     nv[n] = fe_norm(lg, mn, sr, a.nshift[n], a.norm32);
                 }
                 pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
@@ -686,7 +677,7 @@ __device__ __forceinline__ void wave_cfft256x2(int32_t (&va)[8], int32_t (&vb)[8
 template <int MODE, bool PORT>
 __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
     static_assert(MODE != FE_MODE_COLD, "the cold front end runs fe_kernel");
-    __shared__ __attribute__((aligned(16))) int32_t XPs[4][2][FE_X_DW + 272];
+    __shared__ __attribute__((aligned(16))) int32_t XPs[4][2][FE_X_DW + FE_P_DW];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
     const unsigned W = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
@@ -801,7 +792,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
 #pragma unroll
             for (int k = 0; k < FE_MEL_MAXSEG; ++k)
                 if (k < L.mcnt) mac += Mq[L.mfirst + k];
-            const int32_t lg = log10_q15_lds(sat32(mac >> 15), TB.logp);
+            const int32_t lg = log10_q15_lds(sat32_shr15(mac), TB.logp);
             if constexpr (shared) {
                 unsigned slot = ring0 + (unsigned)p.t;
                 if (slot >= (unsigned)a.ring) slot -= (unsigned)a.ring;
@@ -810,7 +801,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
                 int16_t nv[3];
 #pragma unroll
                 for (int n = 0; n < 3; ++n) {
-                    const int32_t mn = TB.split[40 * n + lane].w, sr = TB.split[120 + 40 * n + lane].w;
+                    const int32_t mn = TB.norm[40 * n + lane], sr = TB.norm[120 + 40 * n + lane];
                     nv[n] = fe_norm(lg, mn, sr, a.nshift[n], a.norm32);
                 }
                 pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
@@ -898,20 +889,10 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
         {   // Mel (melSpecProc.c:6-27) of both frames; partial sums into the dead X
             int64_t ma = 0, mb = 0;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) {
-                const uint2 c2 = TB.mc[j][lane];
-                const uint32_t cc[2] = {c2.x, c2.y};
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int i = 2 * j + h;
-                    const int2 pa = make_int2(PA[L.mj0 + 2 * i], PA[L.mj0 + 2 * i + 1]);
-                    const int2 pb = make_int2(PB[L.mj0 + 2 * i], PB[L.mj0 + 2 * i + 1]);
-                    const int32_t c0 = (int32_t)(int16_t)(cc[h] & 0xffff), c1 = (int32_t)cc[h] >> 16;
-                    ma = mad_i64_i32(c0, pa.x, ma);
-                    mb = mad_i64_i32(c0, pb.x, mb);
-                    ma = mad_i64_i32(c1, pa.y, ma);
-                    mb = mad_i64_i32(c1, pb.y, mb);
-                }
+            for (int i = 0; i < 12; ++i) {
+                const int32_t c0 = TB.mc[i][lane];
+                ma = mad_i64_i32(c0, PA[L.mj0 + i], ma);
+                mb = mad_i64_i32(c0, PB[L.mj0 + i], mb);
             }
             reinterpret_cast<int64_t*>(XA)[lane] = ma;
             reinterpret_cast<int64_t*>(XB)[lane] = mb;

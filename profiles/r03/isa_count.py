@@ -54,7 +54,9 @@ def main():
         if m and m.group(1) in labels and labels[m.group(1)] < i:
             loops.append((i - labels[m.group(1)], labels[m.group(1)], i))
     loops.sort(reverse=True)
-    n, a, b = loops[0]
+    # the hot loop: the largest one holding the kernel's q31 products
+    hot = [lp for lp in loops if any(("v_mul_hi_i32" in l or "v_mfma" in l) for l in L[lp[1]:lp[2] + 1])]
+    n, a, b = (hot or loops)[0]
     c = Counter()
     ops = Counter()
     for l in L[a:b + 1]:

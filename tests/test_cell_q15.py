@@ -35,3 +35,14 @@ def test_cell_q15_matches_sat32_random():
     cc = rng.integers(-2**31, 2**31, n)
     x = a * b + f * cc
     np.testing.assert_array_equal(_cell_q15(x), _sat32_ref(x))
+
+
+def test_sat32_shr15_any_int64():
+    """nnsp_dev.h's sat32_shr15 (the same check, used on the front end's Mel
+    sums) holds over the whole int64 range, not only the cell's |x| < 2^47."""
+    rng = np.random.default_rng(11)
+    edges = np.array([-2**63, -2**63 + 1, -2**46 - 1, -2**46, -2**46 + 1, -1, 0, 1, 2**46 - 1, 2**46,
+                      2**46 + 1, 2**63 - 1], np.int64)
+    x = np.concatenate([edges, rng.integers(-2**63, 2**63 - 1, 1 << 20, dtype=np.int64),
+                        rng.integers(-2**48, 2**48, 1 << 20, dtype=np.int64)])
+    np.testing.assert_array_equal(_cell_q15(x), _sat32_ref(x))
