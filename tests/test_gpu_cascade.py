@@ -97,6 +97,20 @@ def test_cascade_control_kernel(th, monkeypatch):
     assert _check(oc, gc, _pcm(S, sum(chunks), 12), chunks) > 50
 
 
+@pytest.mark.parametrize("knob", ["NNSP_CASCADE_SERIAL", "NNSP_CASCADE_DEBUG", "NNSP_CASCADE_TIMING",
+                                  "NNSP_CASCADE_WINDOW", "NNSP_RECUR_CLOCKS"])
+def test_cascade_development_knobs_keep_results(knob, monkeypatch):
+    """The library's remaining environment switches are development aids --
+    every net on one stream (SERIAL), a synchronisation after every launch
+    (DEBUG), per-round event timing (TIMING), a fixed round window (WINDOW),
+    the s_memtime probes of the NN and front-end kernels (RECUR_CLOCKS): none
+    may change a result."""
+    monkeypatch.setenv(knob, "7" if knob == "NNSP_CASCADE_WINDOW" else "1")
+    S, chunks = 90, [100, 37, 1, 63]
+    oc, gc, _ = _build(TH["lively"], S, max(chunks), False, (1, 2, 0), 80, 60, 80, 50)
+    assert _check(oc, gc, _pcm(S, sum(chunks), 13), chunks) > 30
+
+
 @pytest.mark.parametrize("ctl", ["fused", "kernel"])
 def test_cascade_short_lookback_timeouts_and_order(ctl, monkeypatch):
     # odd look-backs, tiny timeouts (counter wrap), a different sequence order

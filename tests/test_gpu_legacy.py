@@ -58,6 +58,18 @@ def test_front_end_stages():
         np.testing.assert_array_equal(lg, O.log10(m))
 
 
+def test_spec2pspec_arm_any_length():
+    """spec2pspec_arm over vectors longer than one frame's 257 bins (the
+    reference loops over len; the device buffer is sized per call)."""
+    rng = np.random.default_rng(3)
+    for n in (1, 1024, 1025, 5000):
+        spec = rng.integers(-2 ** 31 + 1, 2 ** 31, 2 * n).astype(np.int32)   # (no int64 overflow)
+        got = np.zeros(n, np.int32)
+        L().spec2pspec_arm(vp(got), vp(spec), n)
+        ref = ((spec[0::2].astype(np.int64) ** 2 + spec[1::2].astype(np.int64) ** 2) >> 27)
+        np.testing.assert_array_equal(got, ref.astype(np.uint64).astype(np.uint32).view(np.int32))
+
+
 @pytest.mark.parametrize("kind", [0, 1, 2, 3])
 def test_activations(kind):
     x = np.concatenate([np.arange(-200000, 200000, 97), [0, 1, -1, 2 ** 31 - 1, -2 ** 31 + 1]]).astype(np.int32)
