@@ -22,7 +22,7 @@ def main():
         t0 = int(rows[bi]['Start_Timestamp'])
         end = next((b for b in begins if b > bi), len(rows))
         print('--- chunk')
-        for r in rows[bi:end]:
+        for r in rows[max(0, bi - 2):end]:
             s = (int(r['Start_Timestamp']) - t0) / 1e3
             e = (int(r['End_Timestamp']) - t0) / 1e3
             print(f"{short(r['Kernel_Name'])[:48]:48s} {s:8.1f} {e:8.1f} {e - s:7.1f}  grid {r['Grid_Size_X']} wg {r['Workgroup_Size_X']}")
