@@ -373,14 +373,6 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.ep_n = b->ep_proj;
         f.n_list_dev = seg->n_list_dev;
         f.n_list_rec = seg->n_list_rec;
-        f.prio = seg->prio;
-        if (seg->n_host >= 0 && seg->n_list_dev) {   /* the list length is known: grids sized to it */
-            if (seg->n_host == 0) {
-                if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
-                return 0;
-            }
-            f.grid_cap = (seg->n_host + 15) / 16;   /* one 16-stream tile per workgroup (TPW 1) */
-        }
         {   /* proj tiles: pack 2 or 4 streams per 16-row tile when a segment has <= 8 / 4 NN steps */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
             const int steps = (W + 1) / 2;
@@ -390,12 +382,6 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         if (seg->list && !seg->n_list_dev) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
             const long long pt = (long long)seg->n_list * ((W / 2 + 1 + 15) / 16);
-            const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
-            if (need < blocks) blocks = (int)need;
-        }
-        if (seg->n_host >= 0 && seg->n_list_dev) {
-            const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
-            const long long pt = (long long)seg->n_host * ((W / 2 + 1 + 15) / 16);
             const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
             if (need < blocks) blocks = (int)need;
         }

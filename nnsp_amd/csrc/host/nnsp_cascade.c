@@ -114,15 +114,6 @@ struct nnsp_cascade {
     int book_rounds;                /* rounds launched in that chunk */
     int book_ahead, book_ahead_done; /* its look-ahead front end ran; its own front end ran ahead */
     unsigned long long book_frames[3];
-    /* front end beside the rounds (NNSP_COFE=ka,free,grab,kb,vadmask): the
-     * next chunk's shared front end as persistent workgroups (ka per CU, on
-     * the CUs outside `free`) launched with round 0, the rest of it taken by
-     * kb more per CU after the rounds; both take frame runs from one counter */
-    int cofe_ka, cofe_free, cofe_grab, cofe_kb, cofe_vadmask, cofe_prio, cofe_when, cofe_static;
-    void *fe_stream, *vad_stream;
-    unsigned *d_fework;             /* [2] by chunk parity */
-    void *ev_cofe_go, *ev_cofe_done;
-    void *h_cnt, *ev_cnt;           /* pinned: the list lengths of the next round, read by the host */
 };
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
@@ -296,20 +287,6 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
         c->debug = getenv("NNSP_CASCADE_DEBUG") != NULL;
-        const char *cf = getenv("NNSP_COFE");
-        if (cf && sscanf(cf, "%d,%d,%d,%d,%d,%d,%d,%d", &c->cofe_ka, &c->cofe_free, &c->cofe_grab, &c->cofe_kb,
-                         &c->cofe_vadmask, &c->cofe_prio, &c->cofe_when, &c->cofe_static) >= 1 && c->cofe_ka > 0) {
-            if (c->cofe_grab <= 0) c->cofe_grab = 25;
-            if (c->cofe_kb <= 0) c->cofe_kb = 6;
-            if ((e = nnspk_stream_create_cumask(&c->fe_stream, c->cofe_free, 0))) goto fail;
-            if (c->cofe_vadmask && (e = nnspk_stream_create_cumask(&c->vad_stream, c->cofe_free, 0))) goto fail;
-            if (c->vad_stream) c->ns[1] = c->vad_stream;
-            if ((e = nnspk_malloc((void **)&c->d_fework, 2 * sizeof(unsigned)))) goto fail;
-            if ((e = nnspk_event_create(&c->ev_cofe_go)) || (e = nnspk_event_create(&c->ev_cofe_done))) goto fail;
-            if ((e = nnspk_event_create(&c->ev_cnt)) || (e = nnspk_host_alloc(&c->h_cnt, 64))) goto fail;
-        } else {
-            c->cofe_ka = 0;
-        }
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
             c->window = atoi(w);
@@ -355,14 +332,6 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         c->ns[n] = NULL; /* the batch's stream, owned by the batch */
     }
     nnspk_stream_destroy(c->stream);
-    if (c->fe_stream) nnspk_sync(c->fe_stream);
-    nnspk_stream_destroy(c->fe_stream);
-    nnspk_stream_destroy(c->vad_stream);
-    nnspk_free(c->d_fework);
-    nnspk_event_destroy(c->ev_cofe_go);
-    nnspk_event_destroy(c->ev_cofe_done);
-    nnspk_event_destroy(c->ev_cnt);
-    nnspk_host_free(c->h_cnt);
     nnspk_event_destroy(c->ev_book);
     nnspk_host_free(c->h_book);
     free(c);
@@ -412,9 +381,8 @@ static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n
 }
 
 static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, int T, const int32_t *cnt,
-                            const int16_t *hist, void *stream, int n_cold)
+                            const int16_t *hist, void *stream)
 {
-    if (n_cold == 0) return 0;
     nnsp_batch *b = c->net[n];
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
@@ -440,15 +408,13 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     fa.norm32 = b->norm32;
     fa.list = c->d_cold_list[r & 1][n];
     fa.n_list_dev = cnt + 3 + n;
-    fa.prio = c->cofe_prio;
-    if (n_cold > 0) fa.pgrid = (n_cold * 2 + 3) / 4;   /* <= 2 frames per stream, 4 waves per workgroup */
     return nnspk_launch_fe(&fa, stream);
 }
 
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
 static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
-                    void *proj_done, int n_host)
+                    void *proj_done)
 {
     const int timed = c->timing && r < MAX_TIMED;
     nnsp_segment seg;
@@ -468,8 +434,6 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
     seg.fs = a->fs[n];
     seg.n_list_rec = r < MAX_TIMED ? c->d_rcount + 3 * r + n : NULL;
     seg.ctl = c->fused ? a : NULL;
-    seg.prio = c->cofe_prio;
-    seg.n_host = n_host;
     TRY(nnsp_batch_run_nn(c->net[n], T, c->fused ? NULL : c->d_trig[n], NULL, &seg, st));
     DBG(st, "proj + recur", n, r);
     if (timed) TRY(nnspk_event_record(c->ev_t[r][n][2], st));
@@ -487,8 +451,7 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
  * runs the controller for its streams and lists them for the next round, so
  * a net's next round waits only for the other two nets' end of this round.
  * Otherwise: join, casc_control on the main stream, fork. */
-static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm, int T, const int16_t *hist,
-                        const int32_t *lens)
+static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm, int T, const int16_t *hist)
 {
     int32_t *cur = c->d_counts + 6 * (r % 3);
     a->counts = c->d_counts + 6 * ((r + 1) % 3);
@@ -526,10 +489,10 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
             TRY(nnspk_stream_wait(st, c->ev_fork));
         }
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][0], st));
-        TRY(segment_features(c, n, r, pcm, T, cur, hist, st, lens ? lens[3 + n] : -1));
+        TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
-        TRY(round_nn(c, a, r, n, T, cur, hist, st, vad_first && n == 1 ? c->ev_vad_proj : NULL, lens ? lens[n] : -1));
+        TRY(round_nn(c, a, r, n, T, cur, hist, st, vad_first && n == 1 ? c->ev_vad_proj : NULL));
     }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);
@@ -548,16 +511,11 @@ static int join_rounds(nnsp_cascade *c, int r)
  * when T >= H) on the cascade's stream.  tail: the samples of the two frames
  * before the chunk, tail_stride apart per stream. */
 static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *tail, int tail_stride, int abs0,
-                     long long k, unsigned *work, int pgrid, int dstatic, void *stream)
+                     long long k, int ahead, void *stream)
 {
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
-    fa.work = work;
-    fa.grab = c->cofe_grab;
-    fa.pgrid = pgrid;
-    /* the first cofe_static permille of the frames split statically over the co-running launch */
-    fa.dyn_base = (int32_t)(((long long)c->S * T * c->cofe_static / 1000) / 100 * 100);
-    fa.dyn_static = dstatic;
+    (void)ahead;
     fa.pcm = pcm;
     fa.tail = tail;
     fa.tail_stride = tail_stride;
@@ -652,17 +610,6 @@ static int book_take(nnsp_cascade *c)
     return 0;
 }
 
-/* the co-running part of the next chunk's front end (NNSP_COFE) on fe_stream */
-static int cofe_launch_a(nnsp_cascade *c, const int16_t *next_pcm, int next_T, const int16_t *pcm, int T, long long k,
-                         int q1)
-{
-    TRY(nnspk_event_record(c->ev_ahead[q1][0], c->fe_stream));
-    const int cus = 256 - (c->cofe_free / 8) * 8;
-    TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring, k + 1,
-                  c->d_fework + q1, cus * c->cofe_ka, 1, c->fe_stream));
-    return nnspk_event_record(c->ev_cofe_done, c->fe_stream);
-}
-
 int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t *net_ran, int16_t *detected,
                              int16_t *outputs3)
 {
@@ -694,7 +641,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
     TRY(nnspk_event_record(c->ev_fe[0], c->stream));
-    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, NULL, 0, 0, c->stream));
+    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0, c->stream));
     DBG(c->stream, "shared front end", -1, -1);
     TRY(nnspk_event_record(c->ev_fe[1], c->stream));
     c->sfe_ahead = ahead_done;
@@ -711,15 +658,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         a.list[n] = c->d_list[0][n];
         a.cold_list[n] = c->d_cold_list[0][n];
     }
-    const int cofe = ahead && c->cofe_ka > 0;
-    const int q1 = (int)((k + 1) & 1);
-    if (cofe) {   /* the next chunk's front end, persistent, beside the rounds */
-        TRY(nnspk_memset(c->d_fework + q1, 0, sizeof(unsigned), c->stream));
-        TRY(nnspk_event_record(c->ev_cofe_go, c->stream));
-        TRY(nnspk_stream_wait(c->fe_stream, c->ev_cofe_go));
-        TRY(ahead_read(c, q1, 1));
-        if (!c->cofe_when) TRY(cofe_launch_a(c, next_pcm, next_T, pcm, T, k, q1));
-    }
     TRY(nnspk_launch_casc_begin(&a, c->stream));
     DBG(c->stream, "casc_begin", -1, -1);
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
@@ -729,43 +667,16 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
      * its workgroups capped or short-lived, or on a CU partition, it slowed
      * the rounds more than it gained (profiles/r02/sched) */
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
-    if (cofe) {
-        /* round 0 on the whole device; the front end of the next chunk then
-         * takes the CUs outside `free` while rounds 1.. run on the rest, each
-         * launched with grids sized to its list lengths (read by the host once
-         * the previous round has ended: device-sized grids of early-exiting
-         * workgroups would each wait for a free CU first) */
-        TRY(launch_round(c, &a, 0, pcm, T, hist, NULL));
-        if (c->cofe_when) {
-            for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->fe_stream, c->ev_rnd[0][n]));
-            TRY(cofe_launch_a(c, next_pcm, next_T, pcm, T, k, q1));
-        }
-        for (r = 1;; ++r) {
-            for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[(r - 1) & 1][n]));
-            TRY(nnspk_d2h(c->h_cnt, c->d_counts + 6 * (r % 3), 6 * sizeof(int32_t), c->stream));
-            TRY(nnspk_event_record(c->ev_cnt, c->stream));
-            TRY(nnspk_event_sync(c->ev_cnt));
-            int32_t lens[6];
-            memcpy(lens, c->h_cnt, sizeof lens);
-            if (lens[0] + lens[1] + lens[2] == 0) break;
-            TRY(launch_round(c, &a, r, pcm, T, hist, lens));
-        }
-        R = r;
-    }
     for (;;) {
         for (; r < R; ++r) {
-            TRY(launch_round(c, &a, r, pcm, T, hist, NULL));
-            if (cofe && c->cofe_when && r == 0) {   /* after round 0 */
-                for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->fe_stream, c->ev_rnd[0][n]));
-                TRY(cofe_launch_a(c, next_pcm, next_T, pcm, T, k, q1));
-            }
-            if (ahead && !cofe && !ahead_launched) {
+            TRY(launch_round(c, &a, r, pcm, T, hist));
+            if (ahead && !ahead_launched) {
                 for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[r & 1][n]));
                 const int q = (int)((k + 1) & 1);
                 TRY(ahead_read(c, q, 1)); /* slot q's last front end (two chunks ago) is long done */
                 TRY(nnspk_event_record(c->ev_ahead[q][0], c->stream));
                 TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring,
-                              k + 1, NULL, 0, 0, c->stream));
+                              k + 1, 1, c->stream));
                 TRY(nnspk_event_record(c->ev_ahead[q][1], c->stream));
                 c->ahead_pending[q] = 1;
                 ahead_launched = 1;
@@ -773,14 +684,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         }
         TRY(join_rounds(c, r));
         TRY(nnspk_event_record(c->ev[1], c->stream)); /* the rounds' end (complete at the sync below) */
-        if (cofe && !ahead_launched) {   /* the rest of the next chunk's front end on the whole device */
-            TRY(shared_fe(c, next_pcm, next_T, pcm + (size_t)(T - 2) * 160, T * 160, (c->abs0 + T) % c->ring, k + 1,
-                          c->d_fework + q1, 256 * c->cofe_kb, 0, c->stream));
-            TRY(nnspk_stream_wait(c->stream, c->ev_cofe_done));
-            TRY(nnspk_event_record(c->ev_ahead[q1][1], c->stream));
-            c->ahead_pending[q1] = 1;
-            ahead_launched = 1;
-        }
         /* all the chunk's counters in one copy (the next round's list lengths
          * among them): if no round is left they are final, and the
          * bookkeeping needs no further host wait */

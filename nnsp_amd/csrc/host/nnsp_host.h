@@ -94,8 +94,6 @@ typedef struct {
     const CascArgs *ctl;       /* cascade: controller fused into recur (NULL: none) */
     void *proj_done;           /* non-NULL: recorded on the stream once the prefix FC layers are done
                                   (split path: between proj and recur; fused kernel: after it) */
-    int prio;                  /* 1: the kernels' waves raise their issue priority (s_setprio 3) */
-    int n_host;                /* >= 0: the device list's length, known to the host (grids sized to it; 0: no launch) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,

@@ -303,7 +303,6 @@ __device__ __attribute__((aligned(16))) int4 nnsp_proj_zero16;
 // instantiation each, so a G = 1 tile's descriptors are wave-uniform scalars)
 template <class SH, bool ACC32, int GT>
 __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) {   // <= 128 VGPRs: 4 waves per SIMD
-    if (r.prio) __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
@@ -1021,7 +1020,6 @@ struct alignas(16) PipeTile {
 template <class SH, bool ACC32>
 __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
                                                                                             CascArgs ca) {
-    if (r.prio) __builtin_amdgcn_s_setprio(3);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     using CF = PipeCfg<SH>;
     using PT = PipeTile<SH>;
@@ -1589,9 +1587,7 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const Casc
         const int tpw = r->shape == NN_SHAPE_VAD ? PipeCfg<ShapeVad>::TPW
                                                  : (r->shape == NN_SHAPE_KWS ? PipeCfg<ShapeKws>::TPW : PipeCfg<ShapeS2i>::TPW);
         const int tiles = (nrow + 15) / 16;
-        int blocks = (tiles + tpw - 1) / tpw;
-        if (r->grid_cap > 0 && blocks > r->grid_cap) blocks = r->grid_cap;   // the host knows the list length
-        return launch(fn, dim3(blocks), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
+        return launch(fn, dim3((tiles + tpw - 1) / tpw), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
     }
     if (ctl) return (int)hipErrorInvalidValue;   // fused control needs the pipelined kernel
     const int tiles = (nrow + 15) / 16;

@@ -82,15 +82,7 @@ typedef struct {
                                  workgroup 0, its first 64 frames: dbg_clk[1024 + 8 * frame + phase] */
     int32_t norm32;           /* 1: every normalisation's (feature - mean) * stdR >> shift provably fits
                                  int32 (nnsp_norm_fits32): the 32-bit clamp path */
-    /* FE_MODE_SHARED, work non-NULL: persistent workgroups (grid pgrid) take
-     * runs of `grab` frames from the device counter *work (zero before the
-     * first launch on it); several launches may share one counter and split
-     * the chunk between them (the cascade's front end beside its rounds) */
-    int32_t grab;
-    unsigned *work;
-    int32_t pgrid, prio;      /* prio: as FastRun.prio */
-    int32_t dyn_base;         /* frames below it are not in the counter's pool (work: pool frame = dyn_base + counter) */
-    int32_t dyn_static;       /* 1: this launch's waves split frames [0, dyn_base) statically first */
+    int32_t pad3_;
 } FeArgs;
 
 /* feature_module.c:67-73 in 32 bits: |log10 output| < 2^18 (|table| * 0x3796 >> 15
@@ -197,8 +189,6 @@ typedef struct {
      * int16 output, [S][nstep_max][xs] with xs = 16 * ceil(N / 16)) instead of
      * the int32 gate sums gx; recur computes Wx.x itself on MFMA */
     int16_t *xg;
-    int32_t prio;             /* waves raise their issue priority (s_setprio 3) over co-resident kernels */
-    int32_t grid_cap;         /* > 0: the pipelined recur's grid (the host knows the list length <= 16 * TPW * grid_cap) */
 } FastRun;
 
 /* Legacy row-block primitives (affine_Krows_8x16*, rc_Krows_8x16*, rc_8x16*):
@@ -288,10 +278,8 @@ int nnspk_set_device(int d);
 int nnspk_get_device(int *d);
 const char *nnspk_error_string(int e);
 int nnspk_stream_create(void **s);
-/* a stream whose kernels run only on a subset of the CUs: with `free` > 0 the
- * first free / 8 CUs of each XCD (logical CU i sits on XCD i % 8) are left out
- * (invert = 0) or are the only ones used (invert = 1) */
-int nnspk_stream_create_cumask(void **s, int free, int invert);
+/* high != 0: the device's greatest stream priority (its kernels' workgroups
+ * are dispatched ahead of normal-priority streams' when both wait) */
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);

@@ -315,10 +315,7 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // 80-VGPR budget of six waves per SIMD without the shared mode's ring writes.
 // PORT: the ARM_OPTIMIZED=0 build's front end (row N4: Frac15 window, fft.c's
 // rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
-// DYN (FE_MODE_SHARED only): persistent workgroups take runs of a.grab frames
-// from the device counter a.work; a wave claims its next run one run ahead and
-// prefetches across the run boundary (several launches may share a counter).
-template <int MODE, bool PORT, bool DYN = false>
+template <int MODE, bool PORT>
 __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
@@ -333,12 +330,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
     const unsigned nw = gridDim.x * 4u;
     const unsigned per = (nfr + nw - 1) / nw;
-    // persistent mode (shared front end beside the cascade's rounds): runs of
-    // G frames from the counter, the next run claimed one run ahead
-    static_assert(!DYN || MODE == FE_MODE_SHARED, "persistent front end: shared mode only");
-    if (MODE == FE_MODE_COLD && a.prio) __builtin_amdgcn_s_setprio(3);
-    constexpr bool dyn = DYN;
-    if (!dyn && blockIdx.x * 4u * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
+    if (blockIdx.x * 4u * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after the tables, at the end, and the frames it ran
     const unsigned wid0 = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -358,26 +350,8 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
     const unsigned wid = blockIdx.x * 4u + (unsigned)wv;
-    // claim: lane 0's atomic, read (readfirstlane) only when the run ends
-    // (frames below a.dyn_base: split statically over this launch's waves when
-    // a.dyn_static, the dynamic pool starts there)
-    const unsigned dbase = dyn ? (unsigned)a.dyn_base : 0u;
-    auto claim = [&]() -> unsigned { return lane == 0 ? dbase + atomicAdd(a.work, (unsigned)a.grab) : 0u; };
-    unsigned fbeg, fend, nclaim = 0u;
-    if (dyn) {
-        const unsigned ps = a.dyn_static ? (dbase + nw - 1) / nw : 0u;
-        fbeg = wid * ps < dbase ? wid * ps : dbase;
-        fend = fbeg + ps < dbase ? fbeg + ps : dbase;
-        nclaim = claim();
-        if (fbeg >= fend) {
-            fbeg = (unsigned)__builtin_amdgcn_readfirstlane((int)nclaim);
-            fend = fbeg + (unsigned)a.grab < nfr ? fbeg + (unsigned)a.grab : nfr;
-            nclaim = claim();
-        }
-    } else {
-        fbeg = wid * per;
-        fend = fbeg + per < nfr ? fbeg + per : nfr;
-    }
+    const unsigned fbeg = wid * per;
+    const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
     if (wclk) wclk[1] = (long long)__builtin_amdgcn_s_memrealtime();
     // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
     // T); walked incrementally (no per-frame division)
@@ -488,7 +462,6 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         FCLK(0);
         const Pos cur = nx;
         if (cur.t >= cur.lim) {   // wave-uniform: nothing to compute, only the next prefetch
-                                  // (never in the shared mode: every frame of the chunk runs)
             if (f + 1 < fend) {
                 advance(nx);
                 if (nx.t < nx.lim) load_frame(nx, raw);
@@ -527,18 +500,6 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
         if (f + 1 < fend) {   // prefetch the next frame's window (raw is free now)
             advance(nx);
             if (nx.t < nx.lim) load_frame(nx, raw);
-        } else if (dyn) {     // the run's last frame: the next run (claimed a run ago)
-            const unsigned nb = (unsigned)__builtin_amdgcn_readfirstlane((int)nclaim);
-            if (nb < nfr) {
-                f = nb - 1u;
-                fend = nb + (unsigned)a.grab < nfr ? nb + (unsigned)a.grab : nfr;
-                nclaim = claim();
-                nx.i = nb / W;
-                nx.k = nb - nx.i * W;
-                row_of(nx);
-                nx.t = nx.b + (int)nx.k;
-                if (nx.t < nx.lim) load_frame(nx, raw);
-            }
         }
         // the previous frame's features, after the loads: a wait the compiler
         // puts into the prefetch code (path merges) must not cover them
@@ -1708,14 +1669,9 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // the later generations' workgroup turnover lets the nets' rounds in)
     const long long cap = 256LL * 6 * 4;
     if (blocks > cap) blocks = cap;
-    if (a->mode == FE_MODE_SHARED && a->work) {   // persistent workgroups sharing a->work
-        if (a->grab <= 0 || a->pgrid <= 0) return (int)hipErrorInvalidValue;
-        blocks = a->pgrid;
-    }
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 2048) blocks = 2048;
-    if (a->mode == FE_MODE_COLD && a->pgrid > 0 && blocks > a->pgrid) blocks = a->pgrid;
     const dim3 g((unsigned)blocks), blk(256);
     hipStream_t st = (hipStream_t)stream;
     // two frames per wave (fe_kernel2): FE_PAIR_DEFAULT = 0 off, 1 the batch
@@ -1725,7 +1681,7 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     constexpr int pair = FE_PAIR_DEFAULT;
     const bool use_pair = a->mode == FE_MODE_BATCH ? pair >= 1 : (a->mode == FE_MODE_SHARED && pair >= 2);
     // (no segments: every frame of a listed row is inside the chunk)
-    if (use_pair && !a->work && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk) {
+    if (use_pair && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk) {
         // whole multiples of the resident workgroups at four per CU
         long long b2 = (nfr + 7) / 8;
         if (b2 > 256LL * 4 * 4) b2 = 256LL * 4 * 4;
@@ -1739,10 +1695,7 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
         }
         return ok(hipGetLastError());
     }
-    if (a->mode == FE_MODE_SHARED && a->work) {
-        if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, true, true>), g, blk, 0, st, *a);
-        else hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, false, true>), g, blk, 0, st, *a);
-    } else if (a->mode == FE_MODE_SHARED) {
+    if (a->mode == FE_MODE_SHARED) {
         if (a->port) hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, true>), g, blk, 0, st, *a);
         else hipLaunchKernelGGL((fe_kernel<FE_MODE_SHARED, false>), g, blk, 0, st, *a);
     } else if (a->mode == FE_MODE_COLD) {
@@ -1910,18 +1863,6 @@ int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
 const char* nnspk_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 int nnspk_stream_create(void** s) { return ok(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); }
-int nnspk_stream_create_cumask(void** s, int free, int invert) {
-    int n = 0;
-    hipError_t e = hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, 0);
-    if (e != hipSuccess) return (int)e;
-    if (n <= 0 || n > 1024 || n % 8 || free <= 0 || free >= n) return nnspk_stream_create(s);
-    uint32_t m[32] = {0};
-    for (int i = 0; i < n; ++i) {
-        const bool in_free = i / 8 < free / 8;
-        if (in_free == (invert != 0)) m[i / 32] |= 1u << (i % 32);
-    }
-    return ok(hipExtStreamCreateWithCUMask((hipStream_t*)s, (uint32_t)(n / 32), m));
-}
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }
