@@ -650,9 +650,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
      * write (cold frames read d_hist[k % 3]; the look-ahead front end takes
      * its tail from pcm) -- queued now, off the chunk's tail */
     const int16_t *hist = c->d_hist[k % 3];
-    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
-        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
-    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     a.counts = c->d_counts; /* round 0's lists */
     for (int n = 0; n < 3; ++n) {
         a.list[n] = c->d_list[0][n];
@@ -661,11 +658,20 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     TRY(nnspk_launch_casc_begin(&a, c->stream));
     DBG(c->stream, "casc_begin", -1, -1);
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
+    /* behind the fork (off round 0's start): nothing in this chunk reads what
+     * they write -- the cold frames read d_hist[k % 3], the look-ahead front
+     * end takes its tail from pcm */
+    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
+        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
+    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
     int ahead_launched = 0;
     /* the look-ahead front end starts once the nets' first round (the bulk of
      * the chunk's NN work) is done: running beside it from the start, or with
      * its workgroups capped or short-lived, or on a CU partition, it slowed
-     * the rounds more than it gained (profiles/r02/sched) */
+     * the rounds more than it gained (profiles/r02/sched; round 3, persistent
+     * and CU-masked variants: profiles/r03/cofe/README.md); started once VAD's
+     * round 0 is done and S2I's and KWS's recurrences are queued: 0.975 vs
+     * 0.992 G (4 paired runs) */
     int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
     for (;;) {
         for (; r < R; ++r) {

@@ -1166,6 +1166,15 @@ __global__ __launch_bounds__(64) void tail_roll_kernel(int16_t* tail, const int1
     for (int k = 0; k < 5; ++k) tail[(size_t)s * 320 + threadIdx.x + 64 * k] = v[k];
 }
 
+// the common case of tail_roll (every stream, whole chunk, T >= 2, no
+// look-back): the tail := the chunk's last two frames, 16 bytes per thread
+__global__ __launch_bounds__(256) void tail_copy_kernel(uint4* tail, const int16_t* pcm, int S, int T) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;   // 40 uint4 per stream
+    if (i >= 40LL * S) return;
+    const int s = (int)(i / 40), c = (int)(i - 40LL * s);
+    tail[i] = reinterpret_cast<const uint4*>(pcm + ((size_t)s * T + T - 2) * 160)[c];
+}
+
 // each net's normalised log-Mel of silence: mel 0 -> log10_vec's x == 0 -> 1
 // (fixlog10.c:56), then feature_module.c:67-73
 struct NringFill {
@@ -1755,6 +1764,12 @@ int nnspk_launch_tail_roll(int16_t* tail, const int16_t* pcm, int S, int T, cons
                            int hist_frames, void* stream) {
     const int n = list ? n_list : S;
     if (n <= 0) return 0;
+    if (!list && !seg_begin && (seg_len <= 0 || seg_len >= T) && lookback == 0 && T >= 2 && ((uintptr_t)pcm & 15) == 0 && ((uintptr_t)tail & 15) == 0) {
+        const long long nv = 40LL * S;
+        hipLaunchKernelGGL(tail_copy_kernel, dim3((unsigned)((nv + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                           reinterpret_cast<uint4*>(tail), pcm, S, T);
+        return ok(hipGetLastError());
+    }
     hipLaunchKernelGGL(tail_roll_kernel, dim3(n), dim3(64), 0, (hipStream_t)stream, tail, pcm, S, T, list, n_list,
                        seg_begin, seg_len, lookback, hist, hist_frames);
     return ok(hipGetLastError());
