@@ -32,6 +32,7 @@
 /* NNSP_CASCADE_DEBUG: after each launch, wait for the stream and report
  * which launch failed (asynchronous faults otherwise surface at a later sync) */
 static int dbg_step(const nnsp_cascade *c, void *stream, const char *what, int n, int r);
+static void zero_bind(nnsp_cascade *c, int parity);
 static int book_take(nnsp_cascade *c);
 static int ahead_read(nnsp_cascade *c, int q, int wait);
 #define DBG(st, what, n, r)                                  \
@@ -48,6 +49,7 @@ static int ahead_read(nnsp_cascade *c, int q, int wait);
 #define HIST_MAX 99   /* PcmBufClass keeps 100 frames: look-back 0..99 */
 #define MAX_TIMED 32  /* rounds per chunk with per-net device timing */
 #define ZERO_BYTES (3 * 8 + (18 + 2 + MAX_TIMED * 3) * 4)
+#define ZERO_STRIDE 512   /* the counters of chunk parity p at d_zero + p * ZERO_STRIDE */
 
 struct nnsp_cascade {
     nnsp_batch *net[3];
@@ -76,7 +78,8 @@ struct nnsp_cascade {
     int32_t *d_rcount;              /* [MAX_TIMED][3] list lengths each round ran with */
     int32_t *d_last_round;          /* last round a stream was listed for (+1) */
     int32_t *d_cuts;                /* segments cut by a net switch in the chunk */
-    void *d_zero;                   /* frames, counts, last_round, rcount (one allocation) */
+    void *d_zero;                   /* frames, counts, last_round, rcount (one allocation), per chunk parity:
+                                       chunk k counts into block k & 1 and clears block (k + 1) & 1 */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
     void *ev[2];
@@ -115,6 +118,21 @@ struct nnsp_cascade {
     int book_ahead, book_ahead_done; /* its look-ahead front end ran; its own front end ran ahead */
     unsigned long long book_frames[3];
 };
+
+/* the chunk counters of parity p (c->d_* and the kernels' CascArgs pointers) */
+static void zero_bind(nnsp_cascade *c, int parity)
+{
+    char *z = (char *)c->d_zero + (size_t)parity * ZERO_STRIDE;
+    c->d_frames = (unsigned long long *)z;              /* [3] */
+    c->d_counts = (int32_t *)(z + 3 * 8);               /* [18] */
+    c->d_last_round = c->d_counts + 18;                 /* [1] */
+    c->d_cuts = c->d_last_round + 1;                    /* [1] */
+    c->d_rcount = c->d_cuts + 1;                        /* [MAX_TIMED][3] */
+    c->a.counts = c->d_counts;
+    c->a.frames = c->d_frames;
+    c->a.last_round = c->d_last_round;
+    c->a.cuts = c->d_cuts;
+}
 
 int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int8_t *seq, int len_seq,
                         const nnsp_cascade_params *p)
@@ -193,15 +211,11 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     }
     if ((e = nnspk_malloc((void **)&c->d_st, S * sizeof(CascState)))) goto fail;
     /* the per-chunk counters, one allocation zeroed by one memset per chunk */
-    if ((e = nnspk_malloc((void **)&c->d_zero, ZERO_BYTES))) goto fail;
-    if ((e = nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream))) goto fail;
+    if ((e = nnspk_malloc((void **)&c->d_zero, 2 * ZERO_STRIDE))) goto fail;
+    if ((e = nnspk_memset(c->d_zero, 0, 2 * ZERO_STRIDE, c->stream))) goto fail;
     if ((e = nnspk_host_alloc(&c->h_book, ZERO_BYTES))) goto fail;
     if ((e = nnspk_event_create(&c->ev_book))) goto fail;
-    c->d_frames = (unsigned long long *)c->d_zero;                 /* [3] */
-    c->d_counts = (int32_t *)((char *)c->d_zero + 3 * 8);         /* [18] */
-    c->d_last_round = c->d_counts + 18;                             /* [1] */
-    c->d_cuts = c->d_last_round + 1;                                /* [1] */
-    c->d_rcount = c->d_cuts + 1;                                    /* [MAX_TIMED][3] */
+    zero_bind(c, 0);
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */
     if ((e = nnspk_malloc((void **)&c->d_pdef, 3 * 40 * 2))) goto fail;
@@ -625,6 +639,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     }
     TRY(book_take(c)); /* the last chunk's counters: rounds, switches (this chunk's window) */
     const long long k = c->chunk;
+    zero_bind(c, (int)(k & 1));
     CascArgs a = c->a;
     a.T = T;
     a.seg_len = c->window;
@@ -632,7 +647,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     a.detected = detected;
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
-    TRY(nnspk_event_record(c->ev[0], c->stream)); /* the counters (d_zero) were cleared by the last chunk */
+    TRY(nnspk_event_record(c->ev[0], c->stream)); /* this parity's counters were cleared during the last chunk */
     /* look-ahead: the next chunk's shared front end runs while this chunk's
      * rounds run (it writes ring slots and a history buffer this chunk does not
      * read; its STFT tail is this chunk's last two frames) */
@@ -664,6 +679,8 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
         TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
     TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
+    /* the next chunk's counters (copied out and taken at the end of the last call) */
+    TRY(nnspk_memset((char *)c->d_zero + (size_t)((k + 1) & 1) * ZERO_STRIDE, 0, ZERO_BYTES, c->stream));
     int ahead_launched = 0;
     /* the look-ahead front end starts once the nets' first round (the bulk of
      * the chunk's NN work) is done: running beside it from the start, or with
@@ -672,7 +689,11 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
      * and CU-masked variants: profiles/r03/cofe/README.md); started once VAD's
      * round 0 is done and S2I's and KWS's recurrences are queued: 0.975 vs
      * 0.992 G (4 paired runs) */
-    int r = 0, R = c->last_rounds > 0 ? c->last_rounds : 8;
+    /* rounds launched before the first host check: as many as the last chunk
+     * needed, at least 3 (the reference nets' usual count: a chunk that needs
+     * one more than launched pays a host round trip, ~80 us, an empty round
+     * launched in vain a few us of early-exiting workgroups) */
+    int r = 0, R = c->last_rounds > 0 ? (c->last_rounds < 3 ? 3 : c->last_rounds) : 8;
     for (;;) {
         for (; r < R; ++r) {
             TRY(launch_round(c, &a, r, pcm, T, hist));
@@ -693,7 +714,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         /* all the chunk's counters in one copy (the next round's list lengths
          * among them): if no round is left they are final, and the
          * bookkeeping needs no further host wait */
-        TRY(nnspk_d2h(c->h_book, c->d_zero, ZERO_BYTES, c->stream));
+        TRY(nnspk_d2h(c->h_book, c->d_frames, ZERO_BYTES, c->stream));
         TRY(nnspk_event_record(c->ev_book, c->stream));
         TRY(nnspk_sync(c->stream));
         const int32_t *cnt = (const int32_t *)((const char *)c->h_book + 3 * 8) + 6 * (r % 3);
@@ -708,14 +729,13 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         c->pre_T = next_T;
     }
     /* bookkeeping: h_book was copied before the last synchronisation, so it
-     * is taken now (no host wait at the next call), and the device counters
-     * are cleared for the next chunk behind the rounds */
+     * is taken now (no host wait at the next call); this parity's device
+     * counters are cleared by the chunk after next, behind its fork */
     c->book_pending = 1;
     c->book_rounds = r;
     c->book_ahead = ahead_launched;
     c->book_ahead_done = ahead_done;
     TRY(book_take(c));
-    TRY(nnspk_memset(c->d_zero, 0, ZERO_BYTES, c->stream));
     return 0;
 }
 
