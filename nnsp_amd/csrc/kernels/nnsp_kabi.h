@@ -271,6 +271,7 @@ int nnspk_host_alloc(void **p, size_t n);   /* pinned host memory (asynchronous 
 int nnspk_host_free(void *p);
 int nnspk_event_sync(void *e);
 int nnspk_event_done(void *e);              /* 1: the event has completed (no wait) */
+int nnspk_event_spin(void *e);              /* wait for the event by polling it (no sleep / wake-up latency) */
 int nnspk_d2d(void *d, const void *s, size_t n, void *stream);
 int nnspk_sync(void *stream);
 int nnspk_device_count(int *n);

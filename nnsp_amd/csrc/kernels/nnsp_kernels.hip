@@ -1873,6 +1873,13 @@ int nnspk_host_alloc(void** p, size_t n) { return ok(hipHostMalloc(p, n ? n : 16
 int nnspk_host_free(void* p) { return p ? ok(hipHostFree(p)) : 0; }
 int nnspk_event_sync(void* e) { return ok(hipEventSynchronize((hipEvent_t)e)); }
 int nnspk_event_done(void* e) { return hipEventQuery((hipEvent_t)e) == hipSuccess; }
+int nnspk_event_spin(void* e) {
+    for (;;) {
+        const hipError_t r = hipEventQuery((hipEvent_t)e);
+        if (r == hipSuccess) return 0;
+        if (r != hipErrorNotReady) return (int)r;
+    }
+}
 int nnspk_device_count(int* n) { return ok(hipGetDeviceCount(n)); }
 int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
