@@ -493,7 +493,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         const int timed = c->timing && r < MAX_TIMED;
         if (c->fused) {
             if (r == 0) {
-                TRY(nnspk_stream_wait(st, c->ev_fork)); /* casc_begin */
+                if (c->serial || n != 1) TRY(nnspk_stream_wait(st, c->ev_fork)); /* casc_begin (on VAD's stream) */
                 if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
             } else {
                 for (int m = 0; m < 3; ++m)
@@ -670,9 +670,16 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
         a.list[n] = c->d_list[0][n];
         a.cold_list[n] = c->d_cold_list[0][n];
     }
-    TRY(nnspk_launch_casc_begin(&a, c->stream));
-    DBG(c->stream, "casc_begin", -1, -1);
-    if (c->fused) TRY(nnspk_event_record(c->ev_fork, c->stream));
+    /* fused control: casc_begin on VAD's stream, which runs round 0 first --
+     * VAD's cold front end then follows it in order instead of behind a
+     * cross-queue event wait (~12 us); it waits only for a front end this
+     * call ran itself (in the steady state the previous call ran it ahead) */
+    const int begin_on_vad = c->fused && !c->serial;
+    void *bst = begin_on_vad ? c->ns[1] : c->stream;
+    if (begin_on_vad && !ahead_done) TRY(nnspk_stream_wait(bst, c->ev_fe[1]));
+    TRY(nnspk_launch_casc_begin(&a, bst));
+    DBG(bst, "casc_begin", -1, -1);
+    if (c->fused) TRY(nnspk_event_record(c->ev_fork, bst));
     /* behind the fork (off round 0's start): nothing in this chunk reads what
      * they write -- the cold frames read d_hist[k % 3], the look-ahead front
      * end takes its tail from pcm */
