@@ -327,7 +327,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     constexpr int G = GEN ? 1 : GT;
     constexpr int SPT = 16 / G;
     constexpr int FR = 2 * SPT + 4;                   // context frames of one stream's rows
-    const int ntps = G > 1 ? 1 : (wsteps + 15) / 16;
+    const int ntps = (wsteps + SPT - 1) / SPT;        // tiles per group of G streams
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
     if (r.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *r.n_list_rec = nrow;
     const int ngrp = (nrow + G - 1) / G;
@@ -362,7 +362,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     // took 16 more VGPRs per lane held across the FC layer: past 128, spills.)
     const int tstride = (int)gridDim.x * nwv;
     auto grp_of = [&](int t) { return ntps == 1 ? t : (ntps == 4 ? t >> 2 : (ntps == 2 ? t >> 1 : t / ntps)); };
-    auto j0_of = [&](int t) { return 16 * (t - grp_of(t) * ntps); };
+    auto j0_of = [&](int t) { return SPT * (t - grp_of(t) * ntps); };
     // lanes 0..G-1: the tile's stream k = lane (the others read by shuffle); -1: none
     auto list_at = [&](int t) {
         if (t >= ntiles) return -1;
