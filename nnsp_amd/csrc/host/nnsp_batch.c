@@ -248,6 +248,13 @@ int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
     if ((e = nnspk_h2d(b->d_stdR, stdR, 40 * 4, b->stream))) goto fail;
     if ((e = nnspk_memset(b->d_prev5, 0, S * 200 * 2, b->stream))) goto fail;
     if ((e = nnspk_memset(b->d_post, 0, S * sizeof(NnPost), b->stream))) goto fail;
+    {
+        FeArgs ta;
+        memset(&ta, 0, sizeof ta);
+        ta.mode = FE_MODE_BATCH;
+        ta.port = b->port;
+        if ((e = nnspk_build_fe_tables(&b->d_fetab, &ta, b->stream))) goto fail;
+    }
     if ((e = nnsp_batch_reset(b, NULL))) goto fail;
     return 0;
 fail:
@@ -262,7 +269,8 @@ void nnsp_batch_destroy(nnsp_batch *b)
     if (b->stream) nnspk_sync(b->stream);
     nnsp_image_free(&b->im);
     void *bufs[] = {b->d_mean, b->d_stdR, b->d_tail, b->d_prev5, b->d_h, b->d_c, b->d_post,
-                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx, b->d_xg, b->d_clk};
+                    b->d_feats, b->d_pcm, b->d_trig, b->d_logits, b->d_mask, b->d_gx, b->d_xg, b->d_clk,
+                    b->d_fetab};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 3; ++i) nnspk_event_destroy(b->ev[i]);
     nnspk_stream_destroy(b->stream);
@@ -303,6 +311,7 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     if (seg->list && seg->n_list <= 0) return 0;
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
+    fa.tb_img = b->d_fetab;
     fa.pcm = pcm;
     fa.tail = b->d_tail;
     fa.S = b->S;

@@ -78,6 +78,7 @@ struct nnsp_cascade {
     int32_t *d_rcount;              /* [MAX_TIMED][3] list lengths each round ran with */
     int32_t *d_last_round;          /* last round a stream was listed for (+1) */
     int32_t *d_cuts;                /* segments cut by a net switch in the chunk */
+    void *d_fetab;                  /* the shared / cold front end's tables, prebuilt */
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation), per chunk parity:
                                        chunk k counts into block k & 1 and clears block (k + 1) & 1 */
     void *stream;                   /* front end, control; the nets' work forks off it */
@@ -288,6 +289,18 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         nnspk_free(tl);
         if (e) goto fail;
     }
+    {   /* the front end's tables: the shared mode's, with each net's normalisation (the cold mode reads none of those) */
+        FeArgs ta;
+        memset(&ta, 0, sizeof ta);
+        ta.mode = FE_MODE_SHARED;
+        ta.port = nets[0]->port;
+        for (int n = 0; n < 3; ++n) {
+            ta.nring[n] = c->d_nring[n];
+            ta.nmean[n] = nets[n]->d_mean;
+            ta.nstdR[n] = nets[n]->d_stdR;
+        }
+        if ((e = nnspk_build_fe_tables(&c->d_fetab, &ta, c->stream))) goto fail;
+    }
     c->window = 16;      /* the first chunk's window; then chosen per chunk (auto_window) */
     c->auto_window = 1;
     {
@@ -325,7 +338,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
                     c->d_nring[0], c->d_stail,     c->d_fresh,   c->d_pcm,     c->d_det,     c->d_o3,
                     c->d_ran,     c->d_pdef,      c->d_cold_list[0][0],
                     c->d_cold_list[0][1], c->d_cold_list[0][2], c->d_list[1][0], c->d_list[1][1], c->d_list[1][2],
-                    c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2]};
+                    c->d_cold_list[1][0], c->d_cold_list[1][1], c->d_cold_list[1][2], c->d_fetab};
     for (size_t i = 0; i < sizeof bufs / sizeof bufs[0]; ++i) nnspk_free(bufs[i]);
     for (int i = 0; i < 2; ++i) {
         nnspk_event_destroy(c->ev[i]);
@@ -400,6 +413,7 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
     nnsp_batch *b = c->net[n];
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
+    fa.tb_img = c->d_fetab;
     fa.pcm = pcm;
     fa.S = c->S;
     fa.T = T;
@@ -529,6 +543,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
 {
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
+    fa.tb_img = c->d_fetab;
     (void)ahead;
     fa.pcm = pcm;
     fa.tail = tail;
@@ -647,7 +662,6 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     a.detected = detected;
     a.outputs3 = outputs3;
     for (int n = 0; n < 3; ++n) a.fs[n].abs0 = c->abs0;
-    TRY(nnspk_event_record(c->ev[0], c->stream)); /* this parity's counters were cleared during the last chunk */
     /* look-ahead: the next chunk's shared front end runs while this chunk's
      * rounds run (it writes ring slots and a history buffer this chunk does not
      * read; its STFT tail is this chunk's last two frames) */
@@ -655,15 +669,14 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     /* 1. log-Mel of every frame (net-independent), unless the previous call ran it ahead */
     const int ahead_done = c->pre_pcm == pcm && c->pre_T == T;
     c->pre_pcm = NULL;
-    TRY(nnspk_event_record(c->ev_fe[0], c->stream));
-    if (!ahead_done) TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0, c->stream));
-    DBG(c->stream, "shared front end", -1, -1);
-    TRY(nnspk_event_record(c->ev_fe[1], c->stream));
+    if (!ahead_done) {   /* (the chunk's start: ev[0]; ran ahead, casc_begin is launched first) */
+        TRY(nnspk_event_record(c->ev[0], c->stream));
+        TRY(nnspk_event_record(c->ev_fe[0], c->stream));
+        TRY(shared_fe(c, pcm, T, c->d_stail, 0, c->abs0, k, 0, c->stream));
+        DBG(c->stream, "shared front end", -1, -1);
+        TRY(nnspk_event_record(c->ev_fe[1], c->stream));
+    }
     c->sfe_ahead = ahead_done;
-    /* the next chunk's voice buffer (its look-back history) and STFT tail:
-     * they read this chunk's PCM, and nothing in this chunk reads what they
-     * write (cold frames read d_hist[k % 3]; the look-ahead front end takes
-     * its tail from pcm) -- queued now, off the chunk's tail */
     const int16_t *hist = c->d_hist[k % 3];
     a.counts = c->d_counts; /* round 0's lists */
     for (int n = 0; n < 3; ++n) {
@@ -679,6 +692,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     if (begin_on_vad && !ahead_done) TRY(nnspk_stream_wait(bst, c->ev_fe[1]));
     TRY(nnspk_launch_casc_begin(&a, bst));
     DBG(bst, "casc_begin", -1, -1);
+    if (ahead_done) TRY(nnspk_event_record(c->ev[0], c->stream));   /* c->stream is idle: about now */
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, bst));
     /* behind the fork (off round 0's start): nothing in this chunk reads what
      * they write -- the cold frames read d_hist[k % 3], the look-ahead front

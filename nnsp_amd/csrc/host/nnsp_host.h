@@ -73,6 +73,7 @@ struct nnsp_batch {
     int16_t *d_xg;                    /* compiled shapes: proj -> recur LSTM inputs x */
     long long rec_a_off;              /* first byte of the image recur stages into LDS */
     long long *d_clk; /* NNSP_RECUR_CLOCKS development probe */
+    void *d_fetab;    /* the front end's per-workgroup tables, prebuilt (nnspk_build_fe_tables) */
 };
 
 /* One segment launch of a batch: the streams list[0..n_list) (NULL: all),

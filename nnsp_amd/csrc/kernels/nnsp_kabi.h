@@ -83,6 +83,10 @@ typedef struct {
     int32_t norm32;           /* 1: every normalisation's (feature - mean) * stdR >> shift provably fits
                                  int32 (nnsp_norm_fits32): the 32-bit clamp path */
     int32_t pad3_;
+    /* non-NULL: the workgroup's constant tables (twiddles, split, normalisation,
+     * log, window, Mel) prebuilt for this mode / build by nnspk_build_fe_tables,
+     * copied with 16-byte loads instead of being derived per workgroup */
+    const void *tb_img;
 } FeArgs;
 
 /* feature_module.c:67-73 in 32 bits: |log10 output| < 2^18 (|table| * 0x3796 >> 15
@@ -220,6 +224,9 @@ typedef struct {
 
 /* launch layer (nnsp_kernels.hip) */
 int nnspk_launch_fe(const FeArgs *a, void *stream);
+/* the front end's per-workgroup tables for the mode, build and (shared mode)
+ * normalisation of *a, built once into a new device buffer *out (nnspk_free) */
+int nnspk_build_fe_tables(void **out, const FeArgs *a, void *stream);
 /* cascade reset: ring slots of the masked streams := each net's normalised
  * log-Mel of silence */
 int nnspk_launch_nring_fill(int16_t *const nring[3], const int32_t *const nmean[3], const int32_t *const nstdR[3],

@@ -63,6 +63,7 @@ struct FeTables {
                           // sign-extending ds_read_i16 (no VALU unpacking; LDS, not VGPRs:
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
 };   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
+static_assert(sizeof(FeTables) % 16 == 0, "FeTables: copied as 16-byte chunks");
 
 // the per-net normalisation constants (norm[]; with the Mel pad at 264 the
 // tables and buffers stay within 160 KB / 6)
@@ -78,6 +79,25 @@ __device__ __forceinline__ int32_t fe_norm_word(const FeArgs& a, int k) {
 __device__ __forceinline__ uint4* fe_twp(FeTables& T) { return reinterpret_cast<uint4*>(&T.tw[0][0][0]); }
 __device__ __forceinline__ const uint4* fe_twp(const FeTables& T) {
     return reinterpret_cast<const uint4*>(&T.tw[0][0][0]);
+}
+
+template <bool PORT>
+__device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a);
+
+// the workgroup's tables: a prebuilt image (FeArgs.tb_img: every load
+// independent, one memory latency -- deriving them took ~21 us per workgroup,
+// chains of dependent table loads, ~5 % of a front-end workgroup's life) or
+// derived in place
+template <bool PORT>
+__device__ __forceinline__ void fe_tables_load(FeTables& T, const FeArgs& a) {
+    if (a.tb_img) {
+        const uint4* src = reinterpret_cast<const uint4*>(a.tb_img);
+        uint4* dst = reinterpret_cast<uint4*>(&T);
+        constexpr int N = (int)(sizeof(FeTables) / 16);
+        for (int i = threadIdx.x; i < N; i += blockDim.x) dst[i] = src[i];
+    } else {
+        fe_tables_init<PORT>(T, a);
+    }
 }
 
 template <bool PORT>
@@ -336,7 +356,7 @@ __global__ __launch_bounds__(256, 6) void fe_kernel(FeArgs a) {
     const unsigned wid0 = blockIdx.x * 4u + (threadIdx.x >> 6);
     long long* wclk = (a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    fe_tables_init<PORT>(TB, a);
+    fe_tables_load<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = XPs[wv];
@@ -686,7 +706,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
     const unsigned nw = gridDim.x * 4u;
     const unsigned per = ((nfr + nw - 1) / nw + 1) & ~1u;   // even: whole pairs per wave
     if (blockIdx.x * 4u * per >= nfr) return;
-    fe_tables_init<PORT>(TB, a);
+    fe_tables_load<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* XA = XPs[wv][0];
@@ -1655,12 +1675,36 @@ __global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed,
     }
 }
 
+// the front end's per-workgroup tables into a global image (nnspk_build_fe_tables)
+template <bool PORT>
+__global__ __launch_bounds__(256) void fe_tables_build_kernel(FeTables* out, FeArgs a) {
+    fe_tables_init<PORT>(*out, a);
+}
+
 // ============================================================================
 // C-ABI launch layer (plain pointers; stream passed as void*)
 // ============================================================================
 static int ok(hipError_t e) { return e == hipSuccess ? 0 : (int)e; }
 
 extern "C" {
+
+int nnspk_build_fe_tables(void** out, const FeArgs* a, void* stream) {
+    *out = nullptr;
+    FeTables* t = nullptr;
+    hipError_t e = hipMalloc((void**)&t, sizeof(FeTables));
+    if (e != hipSuccess) return (int)e;
+    if (a->port)
+        hipLaunchKernelGGL(fe_tables_build_kernel<true>, dim3(1), dim3(256), 0, (hipStream_t)stream, t, *a);
+    else
+        hipLaunchKernelGGL(fe_tables_build_kernel<false>, dim3(1), dim3(256), 0, (hipStream_t)stream, t, *a);
+    e = hipGetLastError();
+    if (e != hipSuccess) {
+        (void)hipFree(t);
+        return (int)e;
+    }
+    *out = t;
+    return 0;
+}
 
 int nnspk_launch_fe(const FeArgs* a, void* stream) {
     const int nrow = a->n_list_dev ? a->S : (a->list ? a->n_list : a->S);

@@ -26,9 +26,9 @@ L.nnsp_synth_pcm(C.c_void_p(pcm.data_ptr()), S, T, C.c_uint64(1), 0, C.c_int64(0
 for _ in range(3):
     eng.exec_device(pcm.data_ptr(), T, trig.data_ptr())
 fe, nn = eng.last_timing()
-clk = np.zeros((64, 16), np.int64)
+clk = np.zeros(64 * 32, np.int64)   # nnsp_batch_debug_clocks copies 64 x 32 longs
 _lib.check(L.nnsp_batch_debug_clocks(eng.h, C.c_void_p(clk.ctypes.data)), "clocks")
-p = clk[:, 12:16]
+p = clk.reshape(-1, 16)[:64, 12:16]   # tile `it` of wave 0: longs 12 + 16 it + phase
 n = int((p[:, 3] > 0).sum())
 p = p[:n]
 d = np.diff(p, axis=1)
