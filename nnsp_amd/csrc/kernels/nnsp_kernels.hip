@@ -1720,7 +1720,11 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // (also measured in round 3, paired A/B: 1536 blocks -- one generation --
     // 882 M, 3072 951 M, 6144 965 M, 12288 965 M, 24576 954 M cascade frames/s:
     // the later generations' workgroup turnover lets the nets' rounds in)
-    const long long cap = 256LL * 6 * 4;
+    // (round 3, with the prebuilt tables -- staging 22 -> 10.6 us per
+    // workgroup -- eight generations, 67 frames per wave: cascade 3 072
+    // workgroups 0.948 G, 4 608 0.980, 6 144 0.986-0.998, 9 216 0.992,
+    // 12 288 1.016, 18 432 1.008, 24 576 0.992 G; shared FE 2.16 -> 2.09 ms)
+    const long long cap = 256LL * 6 * 8;
     if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
@@ -1737,6 +1741,8 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (use_pair && !a->seg_begin && !a->dbg_spec && !a->dbg_log && !a->dbg_clk) {
         // whole multiples of the resident workgroups at four per CU
         long long b2 = (nfr + 7) / 8;
+        // (round 3, prebuilt tables: 4 096 workgroups 1.196 G VAD frames/s,
+        // 6 144 1.169, 8 192 1.192, 12 288 1.156 -- four generations stay)
         if (b2 > 256LL * 4 * 4) b2 = 256LL * 4 * 4;
         const dim3 g2((unsigned)b2);
         if (a->mode == FE_MODE_SHARED) {
