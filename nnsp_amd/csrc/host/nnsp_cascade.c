@@ -494,7 +494,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
      * of a round before any net's NN kernels, VAD's recurrence after S2I's
      * and KWS's, every recur behind all three projs -- each -2..-7 %) */
     /* round 0 with fused control: VAD (net 1) is launched first and S2I's
-     * and KWS's cold front ends wait for VAD's proj -- every stream starts
+     * and KWS's proj + recur wait for VAD's proj -- every stream starts
      * with VAD's round, so VAD's cold frames and prefix layers are the
      * longest chain of the round and get the whole device (paired A/B over
      * 6 runs, profiles/r03: +1 % cascade frames/s over the plain order) */
@@ -508,7 +508,6 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         if (c->fused) {
             if (r == 0) {
                 if (c->serial || n != 1) TRY(nnspk_stream_wait(st, c->ev_fork)); /* casc_begin (on VAD's stream) */
-                if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
             } else {
                 for (int m = 0; m < 3; ++m)
                     if (m != n) TRY(nnspk_stream_wait(st, c->ev_rnd[(r - 1) & 1][m]));
@@ -520,6 +519,10 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
         TRY(segment_features(c, n, r, pcm, T, cur, hist, st));
         DBG(st, "cold front end", n, r);
         if (timed) TRY(nnspk_event_record(c->ev_t[r][n][1], st));
+        /* S2I's and KWS's round-0 NN waits for VAD's proj; their cold front
+         * ends do not (they ran behind VAD's recurrence for CUs, ~85 us, on
+         * the round's critical path; A/B 1.010 vs 0.995 G) */
+        if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
         TRY(round_nn(c, a, r, n, T, cur, hist, st, vad_first && n == 1 ? c->ev_vad_proj : NULL));
     }
     if (c->fused) return 0;
