@@ -133,7 +133,9 @@ static void plan_fast(nnsp_batch *b)
     b->shape = shape;
     b->nstep_max = (b->Tmax + 1) / 2;
     /* proj: a persistent grid of as many 4-wave workgroups as fit on the
-     * device at once (LDS-bound, at most 8 per CU) */
+     * device at once (LDS-bound, at most 8 per CU); (round 3: 2x / 4x that
+     * grid, for finer balance as in the front end: cascade 1.008 / 0.998 vs
+     * 1.010 G, VAD 1.219 / 1.184 vs 1.194 G -- no gain) */
     int cus = 256, clk = 0;
     char arch[64];
     if (nnspk_device_info(&cus, &clk, arch, (int)sizeof arch) || cus <= 0) cus = 256;
