@@ -386,21 +386,37 @@ def main() -> None:
     ap.add_argument("--no-stress", action="store_true",
                     help="skip the second cascade line on synthetic weights (N=1 only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    # the path has no exchange step (streams are independent shards), so the
+    # ranks' process group only brackets and reduces the timing: gloo, on the
+    # host.  An RCCL group (nccl) measured 0.92 against 1.02 G frames/s at
+    # world size 1: its streams share HIP's four hardware queues with the
+    # cascade's four (GPU_MAX_HW_QUEUES=8: 0.97 G); profiles/r03/torchrun.sh
+    ap.add_argument("--dist-backend", default="gloo", choices=["gloo", "nccl"],
+                    help="process group of the ranks (barriers and the timing / frame-count reductions only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
     args = ap.parse_args()
 
     rank, world, local, launched = dist_env()
+    # stdout carries the one JSON line and nothing else: libraries that print
+    # banners there (RCCL prints its version at process-group init) write to
+    # stderr instead, the line goes to the saved descriptor
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     # the CPU baseline runs on rank 0 at N=1 only; its pool exists before the GPU does
     pool, cpu = cpu_pool() if rank == 0 and world == 1 and not args.no_cpu_baseline else (None, None)
     import torch
 
     dist = None
     torch.cuda.set_device(local if launched else 0)
-    if launched:   # torch.distributed.run: RCCL process group, world size 1 included
+    if launched:   # torch.distributed.run: a process group (--dist-backend), world size 1 included
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     from nnsp_amd import _lib
     from nnsp_amd.engine import device_info
 
@@ -411,7 +427,8 @@ def main() -> None:
     else:
         s0, S = shard_streams(rank, world, total=args.total_streams)
     res = run_workload(args, S, s0, args.weights, dist)
-    elapsed, frames = reduce_run(dist, res["elapsed"], res["frames"], device="cuda")
+    elapsed, frames = reduce_run(dist, res["elapsed"], res["frames"],
+                                 device="cuda" if args.dist_backend == "nccl" else "cpu")
     stress = None
     if args.net == "cascade" and world == 1 and not args.no_stress and args.weights == "ref":
         r2 = run_workload(args, S, s0, "synth")
@@ -450,7 +467,8 @@ def main() -> None:
                        "frames_per_step": args.frames, "accumulator": "32b" if args.acc32 else "64b",
                        "weights": args.weights, "input": args.input,
                        "build": "ARM_OPTIMIZED=1 (shipped)" if args.build == "shipped" else "ARM_OPTIMIZED=0 (portable)",
-                       "parallelism": f"stream shards x{world}" + (" (RCCL process group)" if dist else "")},
+                       "parallelism": f"stream shards x{world}" +
+                                      (f" ({'RCCL' if args.dist_backend == 'nccl' else 'gloo'} process group)" if dist else "")},
             "roofline": dom,
             **{f"roofline_{k}": v for k, v in extra.items()},
             "fe_ms_per_step": res["fe_ms"],
@@ -471,7 +489,8 @@ def main() -> None:
                 out["cpu_baseline"] = cpu_baseline(pool, cpu, args.net, args.acc32, args.weights,
                                                    args.input == "mix", args.cpu_seconds,
                                                    portable=args.build == "portable")
-        print(json.dumps(out))
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist:
         dist.destroy_process_group()
 
