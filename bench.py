@@ -24,12 +24,15 @@ A "step" is one chunk of --frames frames (default 100 = 1 s of audio) for
 every stream of the GPU's shard; streams carry their state across steps
 (continuous audio).
 
-Multi-GPU: one process per GPU (torch.distributed over RCCL, initialised
-whenever torch.distributed.run launched the process, world size 1 included);
-rank r owns a contiguous stream shard (nnsp_amd.shard.shard_streams; weak
-scaling: --streams per GPU, strong: --total-streams split), no data-path
-collective; value = frames of all ranks / max over ranks of the timed wall
-time.
+Multi-GPU: one process per GPU, launched by torch.distributed.run; a process
+group is initialised whenever torch.distributed.run launched the process
+(world size 1 included) -- gloo by default (--dist-backend), because it only
+holds the barriers around the timed region and the timing / frame-count
+reductions (an RCCL group shares HIP's hardware queues with the cascade's
+streams: ~10 % slower).  Rank r owns a contiguous stream shard
+(nnsp_amd.shard.shard_streams; weak scaling: --streams per GPU, strong:
+--total-streams split), no data-path collective; value = frames of all ranks /
+max over ranks of the timed wall time.
 """
 from __future__ import annotations
 
@@ -210,7 +213,6 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     eng = make_engine(args.net, S, T, args.acc32, weights, args.window, args.build == "shipped")
     dwav = None
     if args.input == "mix":
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
         z = np.load(os.path.join(ROOT, "tests", "golden", "test_wavs.npz"))
         wav = np.stack([z[k] for k in ("speech", "galaxy", "galaxy_s2i")])
         dwav = torch.from_numpy(wav).to("cuda")

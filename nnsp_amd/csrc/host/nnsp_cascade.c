@@ -50,6 +50,7 @@ static int ahead_read(nnsp_cascade *c, int q, int wait);
 #define MAX_TIMED 32  /* rounds per chunk with per-net device timing */
 #define ZERO_BYTES (3 * 8 + (18 + 2 + MAX_TIMED * 3) * 4)
 #define ZERO_STRIDE 512   /* the counters of chunk parity p at d_zero + p * ZERO_STRIDE */
+_Static_assert(ZERO_BYTES <= ZERO_STRIDE, "the two chunk-parity counter blocks overlap: raise ZERO_STRIDE");
 
 struct nnsp_cascade {
     nnsp_batch *net[3];
@@ -117,6 +118,8 @@ struct nnsp_cascade {
     int book_pending;               /* a copy is in flight */
     int book_rounds;                /* rounds launched in that chunk */
     int book_ahead, book_ahead_done; /* its look-ahead front end ran; its own front end ran ahead */
+    int chunk_open;                 /* a call launched rounds and did not finish: its parity block holds
+                                       partial counts (cleared by the next call before use) */
     unsigned long long book_frames[3];
 };
 
@@ -189,6 +192,15 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
      * net's reset, the one before it (FE_MODE_COLD re-reads it) */
     c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
     c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
+    /* ring rows s * ring + slot are 32-bit in the kernels (fe_kernel's shared
+     * store, the proj union loads); element offsets beyond are 64-bit */
+    if ((long long)c->S * c->ring >= (1LL << 31)) {
+        nnsp_set_error("nnsp_cascade_create: streams * (look-back + 2 * max_frames) = %lld ring rows, must stay "
+                       "below 2^31", (long long)c->S * c->ring);
+        free(c);
+        *out = NULL;
+        return NNSP_EINVAL;
+    }
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
     for (int i = 0; i < 2; ++i)
@@ -376,6 +388,9 @@ int nnsp_cascade_reset(nnsp_cascade *c, const uint8_t *mask)
         dm = c->d_mask[0];
     }
     c->pre_pcm = NULL; /* a look-ahead front end ran on the old tail: recompute */
+    /* both chunk-parity counter blocks: a failed call may have left partial counts */
+    TRY(nnspk_memset(c->d_zero, 0, 2 * ZERO_STRIDE, c->stream));
+    c->chunk_open = 0;
     TRY(nnspk_launch_casc_reset(c->d_st, c->d_hist[c->chunk % 3], c->H, c->d_stail, c->d_fresh, dm, c->S,
                                 c->stream));
     /* PcmBufClass_reset: every look-back frame is silence */
@@ -658,6 +673,9 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     TRY(book_take(c)); /* the last chunk's counters: rounds, switches (this chunk's window) */
     const long long k = c->chunk;
     zero_bind(c, (int)(k & 1));
+    if (c->chunk_open) /* the last call failed after launching rounds into this block */
+        TRY(nnspk_memset((char *)c->d_zero + (size_t)(k & 1) * ZERO_STRIDE, 0, ZERO_BYTES, c->stream));
+    c->chunk_open = 1;
     CascArgs a = c->a;
     a.T = T;
     a.seg_len = c->window;
@@ -745,13 +763,20 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
          * chunk's first (everything on c->stream is before ev_book); the
          * host first sleeps through the look-ahead front end, so it polls
          * only through the rounds' tail (A/B: 1.004 vs 0.997 G) */
-        if (ahead_launched) TRY(nnspk_event_sync(c->ev_ahead[(k + 1) & 1][1]));
-        TRY(nnspk_event_spin(c->ev_book));
+        /* without a look-ahead front end to sleep through, the whole chunk is
+         * still ahead: a blocking wait, not a core spinning for milliseconds */
+        if (ahead_launched) {
+            TRY(nnspk_event_sync(c->ev_ahead[(k + 1) & 1][1]));
+            TRY(nnspk_event_spin(c->ev_book));
+        } else {
+            TRY(nnspk_event_sync(c->ev_book));
+        }
         const int32_t *cnt = (const int32_t *)((const char *)c->h_book + 3 * 8) + 6 * (r % 3);
         if (cnt[0] + cnt[1] + cnt[2] == 0) break;
         R = r + 2;
     }
     c->launched = r;
+    c->chunk_open = 0;
     c->abs0 = (c->abs0 + T) % c->ring;
     c->chunk = k + 1;
     if (ahead_launched) {

@@ -628,9 +628,23 @@ static void complex32_copy_impl(COMPLEX32 *dst, COMPLEX32 *src)
 {
     cplx(NNSP_CPLX_COPY, &dst->real, 2, src, 2, NULL, 0, 0, 1, 0);
 }
+static int overlaps(const void *a, size_t an, const void *b, size_t bn)
+{
+    const char *pa = (const char *)a, *pb = (const char *)b;
+    return pa < pb + bn && pb < pa + an;
+}
+static void complex32_interprod_impl(COMPLEX32 *out, COMPLEX32 *arry1, COMPLEX32 *arry2, int shift_r, int len);
 static void complex32_affine_impl(COMPLEX32 *out, COMPLEX32 *Mat, COMPLEX32 *input, int shift_r, int len)
 {
     if (len <= 0) return;
+    /* complex.c:14-31 writes out + i row by row: when out aliases input or
+     * Mat, later rows read the rows already written -- run them in that order
+     * (one interprod launch per row, each on the host's updated values) */
+    const size_t vb = nz(len) * sizeof(COMPLEX32);
+    if (overlaps(out, vb, input, vb) || overlaps(out, vb, Mat, vb * nz(len))) {
+        for (int i = 0; i < len; ++i) complex32_interprod_impl(out + i, input, Mat + (size_t)i * nz(len), shift_r, len);
+        return;
+    }
     cplx(NNSP_CPLX_AFFINE, &out->real, 2 * nz(len), Mat, 2 * nz(len) * nz(len), &input->real, 2 * nz(len), shift_r,
          len, 0);
 }

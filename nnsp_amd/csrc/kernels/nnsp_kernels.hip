@@ -445,7 +445,9 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
     };
     if (fbeg >= fend) return;
     const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
-    const unsigned nstride = shared ? (unsigned)a.S * (unsigned)a.ring * 40u : 0u;   // elements between rings
+    // elements between rings: 3 S ring 40 int16 pass 2^32 at cascade sizes the
+    // survey asks for (65 536 streams x T = 1000, 262 144 x T = 200): 64-bit
+    const size_t nstride = shared ? (size_t)(unsigned)a.S * (unsigned)a.ring * 40u : 0u;
     Pos nx;
     nx.i = fbeg / W;
     nx.k = fbeg - nx.i * W;
@@ -470,11 +472,12 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
             if constexpr (shared) {
                 // the host allocates the three rings contiguously (nring[n] =
                 // nring[0] + n * nstride): one base pointer live in the loop
-                const unsigned o = po * 40u + (unsigned)lane;   // < 2^31 (host)
-                int16_t* r0 = a.nring[0] + o;
+                // po = s * ring + slot < 2^31 (nnsp_cascade_create); po * 40
+                // does not fit 32 bits past 2^26 ring rows: 64-bit offsets
+                int16_t* r0 = a.nring[0] + ((size_t)po * 40u + (unsigned)lane);
                 r0[0] = (int16_t)(pv01 & 0xffff);
                 r0[nstride] = (int16_t)(pv01 >> 16);
-                r0[2 * (size_t)nstride] = (int16_t)pv2;
+                r0[2 * nstride] = (int16_t)pv2;
             } else {
                 a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
@@ -792,7 +795,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
         }
     };
     const unsigned ring0 = shared ? (unsigned)a.abs0 % (unsigned)a.ring : 0u;
-    const unsigned nstride = shared ? (unsigned)a.S * (unsigned)a.ring * 40u : 0u;
+    const size_t nstride = shared ? (size_t)(unsigned)a.S * (unsigned)a.ring * 40u : 0u;   // as fe_kernel
     // pending outputs of the previous pair (stored after the next pair's window multiply)
     bool pendA = false, pendB = false;
     unsigned poA = 0, poB = 0;
@@ -801,10 +804,10 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
     auto flush1 = [&](bool pend, unsigned po, uint32_t pv01, int32_t pv2) {
         if (pend && lane < 40) {
             if constexpr (shared) {
-                int16_t* r0 = a.nring[0] + (po * 40u + (unsigned)lane);
+                int16_t* r0 = a.nring[0] + ((size_t)po * 40u + (unsigned)lane);
                 r0[0] = (int16_t)(pv01 & 0xffff);
                 r0[nstride] = (int16_t)(pv01 >> 16);
-                r0[2 * (size_t)nstride] = (int16_t)pv2;
+                r0[2 * nstride] = (int16_t)pv2;
             } else {
                 a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
@@ -1090,6 +1093,10 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
             int16_t* out = &sm.act[(i + 1) & 1][0][0];
             if (Ly.type == NN_LSTM) {
                 const int N = Ly.N;
+                // the previous step's h stores (other lanes of this wave, below)
+                // must be visible to these loads: an explicit workgroup-scope
+                // fence rather than reliance on in-order vector memory
+                __threadfence_block();
                 for (int idx = lane; idx < 16 * N; idx += 64) {   // stage h (the previous step's)
                     const int st = idx / N, u = idx - st * N, gs = s0 + st;
                     sm.h[st][u] = gs < r.S ? r.h[((size_t)gs * img.n_lstm + lst) * hs + u] : (int16_t)0;

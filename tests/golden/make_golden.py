@@ -496,7 +496,7 @@ def fft_complex() -> None:
     w16 = rng.integers(-2**15, 2**15, (12, L, 2)).astype(np.int16)
     sh = np.array([0, 1, 15, 31, 0, 3, 15, 20, 0, 7, 30, 2], np.int32)
     out["cx_a"], out["cx_b"], out["cx_m"], out["cx_w16"], out["cx_shift"] = a, b, m, w16, sh
-    res = {k: [] for k in ("copy", "affine", "interprod", "elmtprod", "add", "arry_add", "neg", "sub", "sub_b",
+    res = {k: [] for k in ("copy", "affine", "affine_alias", "interprod", "elmtprod", "add", "arry_add", "neg", "sub", "sub_b",
                            "mul", "init", "real2cmplx", "arry_real2cmplx", "arry_init")}
     for c in range(12):
         A, B, M, W = (np.ascontiguousarray(v[c]) for v in (a, b, m, w16))
@@ -504,6 +504,8 @@ def fft_complex() -> None:
         R.complex32_copy(P(o), P(A)); res["copy"].append(o[0].copy())
         o = np.zeros((L, 2), np.int32)
         R.complex32_affine(P(o), P(M), P(A), int(sh[c]), L); res["affine"].append(o.copy())
+        o = A.copy()   # out aliasing input: later rows read the rows already written (complex.c:14-31)
+        R.complex32_affine(P(o), P(M), P(o), int(sh[c]), L); res["affine_alias"].append(o.copy())
         o = np.zeros((L, 2), np.int32)
         R.complex32_interprod(P(o), P(A), P(B), int(sh[c]), L); res["interprod"].append(o[0].copy())
         o = np.zeros((L, 2), np.int32)

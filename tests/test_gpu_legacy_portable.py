@@ -317,6 +317,8 @@ def test_complex_helpers_vs_reference(gfc):
         r = o(); L.complex32_copy(O.p(r), O.p(A)); np.testing.assert_array_equal(r[0], gfc["cx_copy"][c])
         r = o(); L.complex32_affine(O.p(r), O.p(M), O.p(A), int(sh[c]), n)
         np.testing.assert_array_equal(r, gfc["cx_affine"][c])
+        r = A.copy(); L.complex32_affine(O.p(r), O.p(M), O.p(r), int(sh[c]), n)   # out aliases input
+        np.testing.assert_array_equal(r, gfc["cx_affine_alias"][c])
         r = o(); L.complex32_interprod(O.p(r), O.p(A), O.p(B), int(sh[c]), n)
         np.testing.assert_array_equal(r[0], gfc["cx_interprod"][c])
         r = o(); L.complex32_complex16_elmtprod(O.p(r), O.p(A), O.p(W), n)
