@@ -184,6 +184,76 @@ def _cpu_worker(net: str, acc32: bool, weights: str, mix: bool, seconds: float, 
     return frames, time.perf_counter() - t0
 
 
+def dropin_cpu_baseline(net: str, pcm, lib: str | None) -> dict:
+    """cpu_baseline leg of --dropin-latency: one stream of the same frames
+    through the oracle on one core (its NNSPClass_exec path, frame after frame
+    inside one C call: no per-frame Python in the timed loop)."""
+    if lib:
+        os.environ["NNSP_ORACLE_LIB"] = lib
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    from oracle import OracleNet
+
+    from nnsp_amd.nets import get_net
+
+    orc = OracleNet(get_net(net, "ref"))
+    st = orc.new_states(1)
+    orc.run(pcm[None, :50], st, want_logits=False, want_feats=False)   # warm
+    reps, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < 2.0:
+        orc.run(pcm[None], st, want_logits=False, want_feats=False)
+        reps += 1
+    us = (time.perf_counter() - t0) / (reps * len(pcm)) * 1e6
+    return {"us_per_frame": us, "cores": 1, "kind": "port",
+            "sample": f"1 stream x {len(pcm)} frames of the speech wav, {reps} passes, one C call per pass"}
+
+
+def dropin_latency(args) -> dict:
+    """The drop-in API's single-stream cost: the
+    reference's NNSPClass_exec (nn_speech.c:74-127) called frame by frame on
+    one stream, as an unchanged single-stream application calls it
+    (nnCntrlClass.c:183).  Each call is one GPU batch of one stream: the frame
+    goes up, the front end, the NN and the post-processing run, the result
+    comes back.  Wall time per call, after warm-up."""
+    import ctypes as C
+
+    import numpy as np
+
+    from nnsp_amd import _lib
+    from nnsp_amd.nets import NN_ID, THRESH_CNTS, THRESH_PROB, get_net
+
+    L = _lib.lib()
+    z = np.load(os.path.join(ROOT, "tests", "golden", "test_wavs.npz"))
+    T = 1000
+    pcm = np.ascontiguousarray(z["speech"][:T * 160].reshape(T, 160), np.int16)
+    out = {}
+    lib, build = native_oracle() if not args.no_cpu_baseline else (None, None)
+    for net in ("vad", "kws", "s2i"):
+        h = _lib.NetHandle(get_net(net, "ref"))
+        thr, cnt = np.array([THRESH_PROB], np.int16), np.array([THRESH_CNTS], np.int16)
+        feat, inst = _lib.FeatureClass(), _lib.NNSPClass()
+        _lib.check(L.NNSPClass_init(C.byref(inst), C.c_void_p(h.addr), C.byref(feat), bytes([NN_ID[net]]),
+                                    _lib.ptr(h.mean), _lib.ptr(h.stdR), _lib.ptr(thr), _lib.ptr(cnt)), "init")
+        L.NNSPClass_reset(C.byref(inst))
+        frames = [np.ascontiguousarray(pcm[t]) for t in range(T)]
+        for t in range(50):   # warm-up: weight image upload, kernel first launches
+            L.NNSPClass_exec(C.byref(inst), _lib.ptr(frames[t]))
+        dt = np.zeros(T)
+        for t in range(T):
+            t0 = time.perf_counter()
+            L.NNSPClass_exec(C.byref(inst), _lib.ptr(frames[t]))
+            dt[t] = time.perf_counter() - t0
+        assert L.nnsp_legacy_status() == 0
+        us = dt * 1e6
+        e = {"gpu_us_per_frame_median": float(np.median(us)), "gpu_us_per_frame_p99": float(np.percentile(us, 99)),
+             "gpu_us_per_frame_mean": float(us.mean()), "frames": T}
+        if not args.no_cpu_baseline:
+            e["cpu_baseline"] = dropin_cpu_baseline(net, pcm, lib)
+            e["cpu_baseline"]["build"] = build
+            e["gpu_over_cpu_time"] = e["gpu_us_per_frame_median"] / e["cpu_baseline"]["us_per_frame"]
+        out[net] = e
+    return out
+
+
 # ---------------------------------------------------------------------------
 # GPU run
 # ---------------------------------------------------------------------------
@@ -300,6 +370,12 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
         mul_src = "measured v_mul_hi_i32 issue rate, profiles/microbench/valu_rates_mi355x.json"
     except Exception:
         pass
+    issue_peak, issue_src = valu_peak / 64 / 2 * 1e12, "one wave64 VALU instruction per 2 SIMD cycles (no probe file)"
+    try:   # measured v_add_u32 issue rate: the chip's VALU wave-instruction issue ceiling, scaled to this device
+        issue_peak = vr["rates"]["v_add_u32"] / 64 * (cu * clk) / (vr["compute_units"] * vr["clock_khz"] * 1e3)
+        issue_src = "measured v_add_u32 rate / 64 lanes (profiles/microbench/valu_rates_mi355x.json)"
+    except Exception:
+        pass
     mfma_peak = 5000.0                         # dense int8 MFMA Tops/s (MI355X_MICROARCH.md: 2x BF16 2.5 PF)
     cascade = args.net == "cascade"
     S, T = res["S"], args.frames
@@ -308,7 +384,8 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
     fe_ms = res["fe_ms"]
     fe_frames = S * T
     fe_ach = fe_frames * FE_MULS_PER_FRAME / (fe_ms / 1e3) / 1e12
-    fe_traffic = kern.get("fe_kernel[shared]" if cascade else "fe_kernel[batch]", {}).get("hbm_bytes_per_launch")
+    fe_prof = kern.get("fe_kernel[shared]" if cascade else "fe_kernel[batch]", {})
+    fe_traffic = fe_prof.get("hbm_bytes_per_launch")
     fe_alg = fe_frames * fe_bytes_per_frame(cascade, T)
     fe = {"kernel": "fe_kernel", "bound": "valu", "achieved": fe_ach, "peak": mul_peak, "unit": "Tops/s",
           "frac": fe_ach / mul_peak, "traffic": fe_traffic,
@@ -317,7 +394,12 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
           "work": "5912 integer multiplies per frame (SURVEY 8(d)) x frames per launch",
           "peak_source": mul_src, "valu_lane_peak": valu_peak, "avg_launch_ms": fe_ms,
           "frames_per_launch": fe_frames, "launches_per_step": 1,
-          "hbm_achieved_GBps": fe_alg / (fe_ms / 1e3) / 1e9, "hbm_peak_GBps": 8000.0}
+          "hbm_achieved_GBps": fe_alg / (fe_ms / 1e3) / 1e9, "hbm_peak_GBps": 8000.0,
+          # the resource that binds: VALU issue (PMC of the profiled run, profiles/pmc_latest.json)
+          "valu_busy": fe_prof.get("valu_busy"),
+          "valu_busy_how": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the kernel's PMC pass",
+          "valu_insts_per_frame": (fe_prof["SQ_INSTS_VALU"] / fe_frames) if fe_prof.get("SQ_INSTS_VALU") else None,
+          "clock_ghz_pmc": fe_prof.get("clock_ghz")}
     # NN: MACs x 2 ops x inferences / the NN kernels' device time
     if cascade:
         ins = res["instrumented"]
@@ -335,16 +417,31 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
         cold_ms = 0.0
     nn_ach = ops / (nn_ms / 1e3) / 1e12 if nn_ms > 0 else 0.0
     nn_traffic = None
+    nn_valu = None
     if kern:
         nn_traffic = sum(v.get("hbm_bytes_per_step", 0) for k, v in kern.items()
                          if k.startswith(("proj_kernel", "recur")))
+        nn_valu = sum(v.get("valu_insts_per_step", 0) for k, v in kern.items()
+                      if k.startswith(("proj_kernel", "recur"))) or None
+    # the NN against VALU issue: its wave-instructions per step (PMC) over its
+    # device time, against the chip's VALU issue ceiling (the MFMA line above
+    # says how little of the matrix cores it uses; this one, how much of the
+    # resource it is actually bound by)
+    nn_issue = nn_valu / (nn_ms / 1e3) if (nn_valu and nn_ms > 0) else None
     nn = {"kernels": "proj_kernel + recur_pipe_kernel (all nets)", "bound": "mfma", "achieved": nn_ach,
           "peak": mfma_peak, "unit": "Tops/s", "frac": nn_ach / mfma_peak, "ms_per_step": nn_ms,
           "cold_fe_ms_per_step": cold_ms, "inferences_per_step": inf, "how": how,
           "work": "int8xint16 MACs per inference (VAD 14616, KWS 56448, S2I 72072) x 2 ops",
           "algorithmic_bytes_per_step": inf * NN_HBM_BYTES_PER_INFERENCE,
           "traffic_bytes_per_step": nn_traffic or None,
-          "traffic_over_algorithmic": (nn_traffic / (inf * NN_HBM_BYTES_PER_INFERENCE)) if nn_traffic else None}
+          "traffic_over_algorithmic": (nn_traffic / (inf * NN_HBM_BYTES_PER_INFERENCE)) if nn_traffic else None,
+          "issue": {"bound": "valu", "achieved": nn_issue / 1e9 if nn_issue else None, "peak": issue_peak / 1e9,
+                    "unit": "G VALU wave-instructions/s", "frac": nn_issue / issue_peak if nn_issue else None,
+                    "valu_insts_per_step": nn_valu,
+                    "valu_insts_per_inference": nn_valu / inf if nn_valu else None,
+                    "peak_source": issue_src,
+                    "how": "SQ_INSTS_VALU of proj + recur per step (PMC, profiles/pmc_latest.json) / the NN's device "
+                           "time per step (ms_per_step above)"}}
     # the dominant kernel: the one with the larger device time per step
     if nn_ms > fe_ms:
         dom = {"kernel": nn["kernels"], "bound": "mfma", "achieved": nn_ach, "peak": mfma_peak, "unit": "Tops/s",
@@ -397,7 +494,18 @@ def main() -> None:
                     help="process group of the ranks (barriers and the timing / frame-count reductions only)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--profile-json", default=os.path.join(ROOT, "profiles", "pmc_latest.json"))
+    ap.add_argument("--dropin-latency", action="store_true",
+                    help="time the drop-in NNSPClass_exec per frame on one stream (GPU) against the oracle on one "
+                         "core; prints its own JSON line instead of the throughput line")
     args = ap.parse_args()
+    if args.dropin_latency:
+        import torch
+
+        torch.cuda.set_device(0)
+        res = dropin_latency(args)
+        print(json.dumps({"metric": "drop-in NNSPClass_exec latency per 10 ms frame, one stream",
+                          "unit": "us/frame", "higher_is_better": False, "nets": res}))
+        return
 
     rank, world, local, launched = dist_env()
     # stdout carries the one JSON line and nothing else: libraries that print

@@ -245,6 +245,33 @@ __device__ __forceinline__ int16_t tanh_q15(int32_t x, const int16_t* tbl) {   /
 __device__ __forceinline__ int16_t sigmoid_q15(int32_t x, const int16_t* tbl) {   // :72-87
     return (int16_t)((tanh_q15(x >> 1, tbl) >> 1) + 16384);
 }
+// tanh_q15 / sigmoid_q15 on the re-indexed table nnsp_tbl_tanh1 (tables.py
+// tanh_interp_shifted; 256 (value, slope) pairs, the split NN kernels' LDS
+// copy): the segment index (|x| + 512) >> 10 needs no clamp from below, the
+// offset in the segment is (|x| + 512) & 1023, and the sign is restored with
+// an xor and a subtract -- 15 VALU instead of ~19 (the LSTM gates evaluate
+// five of these per unit and step).  Equal to tanh_q15 for every int32 but
+// INT32_MIN (tests/test_tables.py, exhaustively over |x| < 2^18 and beyond).
+__device__ __forceinline__ int32_t tanh_q15s_mag(int32_t a, const int16_t* tbl1) {   // a = |x| >= 0
+    const uint32_t bb = (uint32_t)a + 512u;
+    // (one v_bfe_u32 the compiler keeps: from the builtin it emits a shift,
+    // a mask and an add for the scaled table offset instead of bfe + lshl_add)
+    uint32_t kx;
+    asm("v_bfe_u32 %0, %1, 10, 8" : "=v"(kx) : "v"(bb));
+    const int32_t dx = (int32_t)(bb & 1023u);
+    const uint32_t pr = reinterpret_cast<const uint32_t*>(tbl1)[kx];
+    int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (__mul24(dx, (int32_t)(int16_t)(pr >> 16)) >> 15);
+    v = v > 0 ? v : 0;
+    return a >= (5 << 15) ? 0x7fff : v;
+}
+__device__ __forceinline__ int16_t tanh_q15s(int32_t x, const int16_t* tbl1) {
+    const int32_t s = x >> 31;
+    const int32_t y = tanh_q15s_mag((x ^ s) - s, tbl1);
+    return (int16_t)((y ^ s) - s);
+}
+__device__ __forceinline__ int16_t sigmoid_q15s(int32_t x, const int16_t* tbl1) {
+    return (int16_t)((tanh_q15s(x >> 1, tbl1) >> 1) + 16384);
+}
 __device__ __forceinline__ int16_t relu6_q12(int32_t x) {   // :6-17
     int32_t v = x >> 3;
     v = v > 24576 ? 24576 : v;

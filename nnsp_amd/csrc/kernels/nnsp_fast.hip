@@ -32,6 +32,7 @@
 
 using namespace nnsp;
 
+#define TT_BYTES 1024   // LDS copy of nnsp_tbl_tanh1 (tanh_q15s), behind the staged A fragments
 #define P_ASTRIDE 264   // int16 per row of a proj activation buffer
 #define P_UNION 1920    // context frames of a tile: G streams x (32/G + 4) frames x 40 features (int16)
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
@@ -167,7 +168,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
                 if (act == ACT_LINEAR)
                     reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
                 else
-                    out[sc * out_stride + row] = act16(act, v, tt);
+                    out[sc * out_stride + row] = act16s(act, v, tt);
             }
         }
     };
@@ -234,7 +235,7 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
                             if (act == ACT_LINEAR)
                                 reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;
                             else
-                                out[sc * out_stride + row] = act16(act, v, tt);
+                                out[sc * out_stride + row] = act16s(act, v, tt);
                         }
                     }
             };
@@ -306,9 +307,9 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
     using PW = ProjWave<SH>;
-    PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     constexpr bool GEN = SH::generic;
     // wave-uniform tile arithmetic (32-bit, scalar): with the wave index in a
     // VGPR every tile paid three 64-bit divisions on the VALU (~250 VALU per tile)
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     if (pwc) pwc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, false);
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
     __syncthreads();
     if (pwc) pwc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     int ntile_run = 0;
@@ -717,13 +718,13 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     if ((int)(blockIdx.x * (blockDim.x / (64 * RW))) * 16 >= nrow) return;   // whole workgroup past the list
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
     using RT = RecTile<SH>;
     constexpr int R_STRIDE_ = RT::RS;
-    RT* tiles = reinterpret_cast<RT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    RT* tiles = reinterpret_cast<RT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true);
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tpw = blockDim.x / (64 * RW);
     const int tl = wv / RW, g = wv - tl * RW;   // tile in workgroup, wave in tile
@@ -824,11 +825,11 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                                     const int64_t pre = x + hx + er[i].cst;
                                     v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                                 }
-                                gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                                gt[i] = i == 1 ? tanh_q15s(v, tt) : sigmoid_q15s(v, tt);
                             }
                             const int32_t c_old = R.c[sc][u];
                             const int32_t c_new = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old) >> 15);
-                            const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * gt[3]) >> 15);
+                            const int16_t hv = sat16(((int32_t)tanh_q15s(c_new, tt) * gt[3]) >> 15);
                             if (active) R.c[sc][u] = c_new;
                             R.h[cur ^ 1][sc][u] = active ? hv : R.h[cur][sc][u];   // h after all groups (T6)
                         }
@@ -1049,12 +1050,12 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     const int i0 = ((int)blockIdx.x * TPW + sub) * 16;   // tile = 16 consecutive entries of the stream list
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
-    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + 768);
-    PT* RT = reinterpret_cast<PT*>(smem + r.a_lds_bytes + 768 + ep_bytes(r.ep_n));
+    EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
+    PT* RT = reinterpret_cast<PT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     PT& R = RT[sub];
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) tt[i] = nnsp_tbl_tanh[i];
+    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
     if (wgc) wgc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     const int lane = threadIdx.x & 63;
     const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - sub * CF::NWV;   // < RGP: LSTM wave; then stages
@@ -1136,21 +1137,29 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             xr[kt][1] = *reinterpret_cast<const int4*>(p + XS);
         }
     };
+    // ACC32 (int32 accumulators, wrapping): the gate rows' epilogue constants
+    // start the low-plane accumulators of the input half, so the gates add
+    // nothing but the high plane (mod 2^32 the same sum, affine_acc32b.c's
+    // wrap and the proven-int32 acc64 nets alike); the step then loads no cst
+    constexpr bool CST_IN_ACC = ACC32;
     auto x_half = [&]() {   // axh/axl := Wx . x (hi / lo planes) from xr
         v4i bxh[nkt_r], bxl[nkt_r];
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
-            // (past xs: the split of zeros; the A columns there are zero too)
-            const bool in = 64 * kt + 16 * q < XS;
-            const int4 h = in ? xr[kt][0] : make_int4(0, 0, 0, 0);
-            const int4 l = in ? xr[kt][1] : make_int4(0x80808080, 0x80808080, 0x80808080, 0x80808080);
-            bxh[kt] = v4i{h.x, h.y, h.z, h.w};
-            bxl[kt] = v4i{l.x, l.y, l.z, l.w};
+            // lanes whose k range lies past xs loaded column 0 of the row:
+            // used as is, since the A fragments' columns past the LSTM's input
+            // width are zero (a select here cost 16 VALU moves per step)
+            bxh[kt] = v4i{xr[kt][0].x, xr[kt][0].y, xr[kt][0].z, xr[kt][0].w};
+            bxl[kt] = v4i{xr[kt][1].x, xr[kt][1].y, xr[kt][1].z, xr[kt][1].w};
         }
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {   // one row tile's fragments at a time (no LDS stores here)
             axh[k] = v4i{0, 0, 0, 0};
             axl[k] = v4i{0, 0, 0, 0};
+            if (CST_IN_ACC && g + RGP * k < nrt) {
+                const EpRow* er = epl + 16 * (g + RGP * k);
+                axl[k] = v4i{ep_cst<true>(er[0]), ep_cst<true>(er[1]), ep_cst<true>(er[2]), ep_cst<true>(er[3])};
+            }
             if (g + RGP * k < nrt)
 #pragma unroll
                 for (int kt = 0; kt < nkt_r; ++kt) {
@@ -1227,7 +1236,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                         for (int kt = 0; kt < nkt_r; ++kt)
                             w[k][kt] = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * nkt_r + kt) * 1024 + 16 * lane);
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) cst[k][i] = ep_cst<ACC32>(epl[16 * rt + i]);
+                        for (int i = 0; i < 4; ++i) cst[k][i] = CST_IN_ACC ? 0 : ep_cst<ACC32>(epl[16 * rt + i]);
                         c_old[k] = u < N ? R.c[sc][u] : 0;
                         h_old[k] = u < N ? R.h[cur][sc][u] : (int16_t)0;
                     }
@@ -1275,7 +1284,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                 if constexpr (decltype(nolsh)::value) {
                                     const int32_t u = wadd(hx, (int32_t)cst[k][i]);
                                     if (i != 1) {   // sigmoid_q15's >> 1 folded into the layer shift
-                                        gt[i] = (int16_t)((tanh_q15(u >> rsh1, tt) >> 1) + 16384);
+                                        gt[i] = (int16_t)((tanh_q15s(u >> rsh1, tt) >> 1) + 16384);
                                         continue;
                                     }
                                     v = u >> rsh;
@@ -1285,10 +1294,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                     const int64_t pre = (int64_t)hx + cst[k][i];
                                     v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                                 }
-                                gt[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+                                gt[i] = i == 1 ? tanh_q15s(v, tt) : sigmoid_q15s(v, tt);
                             }
                             c_new[k] = cell_q15(gt[0], gt[1], gt[2], c_old[k]);
-                            hv[k] = sat16(((int32_t)tanh_q15(c_new[k], tt) * gt[3]) >> 15);
+                            hv[k] = sat16(((int32_t)tanh_q15s(c_new[k], tt) * gt[3]) >> 15);
                         }
                     }
                 };
@@ -1558,7 +1567,7 @@ extern "C" {
 
 size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape) {
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
-    const size_t base = (size_t)a_bytes + 768 + ep_bytes(ep_rows);
+    const size_t base = (size_t)a_bytes + TT_BYTES + ep_bytes(ep_rows);
     size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
     switch (shape) {   // compiled shapes: recur runs one pipelined tile per workgroup
         case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(PipeTile<ShapeVad>); units = which ? PipeCfg<ShapeVad>::TPW : units; break;

@@ -36,6 +36,8 @@ using namespace nnsp;
 // bit reversal), where the split reads bins k and 256-k.  LDS slots are
 // swizzled (zslot) so that every one of these accesses is bank-conflict-free.
 #define FE_MEL_MAXSEG 3   // max lane segments per Mel bank (nnsp_tbl_melseg)
+#define FE_MEL_LEN 11     // MACs per lane segment (tables.mel_segments max_len: 454 coefficients in 62 segments
+                          // of <= 11 over the 64 lanes; 12 gave 59, 10 would need 65)
 #ifndef FE_WPG
 #define FE_WPG 4          // fe_kernel: waves (frames in flight) per workgroup, sharing its LDS tables
                           // (8: one table staging per 8 waves, 37 KB LDS, three workgroups per CU --
@@ -64,7 +66,7 @@ struct FeTables {
                           // stdR (fe_norm_word) -- dense, so that 40 lanes read 40 banks
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
     uint4 win[64];        // per lane: window taps 128*m + 2*lane, +1 as int16 pairs (0 past tap 479)
-    int16_t mc[12][64];   // per lane: its Mel segment's 12 coefficients, zero-padded, read with
+    int16_t mc[FE_MEL_LEN][64];   // per lane: its Mel segment's coefficients, zero-padded, read with
                           // sign-extending ds_read_i16 (no VALU unpacking; LDS, not VGPRs:
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
 };   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
@@ -138,7 +140,7 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
         }
         const int* sg = nnsp_tbl_melseg + 4 * lane;
         const int mn = sg[2];
-        for (int i = 0; i < 12; ++i) T.mc[i][lane] = (int16_t)(i < mn ? nnsp_tbl_mel[sg[3] + i] : 0);
+        for (int i = 0; i < FE_MEL_LEN; ++i) T.mc[i][lane] = (int16_t)(i < mn ? nnsp_tbl_mel[sg[3] + i] : 0);
         T.win[lane] = make_uint4(w[0], w[1], w[2], w[3]);
     }
 }
@@ -592,11 +594,11 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
         }
         wave_lds_sync();
         FCLK(3);
-        // ---- Mel (melSpecProc.c:6-27): lane segments of <= 12 MACs (zero-padded), then per bank
+        // ---- Mel (melSpecProc.c:6-27): lane segments of <= FE_MEL_LEN MACs (zero-padded), then per bank
         {
             int64_t mac = 0;
 #pragma unroll
-            for (int i = 0; i < 12; ++i) mac = mad_i64_i32((int32_t)TB.mc[i][lane], P[L.mj0 + i], mac);
+            for (int i = 0; i < FE_MEL_LEN; ++i) mac = mad_i64_i32((int32_t)TB.mc[i][lane], P[L.mj0 + i], mac);
             Mp[lane] = mac;
         }
         wave_lds_sync();
@@ -917,7 +919,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
         {   // Mel (melSpecProc.c:6-27) of both frames; partial sums into the dead X
             int64_t ma = 0, mb = 0;
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
+            for (int i = 0; i < FE_MEL_LEN; ++i) {
                 const int32_t c0 = TB.mc[i][lane];
                 ma = mad_i64_i32(c0, PA[L.mj0 + i], ma);
                 mb = mad_i64_i32(c0, PB[L.mj0 + i], mb);

@@ -83,6 +83,20 @@ def tanh_interp() -> np.ndarray:
     return np.minimum(np.stack([val, der], 1).reshape(-1), 32767).astype(np.int16)
 
 
+def tanh_interp_shifted() -> np.ndarray:
+    """The tanh (value, slope) table re-indexed for the split NN kernels'
+    branch-light lookup (nnsp_dev.h tanh_q15s): entry k' = (|x| + 512) >> 10
+    (k' - 1 is activation.c's segment), so the offset inside the segment is
+    (|x| + 512) & 1023 with no clamp of the index from below.  Entry 0 covers
+    |x| < 512, where the reference's segment 0 evaluates to |x| - 1
+    (511 + floor((|x| - 512) * 32760 / 2^15)): (-512, 32767) gives the same.
+    Entries 193..255 keep the 8-bit index in bounds past |x| >= 5 * 2^15, where
+    the result is 32767 regardless (tests/test_tables.py checks all of it)."""
+    t = tanh_interp().astype(np.int64).reshape(-1, 2)
+    pad = np.tile([[32767, 0]], (256 - 1 - len(t), 1))
+    return np.concatenate([[[-512, 32767]], t, pad]).reshape(-1).astype(np.int16)
+
+
 def cfft256_twiddles() -> np.ndarray:
     i = np.arange(192)
     v = np.stack([np.cos(2 * np.pi * i / 256), np.sin(2 * np.pi * i / 256)], 1).reshape(-1) * 2.0 ** 31
@@ -113,7 +127,7 @@ def rfft512_split_coefs() -> np.ndarray:
     return np.stack([a[32 * k], a[32 * k + 1], b[32 * k]], 1).astype(np.int32)
 
 
-def mel_segments(max_len: int = 12, lanes: int = 64) -> np.ndarray:
+def mel_segments(max_len: int = 11, lanes: int = 64) -> np.ndarray:
     """Work split of the 40-bank Mel sum over the 64 lanes of a wave.
 
     Each row = (bank, first bin, n coefficients <= max_len, offset of the first
@@ -188,6 +202,7 @@ def header_text() -> str:
         _c_array("int16_t", "nnsp_tbl_mel", mel),
         _c_array("int16_t", "nnsp_tbl_log", log_interp()),
         _c_array("int16_t", "nnsp_tbl_tanh", tanh_interp()),
+        _c_array("int16_t", "nnsp_tbl_tanh1", tanh_interp_shifted()),
         _c_array("int32_t", "nnsp_tbl_tw256", cfft256_twiddles(), 6),
         _c_array("int32_t", "nnsp_tbl_split", rfft512_split_coefs(), 6),
         _c_array("int32_t", "nnsp_tbl_melseg", mel_segments(), 4),
