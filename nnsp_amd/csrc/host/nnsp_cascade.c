@@ -715,15 +715,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     DBG(bst, "casc_begin", -1, -1);
     if (ahead_done) TRY(nnspk_event_record(c->ev[0], c->stream));   /* c->stream is idle: about now */
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, bst));
-    /* behind the fork (off round 0's start): nothing in this chunk reads what
-     * they write -- the cold frames read d_hist[k % 3], the look-ahead front
-     * end takes its tail from pcm */
-    if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
-        TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
-    TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
-    /* the next chunk's counters (copied out and taken at the end of the last call) */
-    TRY(nnspk_memset((char *)c->d_zero + (size_t)((k + 1) & 1) * ZERO_STRIDE, 0, ZERO_BYTES, c->stream));
-    int ahead_launched = 0;
+    int ahead_launched = 0, behind_launched = 0;
     /* the look-ahead front end starts once the nets' first round (the bulk of
      * the chunk's NN work) is done: running beside it from the start, or with
      * its workgroups capped or short-lived, or on a CU partition, it slowed
@@ -739,6 +731,19 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     for (;;) {
         for (; r < R; ++r) {
             TRY(launch_round(c, &a, r, pcm, T, hist));
+            if (!behind_launched) {
+                /* behind the fork, launched after round 0 (the GPU waited ~30 us
+                 * for round 0's first kernel while the host enqueued these ahead
+                 * of it): nothing in this chunk reads what they write -- the
+                 * cold frames read d_hist[k % 3], the look-ahead front end takes
+                 * its tail from pcm */
+                if (T < c->H) /* shorter chunk: part of the history comes from the previous one */
+                    TRY(nnspk_launch_hist_roll(c->d_hist[(k + 1) % 3], hist, pcm, c->S, T, c->H, c->stream));
+                TRY(nnspk_launch_tail_roll(c->d_stail, pcm, c->S, T, NULL, 0, NULL, 0, 0, NULL, 0, c->stream));
+                /* the next chunk's counters (copied out and taken at the end of the last call) */
+                TRY(nnspk_memset((char *)c->d_zero + (size_t)((k + 1) & 1) * ZERO_STRIDE, 0, ZERO_BYTES, c->stream));
+                behind_launched = 1;
+            }
             if (ahead && !ahead_launched) {
                 for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[r & 1][n]));
                 const int q = (int)((k + 1) & 1);

@@ -38,6 +38,9 @@ static struct {
     jmp_buf jb;
     int sticky;  /* first error since nnsp_legacy_clear(); 0 = none */
     int port;    /* 1: the reference's ARM_OPTIMIZED=0 build (row N4); 2: not yet read */
+    uint8_t *hpin;  /* pinned host staging of NNSPClass_exec: one upload, one download per frame */
+    size_t hpin_cap;
+    void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
 } G = {.port = 2};
 
 /* The build the drop-in API reproduces: the reference selects it at compile
@@ -87,6 +90,8 @@ static int gctx(void)
     if (e) return e;
     G.cap = 4u << 20;
     if ((e = nnspk_malloc((void **)&G.arena, G.cap))) return e;
+    G.hpin_cap = 64u << 10;
+    if ((e = nnspk_host_alloc((void **)&G.hpin, G.hpin_cap))) return e;
     G.ready = 1;
     return 0;
 }
@@ -153,6 +158,8 @@ typedef struct img_node {
     uint64_t bytes;
     nnsp_image im;
     int out_linear;
+    uint8_t *blob;      /* net images: a host copy of every table byte the image was built from */
+    size_t blob_n;
 } img_node;
 static img_node *g_imgs;
 
@@ -207,6 +214,7 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
         if (before_last) before_last->next = NULL;
         else g_imgs = NULL;
         nnsp_image_free(&last->im);
+        free(last->blob);
         free(last);
     }
     img_node *n = (img_node *)calloc(1, sizeof *n);
@@ -227,9 +235,53 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
     return n;
 }
 
-/* A NeuralNetClass's device image: keyed by its address, a hash of its shape,
- * qbits, layer / activation functions and table pointers, and the hash of
- * its tables' bytes. */
+/* the table bytes of a layer list, in order (W, Wr, B per layer): their
+ * total size, and a copy into dst / a comparison with src */
+static size_t layer_span(const nnsp_layer_desc *d, int which)
+{
+    const size_t rows = (size_t)(d->type == NN_LSTM ? 4 * d->N : d->N);
+    if (which == 0) return d->W ? rows * (size_t)d->K : 0;
+    if (which == 1) return d->Wr ? rows * (size_t)d->N : 0;
+    return d->B ? rows * 2 : 0;
+}
+static const void *layer_ptr(const nnsp_layer_desc *d, int which)
+{
+    return which == 0 ? (const void *)d->W : (which == 1 ? (const void *)d->Wr : (const void *)d->B);
+}
+static size_t tables_bytes(const nnsp_layer_desc *L, int nl)
+{
+    size_t n = 0;
+    for (int i = 0; i < nl; ++i)
+        for (int w = 0; w < 3; ++w) n += layer_span(&L[i], w);
+    return n;
+}
+static int tables_equal(const uint8_t *blob, size_t blob_n, const nnsp_layer_desc *L, int nl)
+{
+    size_t o = 0;
+    for (int i = 0; i < nl; ++i)
+        for (int w = 0; w < 3; ++w) {
+            const size_t n = layer_span(&L[i], w);
+            if (!n) continue;
+            if (o + n > blob_n || memcmp(blob + o, layer_ptr(&L[i], w), n)) return 0;
+            o += n;
+        }
+    return o == blob_n;
+}
+static void tables_copy(uint8_t *blob, const nnsp_layer_desc *L, int nl)
+{
+    for (int i = 0; i < nl; ++i)
+        for (int w = 0; w < 3; ++w) {
+            const size_t n = layer_span(&L[i], w);
+            if (n) memcpy(blob, layer_ptr(&L[i], w), n);
+            blob += n;
+        }
+}
+
+/* A NeuralNetClass's device image: keyed by its address and a hash of its
+ * shape, qbits, layer / activation functions and table pointers; the tables'
+ * bytes are compared with the copy the image was built from (memcmp: the
+ * reference reads its tables on every call, so tables rewritten in place get
+ * a new image -- a byte-wise hash of them was ~30 % of a drop-in S2I frame) */
 static img_node *net_image(const NeuralNetClass *net)
 {
     uint64_t h = 1469598103934665603ULL;
@@ -251,12 +303,24 @@ static img_node *net_image(const NeuralNetClass *net)
     int nl = 0, lin = 0;
     CK(nnsp_describe_net(net, L, &nl, &lin));
     for (int i = 0; i < nl; ++i) L[i].portable = port_on();
-    uint64_t bytes = 1469598103934665603ULL;
-    for (int i = 0; i < nl; ++i) bytes = layer_bytes_hash(bytes, &L[i]);
     const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
-    img_node *n = img_find(net, NULL, NULL, NULL, ik, bytes);
-    if (n) return n;
-    return img_add(net, NULL, NULL, NULL, ik, bytes, L, nl, lin);
+    img_node *n = img_find(net, NULL, NULL, NULL, ik, 0);
+    if (n && tables_equal(n->blob, n->blob_n, L, nl)) return n;
+    if (n) { /* tables changed in place: this image is stale */
+        CK(nnspk_sync(G.stream));
+        g_imgs = n->next; /* img_find moved it to the front */
+        nnsp_image_free(&n->im);
+        free(n->blob);
+        free(n);
+    }
+    const size_t nb = tables_bytes(L, nl);
+    uint8_t *blob = (uint8_t *)malloc(nb ? nb : 1);
+    if (!blob) fail(NNSP_ENOMEM, "image cache tables copy");
+    tables_copy(blob, L, nl);
+    n = img_add(net, NULL, NULL, NULL, ik, 0, L, nl, lin);
+    n->blob = blob;
+    n->blob_n = nb;
+    return n;
 }
 
 /* LSTM h/c of a NeuralNetClass <-> device rows [l][hs] (hs: the widest
@@ -817,6 +881,13 @@ static void post_unpack(NNSPClass *p, const NnPost *q)
     memcpy(p->outputs, q->outputs, sizeof q->outputs);
 }
 
+static size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+/* One frame as a GPU batch of one stream.  Everything the call reads goes up
+ * in one copy from a pinned staging buffer, everything it returns comes back
+ * in one (per frame: one upload, the front end, the NN, one download, one
+ * synchronisation; separate small copies from pageable memory made a frame
+ * ~160-250 us, bench.py --dropin-latency). */
 static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
 {
     FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
@@ -827,38 +898,86 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     img.nn_id = pt_inst->nn_id;
     img.thresh_prob = *pt_inst->pt_thresh_prob;
     img.th_count = *pt_inst->pt_th_count_trigger;
-    FeArgs a;
-    memset(&a, 0, sizeof a);
-    const int16_t *pcm_d = (const int16_t *)up(rawPCM, 320);
-    a.pcm = pcm_d;
-    a.tail = (const int16_t *)up(fe->state_stftModule.dataBuffer + 160, 640);
-    a.S = 1; a.T = 1;
-    a.mean = (const int32_t *)up(fe->pt_norm_mean, 160);
-    a.stdR = (const int32_t *)up(fe->pt_norm_stdR, 160);
-    a.norm_shift = 30 - fe->qbit_output;
-    a.feats = (int16_t *)up(NULL, 80);
-    a.dbg_log = (int32_t *)up(NULL, 160);
-    a.port = port_on();
-    CK(nnspk_launch_fe(&a, G.stream));
+    const int hs = net_hs(net);
+    int nls = 0;
+    for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i) nls += net->net_layer_type[i] == lstm;
+    if (nls > NN_MAX_LSTM) nls = NN_MAX_LSTM;
+    const size_t rows = (size_t)(nls ? nls : 1);
+    /* staging layout: inputs | state in and out | outputs */
+    const size_t o_pcm = 0, o_tail = 320, o_mean = o_tail + 640, o_std = o_mean + 160, o_p5 = o_std + 160;
+    const size_t o_post = al16(o_p5 + 400), o_h = o_post + al16(sizeof(NnPost)), o_c = o_h + al16(rows * hs * 2);
+    const size_t o_feat = o_c + al16(rows * hs * 4), o_log = o_feat + 80, o_trig = o_log + 160;
+    const size_t total = al16(o_trig + 2);
+    if (total > G.hpin_cap) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
+    uint8_t *hp = G.hpin;
+    memcpy(hp + o_pcm, rawPCM, 320);
+    memcpy(hp + o_tail, fe->state_stftModule.dataBuffer + 160, 640);
+    memcpy(hp + o_mean, fe->pt_norm_mean, 160);
+    memcpy(hp + o_std, fe->pt_norm_stdR, 160);
+    memcpy(hp + o_p5, fe->normFeatContext + 40, 400);
     NnPost ps;
     post_pack(pt_inst, &ps);
+    memcpy(hp + o_post, &ps, sizeof ps);
+    memset(hp + o_h, 0, o_feat - o_h);
+    {
+        int l = 0;
+        for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
+            if (net->net_layer_type[i] == lstm) {
+                const int N = net->size_layer[i + 1];
+                memcpy(hp + o_h + (size_t)l * hs * 2, net->pt_hstate[i], (size_t)N * 2);
+                memcpy(hp + o_c + (size_t)l * hs * 4, net->pt_cstate[i], (size_t)N * 4);
+                ++l;
+            }
+    }
+    uint8_t *d = (uint8_t *)dscratch(total);
+    CK(nnspk_h2d(d, hp, o_feat, G.stream));
+    FeArgs a;
+    memset(&a, 0, sizeof a);
+    a.pcm = (const int16_t *)(d + o_pcm);
+    a.tail = (const int16_t *)(d + o_tail);
+    a.S = 1; a.T = 1;
+    a.mean = (const int32_t *)(d + o_mean);
+    a.stdR = (const int32_t *)(d + o_std);
+    a.norm_shift = 30 - fe->qbit_output;
+    a.feats = (int16_t *)(d + o_feat);
+    a.dbg_log = (int32_t *)(d + o_log);
+    a.port = port_on();
+    if (!G.fetab[a.port]) { /* deriving them in every launch was ~20 us of dependent loads per frame */
+        FeArgs ta;
+        memset(&ta, 0, sizeof ta);
+        ta.mode = FE_MODE_BATCH;
+        ta.port = a.port;
+        CK(nnspk_build_fe_tables(&G.fetab[a.port], &ta, G.stream));
+    }
+    a.tb_img = G.fetab[a.port];
+    CK(nnspk_launch_fe(&a, G.stream));
     NnRun r;
     memset(&r, 0, sizeof r);
     r.S = 1; r.T = 1; r.mode = NN_MODE_STREAM; r.nl_run = img.nl;
     r.feats = a.feats;
-    r.prev5 = (const int16_t *)up(fe->normFeatContext + 40, 400);
-    r.hs = net_hs(net);
-    net_state_up(net, r.hs, &r.h, &r.c);
-    r.post = up(&ps, sizeof ps);
-    r.trig = (int16_t *)up(NULL, 2);
+    r.prev5 = (const int16_t *)(d + o_p5);
+    r.hs = hs;
+    r.h = (int16_t *)(d + o_h);
+    r.c = (int32_t *)(d + o_c);
+    r.post = d + o_post;
+    r.trig = (int16_t *)(d + o_trig);
     CK(nnspk_launch_nn(&img, &r, G.stream));
-    int16_t f5[40];
-    down(f5, a.feats, 80);
-    down(fe->feature, a.dbg_log, 160);
-    down(&ps, r.post, sizeof ps);
-    net_state_down(net, r.hs, r.h, r.c); /* syncs */
+    CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
+    fin();
+    memcpy(&ps, hp + o_post, sizeof ps);
+    {
+        int l = 0;
+        for (int i = 0; i < net->numlayers && l < NN_MAX_LSTM; ++i)
+            if (net->net_layer_type[i] == lstm) {
+                const int N = net->size_layer[i + 1];
+                memcpy(net->pt_hstate[i], hp + o_h + (size_t)l * hs * 2, (size_t)N * 2);
+                memcpy(net->pt_cstate[i], hp + o_c + (size_t)l * hs * 4, (size_t)N * 4);
+                ++l;
+            }
+    }
+    memcpy(fe->feature, hp + o_log, 160);
     memmove(fe->normFeatContext, fe->normFeatContext + 40, 200 * 2);
-    memcpy(fe->normFeatContext + 200, f5, 80);
+    memcpy(fe->normFeatContext + 200, hp + o_feat, 80);
     memmove(fe->state_stftModule.dataBuffer, fe->state_stftModule.dataBuffer + 160, 320 * 2);
     memcpy(fe->state_stftModule.dataBuffer + 320, rawPCM, 160 * 2);
     post_unpack(pt_inst, &ps);

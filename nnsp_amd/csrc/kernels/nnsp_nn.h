@@ -78,12 +78,16 @@ __device__ __forceinline__ int16_t act16s(int act, int32_t v, const int16_t* tt1
 // through another branch's base -- out of bounds, a memory fault in
 // recur_pipe_kernel.  With the select the base is a VGPR per lane.
 // fs.nring is wave-uniform.
+// KNOWN: fr is the stream's fresh[] value, already loaded by the caller
+// (proj's descriptor pipeline); otherwise it is loaded here for the first two
+// frames of a segment
+template <bool KNOWN = false>
 __device__ __forceinline__ const int16_t* feat8_ptr(const FeatSrc& fs, const int16_t* feats, int s, int T, int b, int t,
-                                                  int part) {
+                                                  int part, int fr = 2) {
     if (!fs.nring) return feats + ((size_t)s * T + t) * 40 + 8 * part;
     // only the first two frames of a segment can be cold: the fresh[] load
     // (and the dependent-load latency) only for those
-    const bool cold = t - b < 2 && t - b + fs.fresh[s] < 2;
+    const bool cold = t - b < 2 && t - b + (KNOWN ? fr : (int)fs.fresh[s]) < 2;
     // (abs0 + t - lookback) mod ring with 0 <= abs0 < ring, 0 <= t < Tmax <=
     // ring and lookback < ring (host): the sum plus ring is in [1, 3 ring),
     // two conditional subtracts instead of a 32-bit division (~30 VALU)
