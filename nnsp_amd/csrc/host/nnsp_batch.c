@@ -343,6 +343,20 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
     return 0;
 }
 
+/* recur (compiled shapes): 16-stream tiles per workgroup, run back to back
+ * through one pipeline -- its fill and drain (4 iterations) and the weight
+ * staging once per workgroup instead of once per tile.  Short segments (a
+ * cascade round's window) gain most; NNSP_RECUR_TSEQ=1..4 overrides. */
+static int recur_tseq(const nnsp_segment *seg, int T)
+{
+    const char *e = getenv("NNSP_RECUR_TSEQ");   /* (read per launch: tests switch it) */
+    const int env = e ? atoi(e) : 0;
+    if (env > 0) return env > 4 ? 4 : env;
+    const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
+    const int steps = (W + 1) / 2;
+    return steps <= 8 ? 4 : (steps <= 16 ? 2 : 1);
+}
+
 int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, const nnsp_segment *seg,
                       void *stream)
 {
@@ -405,6 +419,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;
         f.ep_n = b->ep_rec_n;
+        f.tseq = recur_tseq(seg, T);
         TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, seg->ctl, stream));
     } else {
         NnRun r;

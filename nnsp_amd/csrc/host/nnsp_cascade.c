@@ -237,7 +237,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_nring[0], 3 * S * (size_t)c->ring * 40 * 2))) goto fail;
     for (int i = 1; i < 3; ++i) c->d_nring[i] = c->d_nring[0] + (size_t)i * S * c->ring * 40;
     if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
-    if ((e = nnspk_malloc((void **)&c->d_fresh, S))) goto fail;
+    /* (rounded up to whole dwords: proj DMAs the dword holding a stream's byte) */
+    if ((e = nnspk_malloc((void **)&c->d_fresh, ((size_t)S + 3) & ~(size_t)3))) goto fail;
     for (int i = 0; i < 3; ++i) {
         if ((e = nnspk_malloc((void **)&c->d_trig[i], S * T * 2))) goto fail;
         if ((e = nnspk_malloc((void **)&c->d_mask[i], S))) goto fail;

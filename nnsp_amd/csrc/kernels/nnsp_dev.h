@@ -141,13 +141,30 @@ __device__ __forceinline__ void split_bin(int32_t xr, int32_t xi, int32_t yr, in
 // by tests/test_tables.py) -- and rnd_sub(x, -c) = rnd_add(x, c), so bin 256-k
 // is split_bin with x and y swapped and two of its eight rounded products,
 // xr*A2 (SMMLAR) and yr*A2 (SMMLSR), are bin k's own: 14 products per pair.
+//
+// Each rounded product is one v_mad_i64_i32 with its rounding constant in an
+// SGPR pair, its high word taken as is (rp_add: floor((x c + 2^31) / 2^32);
+// rp_sub: floor((x c + 2^31 - 1) / 2^32), subtracted); the terms are then
+// summed in 32 bits (v_add3 / v_sub).  Written as plain C the compiler chained
+// each product's addend with the previous term's high word -- a v_mov and a
+// 64-bit add per product, 18 extra VALU per frame.
+__device__ __forceinline__ int32_t rp_hi(int32_t x, int32_t c, uint64_t k) {
+    int64_t r;
+    uint64_t carry;
+    asm("v_mad_i64_i32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry) : "v"(x), "v"(c), "s"(k));
+    int32_t h = (int32_t)((uint64_t)r >> 32);
+    asm("" : "+v"(h));   // an opaque high word: no re-association into 64-bit adds
+    return h;
+}
+__device__ __forceinline__ int32_t rp_add(int32_t x, int32_t c) { return rp_hi(x, c, 0x80000000ull); }   // = rnd_add
+__device__ __forceinline__ int32_t rp_sub(int32_t x, int32_t c) { return rp_hi(x, c, 0x7FFFFFFFull); }   // = -rnd_sub
 __device__ __forceinline__ void split_pair(int32_t xr, int32_t xi, int32_t yr, int32_t yi, int32_t A1, int32_t A2,
                                            int32_t B1, int32_t& re0, int32_t& im0, int32_t& re1, int32_t& im1) {
-    const int32_t xa2 = rnd_add(xr, A2), ya2 = rnd_sub(yr, A2);
-    re0 = wadd(wadd(rnd_add(xr, A1), rnd_sub(xi, A2)), wadd(rnd_sub(yi, A2), rnd_add(yr, B1)));
-    im0 = wadd(wadd(xa2, rnd_add(xi, A1)), wadd(rnd_sub(yi, B1), ya2));
-    re1 = wadd(wadd(rnd_add(yr, A1), rnd_add(yi, A2)), wadd(rnd_add(xi, A2), rnd_add(xr, B1)));
-    im1 = wadd(wadd(ya2, rnd_add(yi, A1)), wadd(rnd_sub(xi, B1), xa2));
+    const int32_t xa2 = rp_add(xr, A2), ya2 = rp_sub(yr, A2);   // bin k's xr A2 (+), yr A2 (-)
+    re0 = wsub(wadd(rp_add(xr, A1), rp_add(yr, B1)), wadd(rp_sub(xi, A2), rp_sub(yi, A2)));
+    im0 = wsub(wadd(xa2, rp_add(xi, A1)), wadd(rp_sub(yi, B1), ya2));
+    re1 = wadd(wadd(rp_add(yr, A1), rp_add(yi, A2)), wadd(rp_add(xi, A2), rp_add(xr, B1)));
+    im1 = wsub(wadd(rp_add(yi, A1), xa2), wadd(ya2, rp_sub(xi, B1)));
 }
 
 // spec2pspec_arm (spectrogram_module.c:79-92): truncating cast of (re^2+im^2)>>27

@@ -288,17 +288,48 @@ __device__ __forceinline__ void put_frame(const FastRun& r, int s, int T, int f,
 // activations overwrite its own union once the FC layer has read it (the
 // B operand is loaded before the first output store), so the act rows need
 // no buffer of their own.
-template <class SH>
+//
+// Per G (streams per tile) the union holds G x (32/G + 4) context frames; the
+// descriptor pipeline's slots (pd) take what the tile loop loads ahead by
+// LDS-DMA: per tile parity, lanes 0..G-1, the list entry, segment start,
+// post-state dword (slides) and fresh[] dword.
+template <class SH, int G = 1>
 struct alignas(16) ProjWave {
     static constexpr int AS = SH::generic ? P_ASTRIDE : 64 * SH::NKR + 8;
     static constexpr int NA = SH::generic ? 2 : 1;
-    static constexpr int UNI = (P_UNION + 32) > 16 * AS ? (P_UNION + 32) : 16 * AS;   // int16 per union buffer
+    static constexpr int PU = SH::generic ? P_UNION : G * (32 / G + 4) * 40;      // union int16 of a G tile
+    static constexpr int UNI = (PU + 32) > 16 * AS ? (PU + 32) : 16 * AS;   // int16 per union buffer
     int16_t uni[SH::generic ? 1 : 2][SH::generic ? P_UNION + 32 : UNI];
     int16_t act[SH::generic ? NA : 0][16][AS];
+    int32_t pd[SH::generic ? 0 : 2][4][4];   // [parity][list, seg_begin, post dword, fresh dword][lane < G]
 };
+
+// LDS-DMA (global_load_lds) of BYTES per lane at lds + lane * BYTES, issued
+// from inline asm: the compiler then inserts no wait of its own for it.  With
+// the builtin it put a vmcnt(0) before the first LDS access after the DMA --
+// it cannot tell the buffer being filled from the one being read -- so the
+// next tile's loads were waited for before this tile's compute.  The caller
+// waits (s_waitcnt vmcnt) before reading what it DMA'd.  M0 is saved and
+// restored around it.
+template <int BYTES>
+__device__ __forceinline__ void lds_dma(const void* g, void* lds) {
+    static_assert(BYTES == 4 || BYTES == 16, "lds_dma: dword or dwordx4");
+    const unsigned l =
+        __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)lds);
+    unsigned saved;
+    if constexpr (BYTES == 16)
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(saved) : "v"(g), "s"(l) : "memory");
+    else
+        asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+                     : "=&s"(saved) : "v"(g), "s"(l) : "memory");
+}
 
 // 16 zero bytes: the source of union elements outside a segment (proj_kernel)
 __device__ __attribute__((aligned(16))) int4 nnsp_proj_zero16;
+// where proj's x-row stores of rows without an NN step go (>= XS + 8 bytes)
+__device__ __attribute__((aligned(16))) uint2 nnsp_proj_sink[32];
+__device__ int32_t nnsp_proj_neg1 = -1;   // the list entry of a tile slot past the list
 
 // GT: streams per 16-row tile (compiled shapes: 1, 2 or 4, FastRun.gpt; one
 // instantiation each, so a G = 1 tile's descriptors are wave-uniform scalars)
@@ -308,9 +339,9 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     uint8_t* W = smem;                                           // staged A fragments
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
-    using PW = ProjWave<SH>;
-    PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     constexpr bool GEN = SH::generic;
+    using PW = ProjWave<SH, GEN ? 1 : GT>;
+    PW* pw = reinterpret_cast<PW*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     // wave-uniform tile arithmetic (32-bit, scalar): with the wave index in a
     // VGPR every tile paid three 64-bit divisions on the VALU (~250 VALU per tile)
     const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -347,8 +378,12 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     __syncthreads();
     if (pwc) pwc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     int ntile_run = 0;
-    // stream k of a tile: list entry, segment start b, length L, NN phase
-    struct Seg { int s, b, L, ph; bool ok; };
+    // stream k of a tile: list entry, segment start b, length L, NN phase,
+    // fresh[] (cascade: frames since the net's reset, 0..2; 2 otherwise) --
+    // loaded with the descriptors, ahead: read in the union loads, it made
+    // every union chunk wait (vmcnt(0)) for it, the loads before it and the
+    // last tile's x stores
+    struct Seg { int s, b, L, ph; bool ok; int fr; };
     // development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0's first tiles
     long long* clk = (r.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? r.dbg_clk + 12 : nullptr;
     int it = 0;
@@ -377,6 +412,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
         g.b = g.ok && r.seg_begin ? r.seg_begin[g.s] : 0;
         g.L = g.ok ? (r.seg_len > 0 ? min(r.T, g.b + r.seg_len) : r.T) - g.b : 0;
         g.ph = g.ok ? 1 - reinterpret_cast<const NnPost*>(r.post)[g.s].slides : 0;
+        g.fr = g.ok && r.fs.nring ? min((int)r.fs.fresh[g.s], 2) : 2;
         return g;
     };
     int tile = (int)blockIdx.x * nwv + wv;
@@ -393,7 +429,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
             if (!__any(lane < G && m.ok && 2 * j0 + m.ph < m.L)) return false;
             const Seg g1 = {__builtin_amdgcn_readfirstlane(m.s), __builtin_amdgcn_readfirstlane(m.b),
                             __builtin_amdgcn_readfirstlane(m.L), __builtin_amdgcn_readfirstlane(m.ph),
-                            __builtin_amdgcn_readfirstlane((int)m.ok) != 0};
+                            __builtin_amdgcn_readfirstlane((int)m.ok) != 0, __builtin_amdgcn_readfirstlane(m.fr)};
             constexpr int NU = G * FR * 5;   // 16-byte chunks (8 features) of the union
             if constexpr (G == 1) {
                 // one stream whose window V[t0 .. t0 + FR) lies past prev5 and
@@ -429,9 +465,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                                 row = row >= rg ? row - rg : row;
                             }
                             const char* src = base + (row * 80u + 16u * (unsigned)part);
-                            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                             (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
-                                                             16, 0, 0);
+                            lds_dma<16>(src, &P.uni[bf][512 * mm]);
                         }
                     }
                     return true;
@@ -450,6 +484,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                         g.L = __shfl(m.L, k);
                         g.ph = __shfl(m.ph, k);
                         g.ok = __shfl((int)m.ok, k) != 0;
+                        g.fr = __shfl(m.fr, k);
                     }
                     const int idx = 2 * j0 + g.ph + fr;
                     const int16_t* src = reinterpret_cast<const int16_t*>(&nnsp_proj_zero16);
@@ -457,36 +492,109 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                         if (idx < 5)
                             src = r.prev5 + ((size_t)g.s * 5 + idx) * 40 + 8 * part;
                         else if (idx - 5 < g.L)
-                            src = feat8_ptr(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part);
+                            src = feat8_ptr<true>(r.fs, r.feats, g.s, r.T, g.b, g.b + idx - 5, part, g.fr);
                     }
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                                     (__attribute__((address_space(3))) void*)&P.uni[bf][512 * mm],
-                                                     16, 0, 0);
+                    lds_dma<16>(src, &P.uni[bf][512 * mm]);
                 }
             }
             return true;
         };
-        // descriptors in flight are held packed (3 VGPRs instead of 5; the
-        // kernel sits at 128): s (-1: none), b, L | phase << 16
-        struct SegP { int s, b, lp; };
-        auto pack = [](const Seg& g) { return SegP{g.ok ? g.s : -1, g.b, g.L | (g.ph << 16)}; };
-        auto unpack = [](const SegP& p) { return Seg{p.s < 0 ? 0 : p.s, p.b, p.lp & 0xffff, p.lp >> 16, p.s >= 0}; };
+        // The descriptor pipeline, in LDS: every load of it lands by LDS-DMA
+        // (global_load_lds, tracked like the union's loads by the top-of-tile
+        // wait; the compiler tracks none of it), so no register waits on an
+        // in-flight load.  At the top of tile t: the slots of tile t+1 (DMA'd a
+        // tile earlier) give its descriptor, whose union then loads; the list
+        // entries of tile t+2 (DMA'd a tile earlier) address the DMA of its
+        // segment start, post-state and fresh[] dwords; the list entries of
+        // tile t+3 are DMA'd.  (Until round 4 the descriptors went through
+        // registers: each tile waited out one memory latency for them, and the
+        // loop-carried copies waited for the last tile's stores.)
+        // Slot parity: tile it + k -> pd[(it + k) & 1].
+        const int* dz = reinterpret_cast<const int*>(&nnsp_proj_zero16);
+        auto dma4 = [&](const void* src, int32_t* dst) { lds_dma<4>(src, dst); };   // lanes < G: dst[lane]
+        auto list_dma = [&](int t, int slot) {   // list entry of tile t (-1: none) -> pd[slot][0]
+            const int i = grp_of(t) * G + (lane < G ? lane : 0);
+            const bool ok = t < ntiles && i < nrow;
+            if (r.list) {
+                if (lane < G) dma4(ok ? (const void*)(r.list + i) : (const void*)&nnsp_proj_neg1, &P.pd[slot][0][0]);
+            } else if (lane < G) {
+                P.pd[slot][0][lane] = ok ? i : -1;
+            }
+        };
+        auto desc_dma = [&](int st, int slot) {   // st: lane's stream (lanes < G) -> pd[slot][1..3]
+            if (lane < G) {
+                const int q = st >= 0 ? st : 0;
+                dma4(st >= 0 && r.seg_begin ? (const void*)(r.seg_begin + q) : (const void*)dz, &P.pd[slot][1][0]);
+                dma4(st >= 0 ? (const void*)(reinterpret_cast<const NnPost*>(r.post) + q) : (const void*)dz,
+                     &P.pd[slot][2][0]);
+                dma4(st >= 0 && r.fs.nring ? (const void*)(r.fs.fresh + (q & ~3)) : (const void*)dz, &P.pd[slot][3][0]);
+            }
+        };
+        auto desc_of = [&](int slot) {   // the descriptor in pd[slot] (lanes < G; G = 1: uniform)
+            const int k = lane < G ? lane : 0;
+            Seg g;
+            const int st = P.pd[slot][0][k];
+            g.ok = st >= 0;
+            g.s = g.ok ? st : 0;
+            g.b = g.ok ? P.pd[slot][1][k] : 0;
+            g.L = g.ok ? (r.seg_len > 0 ? min(r.T, g.b + r.seg_len) : r.T) - g.b : 0;
+            g.ph = g.ok ? 1 - (int)(int16_t)(P.pd[slot][2][k] & 0xffff) : 0;
+            const int fr = (int)(int8_t)((unsigned)P.pd[slot][3][k] >> (8 * (g.s & 3)));
+            g.fr = g.ok && r.fs.nring ? min(max(fr, 0), 2) : 2;
+            if (G == 1) {   // wave-uniform: scalars
+                g.s = __builtin_amdgcn_readfirstlane(g.s);
+                g.b = __builtin_amdgcn_readfirstlane(g.b);
+                g.L = __builtin_amdgcn_readfirstlane(g.L);
+                g.ph = __builtin_amdgcn_readfirstlane(g.ph);
+                g.fr = __builtin_amdgcn_readfirstlane(g.fr);
+                g.ok = __builtin_amdgcn_readfirstlane((int)g.ok) != 0;
+            }
+            return g;
+        };
+        // x rows go out as a fixed number of store instructions per tile (rows
+        // past the segment or the buffer to a sink), so the top-of-tile wait
+        // for the next union need not wait for the last tile's stores: they
+        // are the NST youngest vector memory operations
+        constexpr int NST = 2 * ((16 * XC + 63) / 64);
+        // prologue: tile `tile` with plain loads, the slots of tile + tstride
+        // (descriptor) and tile + 2 tstride (list entry) by DMA, waited for
         Seg mine = seg_from(list_at(tile));
-        SegP mine_n = pack(seg_from(list_at(tile + tstride)));
-        int s_nn = list_at(tile + 2 * tstride);
+        list_dma(tile + tstride, (it + 1) & 1);
+        list_dma(tile + 2 * tstride, it & 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        wave_lds_sync();
+        desc_dma(lane < G ? P.pd[(it + 1) & 1][0][lane] : -1, (it + 1) & 1);
         bool have = tile < ntiles && union_issue(mine, tile, 0);
-        int cb = 0;
-        for (; tile < ntiles; tile += tstride, ++it) {
+        bool stored = false;   // the last tile issued its NST x stores after this tile's union loads
+        // two tiles per trip, the buffer and slot parity CB a template constant:
+        // with a run-time parity the compiler could not tell the union being
+        // read from the one being DMA'd and waited (vmcnt(0)) for the next
+        // tile's loads before reading this tile's
+        auto tile_step = [&](const int CB) {
             PCLK(0);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this tile's union landed
+            // this tile's union landed, and every descriptor DMA issued before it
+            if (stored && !clk)
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+            else
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             wave_lds_sync();
-            // descriptors two tiles ahead, then the next tile's union into the
-            // other buffer (its previous contents, the last tile's x rows, were
-            // stored before the wait above)
-            const SegP mine_nn = pack(seg_from(s_nn));
-            s_nn = list_at(tile + 3 * tstride);
-            const bool have_n = tile + tstride < ntiles && union_issue(unpack(mine_n), tile + tstride, cb ^ 1);
+            const Seg nxt = desc_of(CB ^ 1);                               // tile + tstride
+            const int s2 = lane < G ? P.pd[CB][0][lane] : -1;                      // tile + 2 tstride
+            // the slot reads above complete before the DMAs below write the slots
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            desc_dma(s2, CB);                                                // its descriptor
+            if (lane < G) P.pd[CB][0][lane] = s2;                            // (kept beside it)
+            list_dma(tile + 3 * tstride, CB ^ 1);                          // tile + 3 tstride
+            // the next tile's union into the other buffer (its previous
+            // contents, the last tile's x rows, were read into registers
+            // for their stores before the wait above)
+            const bool have_n = tile + tstride < ntiles && union_issue(nxt, tile + tstride, CB ^ 1);
+            // keep the loads here, ahead of the compute (the compiler would
+            // otherwise sink them below it: they write the other buffer)
+            asm volatile("" ::: "memory");
+            stored = false;
             if (have) {
+
                 ++ntile_run;
                 PCLK(1);
                 const int j0 = j0_of(tile);
@@ -497,13 +605,14 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                     g.L = __shfl(mine.L, k);
                     g.ph = __shfl(mine.ph, k);
                     g.ok = __shfl((int)mine.ok, k) != 0;
+                    g.fr = 2;
                     return g;
                 };
                 // ---- the prefix FC layer, K = 240, tanh (row (k, j)'s context =
                 //      uni[k*FR*40 + 80j .. +239]; the per-lane base makes in +
                 //      sc * 80 that row); its output rows overwrite the union
                 const int kr = sc / SPT, jr = sc - kr * SPT;
-                int16_t* U = &P.uni[cb][0];
+                int16_t* U = &P.uni[CB][0];
                 const int16_t* in = U + kr * FR * 40 + 80 * jr - 80 * sc;
                 const NnLayer& L0 = img.L[0];
                 fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
@@ -513,13 +622,17 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                 // ---- the LSTM's input x of every row to HBM, already in the
                 //      MFMA B operand's split form (split_hilo): per row xs high
                 //      bytes, then xs low bytes ^ 0x80; columns N..xs-1 (not
-                //      written by the layer) are stored as zeros
-                for (int c = lane; c < 16 * XC; c += 64) {
-                    const int row = c / XC, part = c - row * XC;
-                    const int kx = row / SPT, jx = row - kx * SPT;
-                    const Seg g = G == 1 ? mine : seg_k(kx);
-                    const int j = j0 + jx;
-                    if (g.ok && j < r.nstep_max && 2 * j + g.ph < g.L) {
+                //      written by the layer) are stored as zeros.  Every lane
+                //      stores (a row without a step to the sink): NST stores
+#pragma unroll
+                for (int c0 = 0; c0 < 16 * XC; c0 += 64) {
+                    const int c = c0 + lane;
+                    if (c0 + 64 <= 16 * XC || c < 16 * XC) {
+                        const int row = c / XC, part = c - row * XC;
+                        const int kx = row / SPT, jx = row - kx * SPT;
+                        const Seg g = G == 1 ? mine : seg_k(kx);
+                        const int j = j0 + jx;
+                        const bool ok = g.ok && j < r.nstep_max && 2 * j + g.ph < g.L;
                         int4 v = *reinterpret_cast<const int4*>(U + row * PW::AS + 8 * part);
                         if (8 * XC > SH::NW && part == XC - 1) {   // mask the columns past N
                             int32_t w4[4] = {v.x, v.y, v.z, v.w};
@@ -530,24 +643,29 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                             }
                             v = make_int4(w4[0], w4[1], w4[2], w4[3]);
                         }
-                        uint8_t* dst = reinterpret_cast<uint8_t*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS) +
-                                       8 * part;
+                        uintptr_t da = ok ? reinterpret_cast<uintptr_t>(
+                                                reinterpret_cast<uint8_t*>(r.xg + ((size_t)g.s * r.nstep_max + j) * SH::XS) +
+                                                8 * part)
+                                          : reinterpret_cast<uintptr_t>(&nnsp_proj_sink[0]);
+                        asm volatile("" : "+v"(da));   // one address per lane: keep the two stores unconditional
+                        // global (not flat) stores: a flat store also counts in lgkmcnt
+                        typedef __attribute__((address_space(1))) uint64_t gu64;
+                        gu64* dst = reinterpret_cast<gu64*>(da);
                         const uint32_t HS = 0x07050301u, LS = 0x06040200u;
-                        *reinterpret_cast<uint2*>(dst) =
-                            make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, HS),
-                                       __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, HS));
-                        *reinterpret_cast<uint2*>(dst + SH::XS) =
-                            make_uint2(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, LS) ^ 0x80808080u,
-                                       __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, LS) ^ 0x80808080u);
+                        auto u64 = [](uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); };
+                        dst[0] = u64(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, HS),
+                                     __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, HS));
+                        dst[SH::XS / 8] = u64(__builtin_amdgcn_perm((uint32_t)v.y, (uint32_t)v.x, LS) ^ 0x80808080u,
+                                              __builtin_amdgcn_perm((uint32_t)v.w, (uint32_t)v.z, LS) ^ 0x80808080u);
                     }
                 }
+                stored = true;
                 PCLK(3);
             }
-            mine = unpack(mine_n);
-            mine_n = mine_nn;
+            mine = nxt;
             have = have_n;
-            cb ^= 1;
-        }
+        };
+        for (; tile < ntiles; tile += tstride, ++it) tile_step(it & 1);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
     Seg mine_n = seg_from(list_at(tile));
@@ -985,9 +1103,15 @@ struct PipeCfg {
     static constexpr int WPG = NWV * TPW;                    // waves per workgroup
     // waves per SIMD the register budget must allow: two workgroups per CU
     // when a workgroup has <= 8 waves (VAD: <= 128 VGPRs), else one
-    static constexpr int MINW = WPG <= 8 ? 2 * ((WPG + 3) / 4) : (WPG + 3) / 4;
+#ifndef PIPE_SMALL_WG_PER_CU
+#define PIPE_SMALL_WG_PER_CU 2
+#endif
+    static constexpr int MINW = WPG <= 8 ? PIPE_SMALL_WG_PER_CU * ((WPG + 3) / 4) : (WPG + 3) / 4;
     static_assert(WPG <= 16, "recur_pipe_kernel: at most 4 waves per SIMD");
 };
+
+// tiles one workgroup can run back to back through its pipeline (FastRun.tseq)
+#define PIPE_KT 4
 
 template <class SH>
 struct alignas(16) PipeTile {
@@ -997,27 +1121,56 @@ struct alignas(16) PipeTile {
     int16_t a2[2][16][RS];
     int16_t a3[2][16][RS];
     int16_t a4[2][16][RS];    // stage 3 -> 4: int32 logits
+    int16_t hs[16][RS];       // h at the start of a tile (its LSTM step 0 reads it)
     int32_t c[16][CW];
-    int32_t phase[16];
-    int32_t nst[16];          // NN steps of each stream's segment
-    int32_t beg[16];          // segment start frame
-    int32_t end[16];          // segment end frame (exclusive)
-    int32_t cut[16];          // fused control: frame that reset the net (-1: none)
+    // the workgroup's tiles, in pipeline order
+    int4 ti[PIPE_KT][16];     // per stream: {stream, segment begin, end (exclusive), phase | valid << 1}
+    int4 ps[PIPE_KT][16][2];  // PostState (32 bytes) as two 16-byte words
+    CascState cst[PIPE_KT][16];
+    int32_t fresh[PIPE_KT][16];
+    int32_t cut[PIPE_KT][16]; // fused control: frame that reset the net (-1: none)
+    int32_t pbt[PIPE_KT][16]; // frame b of a stream starting at NN phase 1 (no NN, trigger carried), -1: none
+    int2 pb[PIPE_KT][16];     // its outputs: trigger | outputs[0] << 16, outputs[1] | outputs[2] << 16
+    int32_t off[8];           // first pipeline step of tiles 1..3 (0x7fffffff past the last), [4]: steps in all
     // the post wave's frame outputs of one step, stored to HBM by another wave
     // one iteration later (double-buffered by iteration parity): frame t,
-    // which of t / t + 1 to write (bits 0 / 1), trigger, outputs[3]
+    // which of t / t + 1 to write (bits 0 / 1), stream, trigger, outputs[3]
     int32_t pt[2][16];
     int32_t pw[2][16];
+    int32_t psid[2][16];
     int16_t po[2][16][4];
 };
+static_assert(PIPE_KT == 4, "the post wave describes one tile per 16 lanes");
 
 //
-// Fused control (cascade, ca.st non-NULL): the stage-3 wave also runs the
+// Fused control (cascade, ca.st non-NULL): the post wave also runs the
 // controller (nnCntrlClass_exec) frame by frame as the triggers come out.  At
 // the frame that resets the net the stream's segment ends: later frames are
-// neither post-processed nor written, the epilogue stores the reset state
+// neither post-processed nor written, the tile's end stores the reset state
 // (NNSPClass_reset) instead of the carried one, and the stream is listed for
 // its next net -- what casc_control_kernel does after the kernel otherwise.
+//
+// Several tiles per workgroup (FastRun.tseq, <= PIPE_KT: consecutive 16-entry
+// blocks of the stream list) run back to back through ONE pipeline: tile k+1's
+// LSTM step 0 follows tile k's last step in the next iteration, while the tail
+// stages still drain tile k.  A short segment (a cascade round of 16 frames is
+// 8 NN steps) otherwise paid the pipeline's fill and drain -- 4 of every 12
+// iterations -- and the weight staging once per tile.  Hand-over at a tile
+// boundary:
+//   * h: the LSTM waves fetch the next tile's h and c (their own units) at a
+//     tile's step 0; h goes to R.hs at step 1 (step 0 of the next tile reads
+//     it; step 0 of this one already has), c stays in registers;
+//   * the final h, c of a tile: stored to HBM by the LSTM waves at its last
+//     step; for a stream whose net was reset (known to the post wave 4
+//     iterations later) the FC waves overwrite them with the zero state when
+//     they roll the tile's feature context.  The LSTM waves' wait for the x
+//     rows they load at the next step (vector memory completes in order) has
+//     completed those stores before then;
+//   * post-processing and controller state: per tile in LDS (loaded once for
+//     all tiles at the start), the post wave switches at the tile's first step
+//     and stores the tile's state and bookkeeping at its last.
+// Every tile but a workgroup's only one runs at least 2 steps (the hand-overs
+// above use a tile's step 1), and every tile at least 1.
 template <class SH, bool ACC32>
 __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
                                                                                             CascArgs ca) {
@@ -1026,6 +1179,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     using PT = PipeTile<SH>;
     constexpr int RGP = CF::LW, RPW = CF::RPW, RS = PT::RS;
     constexpr int N = SH::NW, nrt = SH::NRT, nkt_r = SH::NKR;
+    static_assert(CF::TPW == 1, "recur_pipe_kernel: one pipeline per workgroup");
     // the FC stages store their padding rows too (fc_layer<..., PAD>): the
     // rows must fit a stage buffer's row (int32 logits: two int16 each)
     static_assert(16 * SH::R1 <= RS && 16 * SH::R2 <= RS && 32 * SH::R3 <= RS, "padded FC rows exceed RS");
@@ -1034,10 +1188,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // does; nothing reads or appends to it during this round)
     if (ctl && blockIdx.x == 0 && threadIdx.x < 6) ca.counts_clear[threadIdx.x] = 0;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
-    constexpr int TPW = CF::TPW, TD = 64 * CF::NWV;   // tiles per workgroup, threads per tile
-    if ((int)blockIdx.x * TPW * 16 >= nrow) return;
-    // the workgroup's tiles share the staged weights and tables; everything
-    // else below is per tile (tid / TD instead of threadIdx / blockDim)
+    const int tseq = r.tseq;   // 1..PIPE_KT (host)
+    const int row0 = (int)blockIdx.x * tseq * 16;   // the workgroup's first list entry
+    if (row0 >= nrow) return;
+    const int nk = min(tseq, (nrow - row0 + 15) / 16);   // its tiles
     // development probe (NNSP_RECUR_CLOCKS, the cascade's round 0 / a batch):
     // per workgroup, wall clock (100 MHz) at the start, after staging and at
     // the end, and where it ran (nnsp_hw_where)
@@ -1045,35 +1199,24 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                          ? r.dbg_clk + NNSP_DCLK_RECUR + 4 * blockIdx.x
                          : nullptr;
     if (wgc) wgc[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    const int sub = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) / CF::NWV;
-    const int tid = (int)threadIdx.x - sub * TD;
-    const int i0 = ((int)blockIdx.x * TPW + sub) * 16;   // tile = 16 consecutive entries of the stream list
+    constexpr int TD = 64 * CF::NWV;
+    const int tid = (int)threadIdx.x;
     uint8_t* W = smem;
     int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
-    PT* RT = reinterpret_cast<PT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
-    PT& R = RT[sub];
+    PT& R = *reinterpret_cast<PT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
-    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
+    for (int i = tid; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
     if (wgc) wgc[1] = (long long)__builtin_amdgcn_s_memrealtime();
-    const int lane = threadIdx.x & 63;
-    const int g = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - sub * CF::NWV;   // < RGP: LSTM wave; then stages
+    const int lane = tid & 63;
+    const int g = __builtin_amdgcn_readfirstlane(tid >> 6);   // < RGP: LSTM wave; then stages
     const int sc = lane & 15, q = lane >> 4;
     auto sid = [&](int i) { return r.list ? r.list[i] : i; };
-    const bool valid = i0 + sc < nrow;
-    const int s = valid ? sid(i0 + sc) : 0;
     const NnLayer& LL = img.L[r.li];
     // compiled shapes have xs_sh == 0 (net_shape): the input and recurrent
     // halves of a gate share one MFMA accumulator
     const int rsh = LL.out_sh < 0 ? -LL.out_sh : 0, lsh = LL.out_sh > 0 ? LL.out_sh : 0;
-    for (int idx = tid; idx < 16 * N; idx += TD) {
-        const int st = idx / N, u = idx - st * N;
-        const bool ok = i0 + st < nrow;
-        const int gs = ok ? sid(i0 + st) : 0;
-        R.h[0][st][u] = ok ? r.h[(size_t)gs * NN_MAX_W + u] : (int16_t)0;
-        R.c[st][u] = ok ? r.c[(size_t)gs * NN_MAX_W + u] : 0;
-    }
     const int T = r.T;
     constexpr int SPL = CF::SPLIT;
     const bool post_w = g == RGP + 2 + SPL;   // the post-processing wave
@@ -1082,36 +1225,89 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // long as its LSTM step, splits them over its two FC waves (frame t / t + 1)
     const bool store_w = SPL ? g == RGP + 2 : (g == RGP || g == RGP + 1);
     const int store_bits = SPL ? 3 : (g == RGP ? 1 : 2);
-    PostState ps = {};
-    CascState cst = {};   // fused control: the stream's controller state
-    int cut = -1;
-    if (post_w && lane < 16) {
-        if (ctl && valid) cst = ca.st[s];
-        const int b = valid && r.seg_begin ? r.seg_begin[s] : 0;
+    // ---- the tiles' descriptors (post wave, lane = 16 x tile + stream) and
+    //      their pipeline steps: the most NN steps of the tile's streams
+    if (post_w) {
+        const int k = lane >> 4;
+        const int i = row0 + 16 * k + sc;
+        const bool ok = k < nk && i < nrow;
+        const int s = ok ? sid(i) : 0;
+        const int b = ok && r.seg_begin ? r.seg_begin[s] : 0;
         const int e = r.seg_len > 0 ? min(T, b + r.seg_len) : T;
-        if (valid) ps = reinterpret_cast<const PostState*>(r.post)[s];
-        const int ph = valid ? 1 - ps.slides : 0;
-        R.phase[lane] = ph;
-        R.beg[lane] = b;
-        R.end[lane] = e;
-        R.nst[lane] = valid && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
-        R.pw[0][lane] = R.pw[1][lane] = 0;
+        // the post state as two 16-byte words (a PostState copy went
+        // through scratch: 2-byte members at odd offsets)
+        int4 p0 = make_int4(0, 0, 0, 0), p1 = p0;
+        if (ok) {
+            p0 = reinterpret_cast<const int4*>(r.post)[2 * s];
+            p1 = reinterpret_cast<const int4*>(r.post)[2 * s + 1];
+        }
+        const int ph = ok ? 1 - (int)(int16_t)(p0.x & 0xffff) : 0;   // 1 - slides
+        int m = ok && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
+        R.ti[k][sc] = make_int4(s, b, e, ph | (ok ? 2 : 0));
+        R.ps[k][sc][0] = p0;
+        R.ps[k][sc][1] = p1;
+        if (lane < 16) R.pw[0][lane] = R.pw[1][lane] = 0;   // no frame outputs before the first post step
+        R.pbt[k][sc] = -1;
+        // fresh[] (frames since the net's reset: the cold front end's frames)
+        // as at the kernel start -- the feature-context roll reads through it
+        // after the bookkeeping has overwritten it for the next net
+        R.fresh[k][sc] = ok && r.fs.nring ? (int)r.fs.fresh[s] : 2;
+        if (ctl) {
+            CascState cs = {};
+            if (ok) cs = ca.st[s];
+            R.cst[k][sc] = cs;
+        }
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+        m = max(m, nk > 1 ? 2 : 1);
+        const int m1 = __shfl(m, 16), m2 = __shfl(m, 32), m3 = __shfl(m, 48);
+        if (lane == 0) {
+            const int o1 = m, o2 = o1 + m1, o3 = o2 + m2, o4 = o3 + m3;
+            R.off[1] = nk > 1 ? o1 : 0x7fffffff;
+            R.off[2] = nk > 2 ? o2 : 0x7fffffff;
+            R.off[3] = nk > 3 ? o3 : 0x7fffffff;
+            R.off[4] = nk == 1 ? o1 : (nk == 2 ? o2 : (nk == 3 ? o3 : o4));
+        }
+    }
+    // ---- tile 0's h and c (LSTM waves: the lane's own units); later tiles'
+    //      are fetched during the previous tile
+    int16_t h_nx[RPW];
+    int32_t c_nx[RPW];
+    auto fetch_state = [&](int s_, bool ok) {
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int u = 4 * (g + RGP * k) + q;
+            h_nx[k] = 0;
+            c_nx[k] = 0;
+            if (g + RGP * k < nrt && u < N) {
+                const size_t o = (size_t)(ok ? s_ : 0) * NN_MAX_W + u;
+                const int16_t hv = r.h[o];
+                const int32_t cv = r.c[o];
+                h_nx[k] = ok ? hv : (int16_t)0;
+                c_nx[k] = ok ? cv : 0;
+            }
+        }
+    };
+    auto put_hs = [&]() {
+#pragma unroll
+        for (int k = 0; k < RPW; ++k) {
+            const int u = 4 * (g + RGP * k) + q;
+            if (g + RGP * k < nrt && u < N) R.hs[sc][u] = h_nx[k];
+        }
+    };
+    if (g < RGP) {
+        const bool ok = row0 + sc < nrow;
+        fetch_state(ok ? sid(row0 + sc) : 0, ok);
+        put_hs();
     }
     __syncthreads();
-    const int phase = R.phase[sc];
-    const int b = R.beg[sc];
-    const int e = R.end[sc];   // segment: frames b..e-1
-    int nsteps = 0, nloop = 0;   // this tile's NN steps; the workgroup's (the barriers' trip count)
-#pragma unroll
-    for (int i = 0; i < 16; ++i) nsteps = max(nsteps, R.nst[i]);
-#pragma unroll
-    for (int k = 0; k < TPW; ++k)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) nloop = max(nloop, RT[k].nst[i]);
-    if (post_w && lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
-        put_frame(r, s, T, b, ps);
-        if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
-    }
+    const int off1 = __builtin_amdgcn_readfirstlane(R.off[1]);
+    const int off2 = __builtin_amdgcn_readfirstlane(R.off[2]);
+    const int off3 = __builtin_amdgcn_readfirstlane(R.off[3]);
+    const int total = __builtin_amdgcn_readfirstlane(R.off[4]);   // pipeline steps of all tiles
+    auto tile_of = [&](int j) { return (j >= off1 ? 1 : 0) + (j >= off2 ? 1 : 0) + (j >= off3 ? 1 : 0); };
+    auto off_of = [&](int k) { return k == 0 ? 0 : (k == 1 ? off1 : (k == 2 ? off2 : off3)); };
+    auto end_of = [&](int k) { return k + 1 < nk ? off_of(k + 1) : total; };
     // staged region: the LSTM's input fragments, then its recurrent ones, then the FC tail
     const uint8_t* Ax = W;
     const uint8_t* Ar = W + (LL.ar_off - LL.a_off);
@@ -1125,10 +1321,13 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // The loads land in xr untouched (lanes past the row read column 0 of it)
     // and x_half zeroes those lanes: any use of a load result right after it
     // (a select, a copy) made the wave wait the full load latency every step.
-    auto load_x = [&](int jj) {   // split x of step jj for the lane's stream (B fragments: high, low bytes)
-        const bool ok = valid && b + 2 * jj + phase < e;
+    auto load_x = [&](int jj) {   // split x of pipeline step jj for the lane's stream (B fragments: high, low bytes)
+        const int kx = tile_of(jj);
+        const int jl = jj - off_of(kx);
+        const int4 d = R.ti[kx][sc];
+        const bool ok = (d.w & 2) && d.y + 2 * jl + (d.w & 1) < d.z;
         const uint8_t* src =
-            reinterpret_cast<const uint8_t*>(r.xg + ((size_t)(ok ? s : 0) * r.nstep_max + (ok ? jj : 0)) * XS);
+            reinterpret_cast<const uint8_t*>(r.xg + ((size_t)(ok ? d.x : 0) * r.nstep_max + (ok ? jl : 0)) * XS);
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
             const int k0 = 64 * kt + 16 * q;
@@ -1169,7 +1368,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 }
         }
     };
-    if (g < RGP) {   // (past the segment: row 0 of xg, unused)
+    if (g < RGP) {   // (past a segment: row 0 of xg, unused)
         load_x(0);
         x_half();
         load_x(1);
@@ -1181,23 +1380,30 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             const int fl = R.pw[p][lane] & store_bits;
             if (fl) {
                 const int ft = R.pt[p][lane];
+                const int fs_ = R.psid[p][lane];
                 const int16_t* o = R.po[p][lane];
-                if (fl & 1) put_out(r, s, T, ft, o[0], o[1], o[2], o[3]);
-                if (fl & 2) put_out(r, s, T, ft + 1, o[0], o[1], o[2], o[3]);
+                if (fl & 1) put_out(r, fs_, T, ft, o[0], o[1], o[2], o[3]);
+                if (fl & 2) put_out(r, fs_, T, ft + 1, o[0], o[1], o[2], o[3]);
             }
         }
     };
+    // the post wave's state: the current tile's streams (lanes: sc)
+    PostState ps = {};
+    CascState cst = {};   // fused control: the stream's controller state
+    int cut = -1;
+    int s = 0, b = 0, e = 0, phase = 0;
+    bool valid = false;
     const NnLayer& L2 = img.L[r.li + 1];
     const NnLayer& L3 = img.L[r.li + 2];
     const NnLayer& L4 = img.L[r.li + 3];
     // development probe (NNSP_RECUR_CLOCKS): s_memtime at the start and end of each
-    // iteration's work of LSTM wave 0 and the three stage waves, tile 0
+    // iteration's work of LSTM wave 0 and the three stage waves, workgroup 0
     // (RECUR_CLK_WAVE: which LSTM wave records into slots 0-1; development)
 #ifndef RECUR_CLK_WAVE
 #define RECUR_CLK_WAVE 0
 #endif
     constexpr int CLKW = RECUR_CLK_WAVE < RGP ? RECUR_CLK_WAVE : 0;
-    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && sub == 0 && lane == 0 && (g == CLKW || g >= RGP))
+    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 && (g == CLKW || g >= RGP))
                          ? r.dbg_clk + 2 * (g == CLKW ? 0 : g - RGP + 1)
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the
@@ -1214,12 +1420,17 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         constexpr int role = decltype(RL)::value;   // 0 LSTM, 1-3 FC stages 1-3, 4 post
         if (clk && j < 64) clk[j * 16] = (long long)__builtin_amdgcn_s_memtime();
         if constexpr (role == 0) {
-            if (j < nsteps) {
-                // ---- LSTM step j: row tile = 4 units x gates i, j, f, o
-                const int t = b + 2 * j + phase;
-                const bool active = valid && t < e;
+            if (j < total) {
+                // ---- LSTM step j (the tile's step jl): row tile = 4 units x gates i, j, f, o
+                const int tk = tile_of(j);
+                const int jl = j - off_of(tk);
+                const int4 d = R.ti[tk][sc];
+                const int t = d.y + 2 * jl + (d.w & 1);
+                const bool active = (d.w & 2) && t < d.z;
+                const bool first = jl == 0;   // h from R.hs, c from the fetch registers
+                const int16_t* hsrc = first ? &R.hs[0][0] : &R.h[cur][0][0];
                 v4i bh[nkt_r], bl[nkt_r];
-                load_b<nkt_r>(&R.h[cur][0][0], RS, nkt_r, lane, bh, bl);
+                load_b<nkt_r>(hsrc, RS, nkt_r, lane, bh, bl);
                 // every LDS load of the step (A fragments, epilogue constants,
                 // cell state, the previous h kept for inactive streams) before
                 // the first store: loads cannot be moved across LDS stores
@@ -1231,14 +1442,18 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 for (int k = 0; k < RPW; ++k) {
                     const int rt = g + RGP * k;
                     const int u = 4 * rt + q;
+                    c_old[k] = 0;
+                    h_old[k] = 0;
                     if (rt < nrt) {
 #pragma unroll
                         for (int kt = 0; kt < nkt_r; ++kt)
                             w[k][kt] = *reinterpret_cast<const v4i*>(Ar + (size_t)(rt * nkt_r + kt) * 1024 + 16 * lane);
 #pragma unroll
                         for (int i = 0; i < 4; ++i) cst[k][i] = CST_IN_ACC ? 0 : ep_cst<ACC32>(epl[16 * rt + i]);
-                        c_old[k] = u < N ? R.c[sc][u] : 0;
-                        h_old[k] = u < N ? R.h[cur][sc][u] : (int16_t)0;
+                        if (u < N) {
+                            c_old[k] = first ? c_nx[k] : R.c[sc][u];
+                            h_old[k] = hsrc[sc * RS + u];
+                        }
                     }
                 }
                 v4i hh[RPW], hl[RPW];
@@ -1263,6 +1478,11 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 x_half();
                 LCLK(3);
                 load_x(j + 2);
+                // the next tile's h and c: fetched now, h into R.hs at step 1
+                if (first && tk + 1 < nk) {
+                    const int4 dn = R.ti[tk + 1][sc];
+                    fetch_state(dn.x, (dn.w & 2) != 0);
+                }
                 LCLK(4);
                 int32_t c_new[RPW];
                 int16_t hv[RPW];
@@ -1306,41 +1526,78 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 else
                     gates(std::false_type{});
                 LCLK(1);
+                // a tile's last step with another tile behind it: its final
+                // state goes to HBM from here (the last tile's: after the loop)
+                const bool hand = tk + 1 < nk && j + 1 == off_of(tk + 1) && (d.w & 2);
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
                     const int rt = g + RGP * k;
                     const int u = 4 * rt + q;
                     if (rt < nrt && u < N) {
-                        if (active) R.c[sc][u] = c_new[k];
-                        R.h[cur ^ 1][sc][u] = active ? hv[k] : h_old[k];   // h after all groups (T6)
+                        const int32_t cv = active ? c_new[k] : c_old[k];
+                        const int16_t hn = active ? hv[k] : h_old[k];
+                        R.c[sc][u] = cv;
+                        R.h[cur ^ 1][sc][u] = hn;   // h after all groups (T6)
+                        if (jl == 1) R.hs[sc][u] = h_nx[k];
+                        if (hand) {
+                            r.h[(size_t)d.x * NN_MAX_W + u] = hn;
+                            r.c[(size_t)d.x * NN_MAX_W + u] = cv;
+                        }
                     }
                 }
                 LCLK(2);
             }
-        } else if constexpr (role == 1) {   // stage 1: step j-1
-            if (j >= 1 && j - 1 < nsteps)
-                fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
-                    L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
-                    RS, tt, lane);
-            if (!SPL) flush(cur ^ 1);
-        } else if constexpr (role == 2) {   // stage 2: step j-2
-            if (j >= 2 && j - 2 < nsteps)
-                fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
-                    L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
-                    &R.a3[cur][0][0], RS, tt, lane);
-            if (!SPL) flush(cur ^ 1);
-        } else if constexpr (role == 3) {   // stage 3 (split): step j-3
-            if (j >= 3 && j - 3 < nsteps)
-                fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
-                    L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
-                    &R.a4[cur][0][0], RS, tt, lane);
-            flush(cur ^ 1);   // the post wave's outputs of the previous iteration
-        } else {   // post: step j-3-SPL
+        } else if constexpr (role <= 3) {
+            if constexpr (role == 1) {   // stage 1: step j-1
+                if (j >= 1 && j - 1 < total)
+                    fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
+                        L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
+                        RS, tt, lane);
+                if (!SPL) flush(cur ^ 1);
+            } else if constexpr (role == 2) {   // stage 2: step j-2
+                if (j >= 2 && j - 2 < total)
+                    fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
+                        L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
+                        &R.a3[cur][0][0], RS, tt, lane);
+                if (!SPL) flush(cur ^ 1);
+            } else {   // stage 3 (split): step j-3
+                if (j >= 3 && j - 3 < total)
+                    fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
+                        L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
+                        &R.a4[cur][0][0], RS, tt, lane);
+                flush(cur ^ 1);   // the post wave's outputs of the previous iteration
+            }
+        } else {   // post: step jp = j-3-SPL
           int wfl = 0;   // frames of this step to store (bits: t, t + 1)
           int t = 0;
-          if (j >= 3 + SPL && j - 3 - SPL < nsteps) {
-            const int jj = j - 3 - SPL;
-            t = b + 2 * jj + phase;
+          const int jp = j - 3 - SPL;
+          if (jp >= 0 && jp < total) {
+            const int tk = tile_of(jp);
+            const int jl = jp - off_of(tk);
+            if (jl == 0) {   // the tile's streams
+                const int4 d = R.ti[tk][sc];
+                s = d.x;
+                b = d.y;
+                e = d.z;
+                phase = d.w & 1;
+                valid = (d.w & 2) != 0;
+                cut = -1;
+                if (lane < 16) {
+                    const int4 p0 = R.ps[tk][lane][0], p1 = R.ps[tk][lane][1];
+                    static_assert(sizeof(PostState) == 32, "PostState: two 16-byte words");
+                    __builtin_memcpy(&ps, &p0, 16);
+                    __builtin_memcpy(reinterpret_cast<char*>(&ps) + 16, &p1, 16);
+                    if (ctl) cst = R.cst[tk][lane];
+                }
+                if (lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
+                    R.pbt[tk][lane] = b;   // (stored after the loop)
+                    R.pb[tk][lane] =
+                        make_int2((int)((uint32_t)(uint16_t)ps.trigger | ((uint32_t)(uint16_t)ps.outputs[0] << 16)),
+                                  (int)((uint32_t)(uint16_t)ps.outputs[1] | ((uint32_t)(uint16_t)ps.outputs[2] << 16)));
+                    if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
+                }
+            }
+            t = b + 2 * jl + phase;
             const bool active = valid && t < e;
             if (!SPL) {   // the last FC layer on this wave too
                 fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
@@ -1383,9 +1640,26 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
               R.pw[cur][lane] = wfl;
               if (wfl) {
                   R.pt[cur][lane] = t;
+                  R.psid[cur][lane] = s;
                   *reinterpret_cast<int2*>(R.po[cur][lane]) =
                       make_int2((int)((uint32_t)(uint16_t)ps.trigger | ((uint32_t)(uint16_t)ps.outputs[0] << 16)),
                                 (int)((uint32_t)(uint16_t)ps.outputs[1] | ((uint32_t)(uint16_t)ps.outputs[2] << 16)));
+              }
+          }
+          // the tile's last step: its post-processing and controller state
+          // and reset frame to LDS, for the bookkeeping after the loop (in the
+          // loop, its pointers and counters took SGPRs that every role's loop
+          // then spilled to VGPR lanes)
+          if (jp >= 0 && jp < total && lane < 16) {
+              const int tk = tile_of(jp);
+              if (jp + 1 == end_of(tk)) {
+                  R.cut[tk][lane] = valid ? cut : -1;
+                  int4 p0, p1;
+                  __builtin_memcpy(&p0, &ps, 16);
+                  __builtin_memcpy(&p1, reinterpret_cast<const char*>(&ps) + 16, 16);
+                  R.ps[tk][lane][0] = p0;
+                  R.ps[tk][lane][1] = p1;
+                  R.cst[tk][lane] = cst;
               }
           }
         }
@@ -1397,9 +1671,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // values live across it, spilled ~170 SGPRs to VGPR lanes and paid a
     // v_readlane (a VALU issue) per use -- 15-20 % of the kernel's VALU code
     auto run = [&](auto RL) {
-        for (int j = 0; j < nloop + 3 + SPL; j += 2) {
+        for (int j = 0; j < total + 3 + SPL; j += 2) {
             iteration(j, std::integral_constant<int, 0>{}, RL);
-            if (j + 1 < nloop + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{}, RL);
+            if (j + 1 < total + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{}, RL);
         }
     };
     if (g < RGP)
@@ -1414,85 +1688,139 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         run(std::integral_constant<int, 4>{});
 #undef LCLK
     // the last iteration's post outputs (each iteration ends with a barrier)
-    if (store_w) flush((nloop + 2 + SPL) & 1);
-    if (ctl) {
-        if (post_w && lane < 16) R.cut[lane] = valid ? cut : -1;
-        __syncthreads();
+    if (store_w) flush((total + 2 + SPL) & 1);
+    // ---- the tiles' ends, after the loop (inside it, their pointers and
+    //      counters cost every role's loop SGPRs, spilled to VGPR lanes).
+    //      Frame b of the streams that started at NN phase 1 (no NN, the
+    //      trigger carried):
+    for (int idx = tid; idx < 16 * nk; idx += TD) {
+        const int k = idx >> 4, st = idx & 15;
+        const int f = R.pbt[k][st];
+        if (f >= 0) {
+            const int2 o = R.pb[k][st];
+            put_out(r, R.ti[k][st].x, T, f, (int16_t)(o.x & 0xffff), (int16_t)((uint32_t)o.x >> 16),
+                    (int16_t)(o.y & 0xffff), (int16_t)((uint32_t)o.y >> 16));
+        }
     }
-    // ---- state out: LSTM step nsteps-1 wrote h[nsteps & 1]; a stream whose
-    //      net was reset gets the zero state (NeuralNetClass_setDefault)
-    const int hb = nsteps & 1;
+    // LSTM state: the last tile's from LDS (step total-1 wrote h[total & 1]);
+    // the earlier tiles' went out from the LSTM waves at their last step.  A
+    // stream whose net was reset gets the zero state
+    // (NeuralNetClass_setDefault) -- over what the LSTM waves stored: their
+    // wait for the x rows of two steps later completed those stores (vector
+    // memory completes in order)
+    const int tl = nk - 1;
+    const int hb = total & 1;
     for (int idx = tid; idx < 16 * N; idx += TD) {
         const int st = idx / N, u = idx - st * N;
-        if (i0 + st < nrow) {
-            const int gs = sid(i0 + st);
-            const bool rs = ctl && R.cut[st] >= 0;
-            r.h[(size_t)gs * NN_MAX_W + u] = rs ? (int16_t)0 : R.h[hb][st][u];
-            r.c[(size_t)gs * NN_MAX_W + u] = rs ? 0 : R.c[st][u];
+        const int4 d = R.ti[tl][st];
+        if (d.w & 2) {
+            const bool rs = ctl && R.cut[tl][st] >= 0;
+            r.h[(size_t)d.x * NN_MAX_W + u] = rs ? (int16_t)0 : R.h[hb][st][u];
+            r.c[(size_t)d.x * NN_MAX_W + u] = rs ? 0 : R.c[st][u];
         }
     }
-    if (post_w && lane < 16 && valid && b < e) {
-        if (cut >= 0)
-            nnsp::post_reset(ps);
-        else
-            ps.slides = (int16_t)(ps.slides ^ ((e - b) & 1));
-        reinterpret_cast<PostState*>(r.post)[s] = ps;
-    }
-    // ---- feature context (normFeatContext slots 1..5) := last 5 of prev5 ++ feats[b..e):
-    // all of the tile's reads before any write (a stream's old slots feed its new ones).
-    // A reset net (FeatureClass_setDefault): slots 1..4 := the default, slot 5
-    // keeps the feature of the frame that reset it (T4).
-    int4 cv[2];
-    int ci[2];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-        const int idx = tid + TD * k;   // (stream in tile, 16-byte chunk of 5x40)
-        ci[k] = -1;
-        if (idx < 16 * 25 && i0 + idx / 25 < nrow) {
-            const int st = idx / 25, c = idx - st * 25, m = c / 5, part = c - 5 * m;
-            const int L = R.end[st] - R.beg[st];
-            if (L > 0) {
-                const int gs = sid(i0 + st), jx = L + m;
-                const int ct = ctl ? R.cut[st] : -1;
-                if (ct >= 0)
-                    cv[k] = m < 4 ? reinterpret_cast<const int4*>(ca.prev_default[r.net_id])[part]
-                                  : feat8(r.fs, r.feats, gs, T, R.beg[st], ct, part);
+    if (ctl) {
+        constexpr int NH = (2 * N + 15) / 16, NC = (4 * N + 15) / 16;   // 16-byte chunks of the h, c rows
+        for (int idx = tid; idx < (nk - 1) * 16 * (NH + NC); idx += TD) {
+            const int k = idx / (16 * (NH + NC)), rem = idx - k * 16 * (NH + NC);
+            const int st = rem / (NH + NC), ch = rem - st * (NH + NC);
+            const int4 d = R.ti[k][st];
+            if ((d.w & 2) && R.cut[k][st] >= 0) {
+                if (ch < NH)
+                    reinterpret_cast<int4*>(r.h + (size_t)d.x * NN_MAX_W)[ch] = make_int4(0, 0, 0, 0);
                 else
-                    cv[k] = jx < 5 ? *reinterpret_cast<const int4*>(r.prev5 + ((size_t)gs * 5 + jx) * 40 + 8 * part)
-                                   : feat8(r.fs, r.feats, gs, T, R.beg[st], R.beg[st] + jx - 5, part);
-                ci[k] = gs * 25 + c;
+                    reinterpret_cast<int4*>(r.c + (size_t)d.x * NN_MAX_W)[ch - NH] = make_int4(0, 0, 0, 0);
             }
         }
     }
+    // ---- feature context (normFeatContext slots 1..5) := last 5 of prev5 ++
+    //      feats[b..e); a reset net (FeatureClass_setDefault): slots 1..4 :=
+    //      the default, slot 5 := the feature of the frame that reset it (T4).
+    //      All reads before any write (a stream's old slots feed its new
+    //      ones); every lane loads, through a selected address (selected
+    //      values went through scratch)
+    auto ctx_src = [&](int idx, int& ci) -> const int4* {   // idx: (tile, stream, 16-byte chunk of 5x40)
+        ci = -1;
+        const int4* p = &nnsp_proj_zero16;
+        const int k = idx / 400, rem = idx - 400 * k;
+        if (k < nk) {
+            const int st = rem / 25, c = rem - st * 25, m = c / 5, part = c - 5 * m;
+            const int4 d = R.ti[k][st];
+            const int L = d.z - d.y;
+            if ((d.w & 2) && L > 0) {
+                const int jx = L + m;
+                const int ct = ctl ? R.cut[k][st] : -1;
+                const int fr = R.fresh[k][st];
+                if (ct >= 0)
+                    p = m < 4 ? reinterpret_cast<const int4*>(ca.prev_default[r.net_id]) + part
+                              : reinterpret_cast<const int4*>(feat8_ptr<true>(r.fs, r.feats, d.x, T, d.y, ct, part, fr));
+                else
+                    p = jx < 5 ? reinterpret_cast<const int4*>(r.prev5 + ((size_t)d.x * 5 + jx) * 40 + 8 * part)
+                               : reinterpret_cast<const int4*>(
+                                     feat8_ptr<true>(r.fs, r.feats, d.x, T, d.y, d.y + jx - 5, part, fr));
+                ci = d.x * 25 + c;
+            }
+        }
+        return p;
+    };
+    constexpr int NCK = (PIPE_KT * 400 + TD - 1) / TD;   // context chunks per thread (named: an array went to scratch)
+    static_assert(NCK >= 2 && NCK <= 4, "recur_pipe_kernel: 2-4 context chunks per thread");
+    int ci0, ci1, ci2 = -1, ci3 = -1;
+    const int4 cv0 = *ctx_src(tid, ci0);
+    const int4 cv1 = *ctx_src(tid + TD, ci1);
+    int4 cv2 = make_int4(0, 0, 0, 0), cv3 = cv2;
+    if constexpr (NCK > 2) cv2 = *ctx_src(tid + 2 * TD, ci2);
+    if constexpr (NCK > 3) cv3 = *ctx_src(tid + 3 * TD, ci3);
     __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-        if (ci[k] >= 0) reinterpret_cast<int4*>(r.prev5)[ci[k]] = cv[k];
+    int4* p5 = reinterpret_cast<int4*>(r.prev5);
+    if (ci0 >= 0) p5[ci0] = cv0;
+    if (ci1 >= 0) p5[ci1] = cv1;
+    if (ci2 >= 0) p5[ci2] = cv2;
+    if (ci3 >= 0) p5[ci3] = cv3;
+    // ---- post-processing state and (fused control) the controller's
+    //      bookkeeping, casc_control_kernel's tail: frames since the reset of
+    //      the net the stream runs next, position, next segment start, next
+    //      round's lists.  Post wave, lane = 16 x tile + stream.
+    if (post_w) {
+        const int k = lane >> 4;
+        const int4 d = R.ti[k][sc];
+        const bool ok = k < nk && (d.w & 2);
+        const int sb = d.x, bb = d.y, ee = d.z, ct = R.cut[k][sc];
+        if (ok && bb < ee) {
+            PostState pz;
+            const int4 p0 = R.ps[k][sc][0], p1 = R.ps[k][sc][1];
+            __builtin_memcpy(&pz, &p0, 16);
+            __builtin_memcpy(reinterpret_cast<char*>(&pz) + 16, &p1, 16);
+            if (ct >= 0)
+                nnsp::post_reset(pz);
+            else
+                pz.slides = (int16_t)(pz.slides ^ ((ee - bb) & 1));
+            __builtin_memcpy(reinterpret_cast<int4*>(r.post) + 2 * sb, &pz, 32);
+        }
+        if (ctl) {
+            bool want = false;
+            int n_next = 0, b_next = T, fr_next = 2;
+            if (ok) {
+                const CascState cz = R.cst[k][sc];
+                fr_next = ct >= 0 ? 0 : min(2, R.fresh[k][sc] + (ee - bb));
+                b_next = ct >= 0 ? ct + 1 : ee;
+                ca.fresh[sb] = (int8_t)fr_next;
+                ca.st[sb] = cz;
+                ca.seg_begin[sb] = b_next;
+                if (b_next < T) {
+                    want = true;
+                    n_next = nnsp::seq_at(ca, cz.pos);
+                }
+            }
+            nnsp::list_next(ca, n_next, sb, want, fr_next);
+            if (ca.last_round && __ballot(want) && lane == 0) atomicMax(ca.last_round, ca.round + 1);
+            nnsp::add_frames(ca, n_next, nnsp::next_frames(ca, T, want, b_next));
+            nnsp::count_cuts(ca, ok && ct >= 0);
+        }
+    }
     if (wgc) {
         wgc[2] = (long long)__builtin_amdgcn_s_memrealtime();
-        wgc[3] = (long long)nsteps | (nnsp_hw_where() << 32);
-    }
-    if (ctl && post_w) {
-        // ---- controller bookkeeping (casc_control_kernel's tail): frames since
-        //      the reset of the net the stream runs next (its feat8 reads above
-        //      are done), position, next segment start, next round's lists
-        bool want = false;
-        int n_next = 0, b_next = T, fr_next = 2;
-        if (lane < 16 && valid) {
-            fr_next = cut >= 0 ? 0 : min(2, (int)ca.fresh[s] + (e - b));
-            b_next = cut >= 0 ? cut + 1 : e;
-            ca.fresh[s] = (int8_t)fr_next;
-            ca.st[s] = cst;
-            ca.seg_begin[s] = b_next;
-            if (b_next < T) {
-                want = true;
-                n_next = nnsp::seq_at(ca, cst.pos);
-            }
-        }
-        nnsp::list_next(ca, n_next, s, want, fr_next);
-        if (ca.last_round && __ballot(want) && lane == 0) atomicMax(ca.last_round, ca.round + 1);
-        nnsp::add_frames(ca, n_next, nnsp::next_frames(ca, T, want, b_next));
-        nnsp::count_cuts(ca, lane < 16 && valid && cut >= 0);
+        wgc[3] = (long long)total | (nnsp_hw_where() << 32);
     }
 }
 
@@ -1565,22 +1893,38 @@ int launch(const void* fn, dim3 grid, dim3 blk, size_t lds, void* stream, const 
 
 extern "C" {
 
-size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape) {
+}  // extern "C"
+
+namespace {
+template <class SH>
+size_t proj_wave_bytes(int gpt) {
+    return gpt == 4 ? sizeof(ProjWave<SH, 4>) : (gpt == 2 ? sizeof(ProjWave<SH, 2>) : sizeof(ProjWave<SH, 1>));
+}
+// gpt: streams per proj tile of the launch (the ProjWave layout depends on it)
+size_t fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape, int gpt) {
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
     const size_t base = (size_t)a_bytes + TT_BYTES + ep_bytes(ep_rows);
     size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
     switch (shape) {   // compiled shapes: recur runs one pipelined tile per workgroup
-        case NN_SHAPE_VAD: pw = sizeof(ProjWave<ShapeVad>); rt = sizeof(PipeTile<ShapeVad>); units = which ? PipeCfg<ShapeVad>::TPW : units; break;
-        case NN_SHAPE_KWS: pw = sizeof(ProjWave<ShapeKws>); rt = sizeof(PipeTile<ShapeKws>); units = which ? PipeCfg<ShapeKws>::TPW : units; break;
-        case NN_SHAPE_S2I: pw = sizeof(ProjWave<ShapeS2i>); rt = sizeof(PipeTile<ShapeS2i>); units = which ? PipeCfg<ShapeS2i>::TPW : units; break;
+        case NN_SHAPE_VAD: pw = proj_wave_bytes<ShapeVad>(gpt); rt = sizeof(PipeTile<ShapeVad>); units = which ? PipeCfg<ShapeVad>::TPW : units; break;
+        case NN_SHAPE_KWS: pw = proj_wave_bytes<ShapeKws>(gpt); rt = sizeof(PipeTile<ShapeKws>); units = which ? PipeCfg<ShapeKws>::TPW : units; break;
+        case NN_SHAPE_S2I: pw = proj_wave_bytes<ShapeS2i>(gpt); rt = sizeof(PipeTile<ShapeS2i>); units = which ? PipeCfg<ShapeS2i>::TPW : units; break;
         default: break;
     }
     return base + (size_t)units * (which == 0 ? pw : rt);
 }
+}  // namespace
+
+extern "C" {
+
+// the planner's size: proj with one stream per tile (whole-chunk segments)
+size_t nnspk_fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape) {
+    return fast_lds_bytes(which, a_bytes, units, ep_rows, shape, 1);
+}
 
 int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, int waves, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(0, r->a_lds_bytes, waves, r->ep_n, r->shape);
     if (r->shape != NN_SHAPE_GENERIC && r->gpt != 1 && r->gpt != 2 && r->gpt != 4) return (int)hipErrorInvalidValue;
+    const size_t lds = fast_lds_bytes(0, r->a_lds_bytes, waves, r->ep_n, r->shape, r->gpt);
     return launch(pick_proj(r->shape, img->acc32 || r->ep32, r->gpt), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
 }
 
@@ -1593,10 +1937,11 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const Casc
     if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb)) {
         CascArgs none;
         memset(&none, 0, sizeof none);
-        const int tpw = r->shape == NN_SHAPE_VAD ? PipeCfg<ShapeVad>::TPW
-                                                 : (r->shape == NN_SHAPE_KWS ? PipeCfg<ShapeKws>::TPW : PipeCfg<ShapeS2i>::TPW);
+        FastRun rr = *r;   // tiles per workgroup, run back to back through its pipeline
+        rr.tseq = rr.tseq < 1 ? 1 : (rr.tseq > PIPE_KT ? PIPE_KT : rr.tseq);
         const int tiles = (nrow + 15) / 16;
-        return launch(fn, dim3((tiles + tpw - 1) / tpw), dim3(64 * waves), lds, stream, img, r, ctl ? ctl : &none);
+        return launch(fn, dim3((tiles + rr.tseq - 1) / rr.tseq), dim3(64 * waves), lds, stream, img, &rr,
+                      ctl ? ctl : &none);
     }
     if (ctl) return (int)hipErrorInvalidValue;   // fused control needs the pipelined kernel
     const int tiles = (nrow + 15) / 16;

@@ -160,7 +160,8 @@ typedef struct {
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
 typedef struct {
     int32_t S, T, li, nstep_max;
-    int32_t a_lds_bytes, pad;
+    int32_t a_lds_bytes;
+    int32_t tseq;             /* compiled shapes' recur: 16-stream tiles per workgroup, run back to back (1..4) */
     int64_t a_off;            /* byte offset in NnImage.A of the LDS-staged region */
     const int16_t *feats;     /* [S][T][40] */
     int16_t *prev5;           /* [S][5][40]; recur rolls it forward over the segment */

@@ -216,3 +216,17 @@ def test_stats_right_after_exec_device():
             gc.net_stats(n)
     gc.sync()
     gc.close()
+
+
+@pytest.mark.parametrize("tseq", ["2", "3"])
+@pytest.mark.parametrize("window", [0, 16])
+def test_cascade_recur_tiles_back_to_back(tseq, window, monkeypatch):
+    """Several recur tiles per workgroup through one pipeline (the default for
+    short windows): at a tile boundary the next tile's LSTM state, the finished
+    tile's state (zero for a stream whose net was reset), its feature context
+    and the controller's bookkeeping all change hands mid-pipeline."""
+    monkeypatch.setenv("NNSP_RECUR_TSEQ", tseq)
+    S, chunks = 150, [100, 37, 1, 63]
+    oc, gc, _ = _build(TH["lively"], S, max(chunks), True, (1, 2, 0), 80, 60, 80, 50)
+    gc.set_window(window)
+    assert _check(oc, gc, _pcm(S, sum(chunks), 21), chunks) > 50

@@ -93,3 +93,14 @@ def test_reset_mask(name):
         orc.reset_streams(st, mask)
         eng.reset(mask)
     eng.close()
+
+
+@pytest.mark.parametrize("name", NETS)
+@pytest.mark.parametrize("tseq", ["1", "3", "4"])
+def test_recur_tiles_back_to_back(name, tseq, monkeypatch):
+    # several 16-stream tiles per recur workgroup through one pipeline
+    # (FastRun.tseq): 75 streams = 5 tiles, so tseq 3 leaves a workgroup of 3
+    # tiles and one of 2 (the last one partial); chunks of 40, 9, 2 and 13
+    # frames give tiles of 20, 5, 1 and 7 NN steps (and padded 1-step tiles)
+    monkeypatch.setenv("NNSP_RECUR_TSEQ", tseq)
+    _compare(name, True, S=75, chunks=[40, 9, 2, 13])
