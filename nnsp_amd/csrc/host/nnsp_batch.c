@@ -415,6 +415,8 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         }
         TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
         if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
+        for (int k = 0; k < 2; ++k)
+            if (seg->recur_wait[k]) TRY(nnspk_stream_wait(stream, seg->recur_wait[k]));
         f.a_off = b->rec_a_off;
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;

@@ -88,6 +88,8 @@ struct nnsp_cascade {
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
     void *ev_vad_proj;              /* VAD's round-0 prefix FC layers done */
+    void *ev_r0proj[3];             /* round-0 prefix FC layers done, per net (r0_order 3) */
+    int r0_order;                   /* round 0's launch order (NNSP_R0_ORDER, see launch_round) */
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
@@ -209,6 +211,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     for (int q = 0; q < 2; ++q)
         if ((e = nnspk_event_create(&c->ev_ahead[q][0])) || (e = nnspk_event_create(&c->ev_ahead[q][1]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_vad_proj))) goto fail;
+    for (int n = 0; n < 3; ++n)
+        if ((e = nnspk_event_create(&c->ev_r0proj[n]))) goto fail;
     for (int n = 0; n < 3; ++n) {
         /* each net's rounds run on its batch's own stream: the cascade adds
          * one stream (c->stream) to the three, so on a device with four
@@ -318,6 +322,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     c->auto_window = 1;
     {
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
+        {
+            const char *o = getenv("NNSP_R0_ORDER");
+            c->r0_order = o ? atoi(o) : 0;
+        }
         /* the controller runs inside the nets' pipelined recur kernels when all
          * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
          * casc_control launch per round instead).  Serial mode keeps it: the
@@ -359,6 +367,7 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     }
     nnspk_event_destroy(c->ev_fork);
     nnspk_event_destroy(c->ev_vad_proj);
+    for (int n = 0; n < 3; ++n) nnspk_event_destroy(c->ev_r0proj[n]);
     for (int q = 0; q < 2; ++q) {
         nnspk_event_destroy(c->ev_ahead[q][0]);
         nnspk_event_destroy(c->ev_ahead[q][1]);
@@ -458,12 +467,14 @@ static int segment_features(nnsp_cascade *c, int n, int r, const int16_t *pcm, i
 /* net n's NN kernels of round r on stream st (after its cold front end);
  * wait_cold: first wait for the other nets' cold front ends (ev_join) */
 static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *cur, const int16_t *hist, void *st,
-                    void *proj_done)
+                    void *proj_done, void *recur_wait0, void *recur_wait1)
 {
     const int timed = c->timing && r < MAX_TIMED;
     nnsp_segment seg;
     memset(&seg, 0, sizeof seg);
     seg.proj_done = proj_done;
+    seg.recur_wait[0] = recur_wait0;
+    seg.recur_wait[1] = recur_wait1;
     seg.list = c->d_list[r & 1][n];
     seg.n_list_dev = cur + n;
     seg.seg_begin = c->d_seg_begin;
@@ -514,9 +525,15 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
      * with VAD's round, so VAD's cold frames and prefix layers are the
      * longest chain of the round and get the whole device (paired A/B over
      * 6 runs, profiles/r03: +1 % cascade frames/s over the plain order) */
-    static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2};
-    const int vad_first = r == 0 && c->fused && !c->serial;
-    const int *order = vad_first ? o_vad : o_plain;
+    /* r0_order (NNSP_R0_ORDER, development): 0 the order above; 1 VAD launched
+     * first, nothing waits; 3 S2I and KWS launched first, VAD's recurrence
+     * waits for their proj (so that their prefix layers get CUs before VAD's
+     * 2 048 recurrence workgroups take them all) */
+    static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2}, o_vad_last[3] = {0, 2, 1};
+    const int r0 = r == 0 && c->fused && !c->serial;
+    const int vad_first = r0 && c->r0_order == 0;
+    const int vad_last = r0 && c->r0_order == 3;
+    const int *order = vad_last ? o_vad_last : (r0 ? o_vad : o_plain);
     for (int i = 0; i < 3; ++i) {
         const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];
@@ -539,7 +556,9 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
          * ends do not (they ran behind VAD's recurrence for CUs, ~85 us, on
          * the round's critical path; A/B 1.010 vs 0.995 G) */
         if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
-        TRY(round_nn(c, a, r, n, T, cur, hist, st, vad_first && n == 1 ? c->ev_vad_proj : NULL));
+        void *pd = vad_first && n == 1 ? c->ev_vad_proj : (vad_last && n != 1 ? c->ev_r0proj[n] : NULL);
+        TRY(round_nn(c, a, r, n, T, cur, hist, st, pd, vad_last && n == 1 ? c->ev_r0proj[0] : NULL,
+                     vad_last && n == 1 ? c->ev_r0proj[2] : NULL));
     }
     if (c->fused) return 0;
     return nnspk_launch_casc_control(a, c->stream);

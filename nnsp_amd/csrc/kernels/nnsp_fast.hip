@@ -1171,7 +1171,11 @@ static_assert(PIPE_KT == 4, "the post wave describes one tile per 16 lanes");
 //     and stores the tile's state and bookkeeping at its last.
 // Every tile but a workgroup's only one runs at least 2 steps (the hand-overs
 // above use a tile's step 1), and every tile at least 1.
-template <class SH, bool ACC32>
+// MT: compiled for several tiles (FastRun.tseq > 1).  The one-tile
+// instantiation compiles the hand-overs and tile switches away: with them the
+// post and LSTM waves' loops carried the switch code (if-converted into
+// selects every step), and the FC waves on their SIMDs lost issue slots to it.
+template <class SH, bool ACC32, bool MT>
 __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
                                                                                             CascArgs ca) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1188,10 +1192,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // does; nothing reads or appends to it during this round)
     if (ctl && blockIdx.x == 0 && threadIdx.x < 6) ca.counts_clear[threadIdx.x] = 0;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
-    const int tseq = r.tseq;   // 1..PIPE_KT (host)
+    const int tseq = MT ? r.tseq : 1;   // 1..PIPE_KT (host)
     const int row0 = (int)blockIdx.x * tseq * 16;   // the workgroup's first list entry
     if (row0 >= nrow) return;
-    const int nk = min(tseq, (nrow - row0 + 15) / 16);   // its tiles
+    const int nk = MT ? min(tseq, (nrow - row0 + 15) / 16) : 1;   // its tiles
     // development probe (NNSP_RECUR_CLOCKS, the cascade's round 0 / a batch):
     // per workgroup, wall clock (100 MHz) at the start, after staging and at
     // the end, and where it ran (nnsp_hw_where)
@@ -1298,16 +1302,27 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     if (g < RGP) {
         const bool ok = row0 + sc < nrow;
         fetch_state(ok ? sid(row0 + sc) : 0, ok);
-        put_hs();
+        if constexpr (MT) {
+            put_hs();
+        } else {   // one tile: its step 0 reads h[0] and c as every later step reads them
+#pragma unroll
+            for (int k = 0; k < RPW; ++k) {
+                const int u = 4 * (g + RGP * k) + q;
+                if (g + RGP * k < nrt && u < N) {
+                    R.h[0][sc][u] = h_nx[k];
+                    R.c[sc][u] = c_nx[k];
+                }
+            }
+        }
     }
     __syncthreads();
     const int off1 = __builtin_amdgcn_readfirstlane(R.off[1]);
     const int off2 = __builtin_amdgcn_readfirstlane(R.off[2]);
     const int off3 = __builtin_amdgcn_readfirstlane(R.off[3]);
     const int total = __builtin_amdgcn_readfirstlane(R.off[4]);   // pipeline steps of all tiles
-    auto tile_of = [&](int j) { return (j >= off1 ? 1 : 0) + (j >= off2 ? 1 : 0) + (j >= off3 ? 1 : 0); };
-    auto off_of = [&](int k) { return k == 0 ? 0 : (k == 1 ? off1 : (k == 2 ? off2 : off3)); };
-    auto end_of = [&](int k) { return k + 1 < nk ? off_of(k + 1) : total; };
+    auto tile_of = [&](int j) { return MT ? (j >= off1 ? 1 : 0) + (j >= off2 ? 1 : 0) + (j >= off3 ? 1 : 0) : 0; };
+    auto off_of = [&](int k) { return MT ? (k == 0 ? 0 : (k == 1 ? off1 : (k == 2 ? off2 : off3))) : 0; };
+    auto end_of = [&](int k) { return MT && k + 1 < nk ? off_of(k + 1) : total; };
     // staged region: the LSTM's input fragments, then its recurrent ones, then the FC tail
     const uint8_t* Ax = W;
     const uint8_t* Ar = W + (LL.ar_off - LL.a_off);
@@ -1321,13 +1336,31 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // The loads land in xr untouched (lanes past the row read column 0 of it)
     // and x_half zeroes those lanes: any use of a load result right after it
     // (a select, a copy) made the wave wait the full load latency every step.
+    // the LSTM waves' view of a tile (lane: its stream): first NN frame,
+    // segment end, stream, valid -- read from LDS only when a step enters a
+    // tile (read every step, the lookup and unpacking cost the LSTM waves VALU
+    // issue that the stage waves on their SIMDs then waited for)
+    struct TileLane {
+        int t0, e, s;
+        bool v;
+    };
+    auto tile_lane = [&](int k) {
+        const int4 d = R.ti[k][sc];
+        return TileLane{d.y + (d.w & 1), d.z, d.x, (d.w & 2) != 0};
+    };
+    TileLane ll = {0, 0, 0, false};   // the LSTM step's tile
+    TileLane xl = {0, 0, 0, false};   // load_x's tile (xk)
+    int xk = -1;
     auto load_x = [&](int jj) {   // split x of pipeline step jj for the lane's stream (B fragments: high, low bytes)
         const int kx = tile_of(jj);
+        if (MT && kx != xk) {
+            xl = tile_lane(kx);
+            xk = kx;
+        }
         const int jl = jj - off_of(kx);
-        const int4 d = R.ti[kx][sc];
-        const bool ok = (d.w & 2) && d.y + 2 * jl + (d.w & 1) < d.z;
+        const bool ok = xl.v && xl.t0 + 2 * jl < xl.e;
         const uint8_t* src =
-            reinterpret_cast<const uint8_t*>(r.xg + ((size_t)(ok ? d.x : 0) * r.nstep_max + (ok ? jl : 0)) * XS);
+            reinterpret_cast<const uint8_t*>(r.xg + ((size_t)(ok ? xl.s : 0) * r.nstep_max + (ok ? jl : 0)) * XS);
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
             const int k0 = 64 * kt + 16 * q;
@@ -1369,6 +1402,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         }
     };
     if (g < RGP) {   // (past a segment: row 0 of xg, unused)
+        ll = xl = tile_lane(0);
+        xk = 0;
         load_x(0);
         x_half();
         load_x(1);
@@ -1393,6 +1428,46 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     int cut = -1;
     int s = 0, b = 0, e = 0, phase = 0;
     bool valid = false;
+    // a tile's first post step: its streams, their post-processing and
+    // controller state; frame b of a stream at NN phase 1 (no NN, the trigger
+    // carried) runs the controller here, its outputs are stored after the loop
+    auto post_start = [&](int tk) {
+        const int4 d = R.ti[tk][sc];
+        s = d.x;
+        b = d.y;
+        e = d.z;
+        phase = d.w & 1;
+        valid = (d.w & 2) != 0;
+        cut = -1;
+        if (lane < 16) {
+            const int4 p0 = R.ps[tk][lane][0], p1 = R.ps[tk][lane][1];
+            static_assert(sizeof(PostState) == 32, "PostState: two 16-byte words");
+            __builtin_memcpy(&ps, &p0, 16);
+            __builtin_memcpy(reinterpret_cast<char*>(&ps) + 16, &p1, 16);
+            if (ctl) cst = R.cst[tk][lane];
+        }
+        if (lane < 16 && valid && phase == 1 && b < e) {
+            R.pbt[tk][lane] = b;
+            R.pb[tk][lane] =
+                make_int2((int)((uint32_t)(uint16_t)ps.trigger | ((uint32_t)(uint16_t)ps.outputs[0] << 16)),
+                          (int)((uint32_t)(uint16_t)ps.outputs[1] | ((uint32_t)(uint16_t)ps.outputs[2] << 16)));
+            if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
+        }
+    };
+    // a tile's last post step: its post-processing and controller state and
+    // reset frame to LDS, for the bookkeeping after the loop (in the loop, its
+    // pointers and counters took SGPRs every role's loop then spilled)
+    auto post_end = [&](int tk) {
+        if (lane < 16) {
+            R.cut[tk][lane] = valid ? cut : -1;
+            int4 p0, p1;
+            __builtin_memcpy(&p0, &ps, 16);
+            __builtin_memcpy(&p1, reinterpret_cast<const char*>(&ps) + 16, 16);
+            R.ps[tk][lane][0] = p0;
+            R.ps[tk][lane][1] = p1;
+            R.cst[tk][lane] = cst;
+        }
+    };
     const NnLayer& L2 = img.L[r.li + 1];
     const NnLayer& L3 = img.L[r.li + 2];
     const NnLayer& L4 = img.L[r.li + 3];
@@ -1424,10 +1499,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 // ---- LSTM step j (the tile's step jl): row tile = 4 units x gates i, j, f, o
                 const int tk = tile_of(j);
                 const int jl = j - off_of(tk);
-                const int4 d = R.ti[tk][sc];
-                const int t = d.y + 2 * jl + (d.w & 1);
-                const bool active = (d.w & 2) && t < d.z;
-                const bool first = jl == 0;   // h from R.hs, c from the fetch registers
+                const bool first = MT && jl == 0;   // h from R.hs, c from the fetch registers
+                if (first) ll = tile_lane(tk);
+                const int t = ll.t0 + 2 * jl;
+                const bool active = ll.v && t < ll.e;
                 const int16_t* hsrc = first ? &R.hs[0][0] : &R.h[cur][0][0];
                 v4i bh[nkt_r], bl[nkt_r];
                 load_b<nkt_r>(hsrc, RS, nkt_r, lane, bh, bl);
@@ -1479,7 +1554,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 LCLK(3);
                 load_x(j + 2);
                 // the next tile's h and c: fetched now, h into R.hs at step 1
-                if (first && tk + 1 < nk) {
+                if (MT && first && tk + 1 < nk) {
                     const int4 dn = R.ti[tk + 1][sc];
                     fetch_state(dn.x, (dn.w & 2) != 0);
                 }
@@ -1528,7 +1603,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 LCLK(1);
                 // a tile's last step with another tile behind it: its final
                 // state goes to HBM from here (the last tile's: after the loop)
-                const bool hand = tk + 1 < nk && j + 1 == off_of(tk + 1) && (d.w & 2);
+                const bool hand = MT && tk + 1 < nk && j + 1 == off_of(tk + 1) && ll.v;
 #pragma unroll
                 for (int k = 0; k < RPW; ++k) {
                     const int rt = g + RGP * k;
@@ -1538,10 +1613,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                         const int16_t hn = active ? hv[k] : h_old[k];
                         R.c[sc][u] = cv;
                         R.h[cur ^ 1][sc][u] = hn;   // h after all groups (T6)
-                        if (jl == 1) R.hs[sc][u] = h_nx[k];
+                        if (MT && jl == 1) R.hs[sc][u] = h_nx[k];
                         if (hand) {
-                            r.h[(size_t)d.x * NN_MAX_W + u] = hn;
-                            r.c[(size_t)d.x * NN_MAX_W + u] = cv;
+                            r.h[(size_t)ll.s * NN_MAX_W + u] = hn;
+                            r.c[(size_t)ll.s * NN_MAX_W + u] = cv;
                         }
                     }
                 }
@@ -1574,29 +1649,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
           if (jp >= 0 && jp < total) {
             const int tk = tile_of(jp);
             const int jl = jp - off_of(tk);
-            if (jl == 0) {   // the tile's streams
-                const int4 d = R.ti[tk][sc];
-                s = d.x;
-                b = d.y;
-                e = d.z;
-                phase = d.w & 1;
-                valid = (d.w & 2) != 0;
-                cut = -1;
-                if (lane < 16) {
-                    const int4 p0 = R.ps[tk][lane][0], p1 = R.ps[tk][lane][1];
-                    static_assert(sizeof(PostState) == 32, "PostState: two 16-byte words");
-                    __builtin_memcpy(&ps, &p0, 16);
-                    __builtin_memcpy(reinterpret_cast<char*>(&ps) + 16, &p1, 16);
-                    if (ctl) cst = R.cst[tk][lane];
-                }
-                if (lane < 16 && valid && phase == 1 && b < e) {   // frame b: no NN, trigger carried
-                    R.pbt[tk][lane] = b;   // (stored after the loop)
-                    R.pb[tk][lane] =
-                        make_int2((int)((uint32_t)(uint16_t)ps.trigger | ((uint32_t)(uint16_t)ps.outputs[0] << 16)),
-                                  (int)((uint32_t)(uint16_t)ps.outputs[1] | ((uint32_t)(uint16_t)ps.outputs[2] << 16)));
-                    if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = b;
-                }
-            }
+            if (MT && jl == 0) post_start(tk);
             t = b + 2 * jl + phase;
             const bool active = valid && t < e;
             if (!SPL) {   // the last FC layer on this wave too
@@ -1650,17 +1703,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
           // and reset frame to LDS, for the bookkeeping after the loop (in the
           // loop, its pointers and counters took SGPRs that every role's loop
           // then spilled to VGPR lanes)
-          if (jp >= 0 && jp < total && lane < 16) {
+          if (MT && jp >= 0 && jp < total) {
               const int tk = tile_of(jp);
-              if (jp + 1 == end_of(tk)) {
-                  R.cut[tk][lane] = valid ? cut : -1;
-                  int4 p0, p1;
-                  __builtin_memcpy(&p0, &ps, 16);
-                  __builtin_memcpy(&p1, reinterpret_cast<const char*>(&ps) + 16, 16);
-                  R.ps[tk][lane][0] = p0;
-                  R.ps[tk][lane][1] = p1;
-                  R.cst[tk][lane] = cst;
-              }
+              if (jp + 1 == end_of(tk)) post_end(tk);
           }
         }
         if (clk && j < 64) clk[j * 16 + 1] = (long long)__builtin_amdgcn_s_memtime();
@@ -1676,6 +1721,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             if (j + 1 < total + 3 + SPL) iteration(j + 1, std::integral_constant<int, 1>{}, RL);
         }
     };
+    if constexpr (!MT)
+        if (post_w) post_start(0);
     if (g < RGP)
         run(std::integral_constant<int, 0>{});
     else if (g == RGP)
@@ -1689,6 +1736,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
 #undef LCLK
     // the last iteration's post outputs (each iteration ends with a barrier)
     if (store_w) flush((total + 2 + SPL) & 1);
+    if constexpr (!MT) {
+        if (post_w) post_end(0);
+        __syncthreads();
+    }
     // ---- the tiles' ends, after the loop (inside it, their pointers and
     //      counters cost every role's loop SGPRs, spilled to VGPR lanes).
     //      Frame b of the streams that started at NN phase 1 (no NN, the
@@ -1855,15 +1906,29 @@ const void* pick_proj(int shape, bool acc32, int gpt) {
 
 template <class SH>
 const void* pipe_fn(bool acc32) {
-    return acc32 ? (const void*)recur_pipe_kernel<SH, true> : (const void*)recur_pipe_kernel<SH, false>;
+    return acc32 ? (const void*)recur_pipe_kernel<SH, true, false> : (const void*)recur_pipe_kernel<SH, false, false>;
+}
+template <class SH>
+const void* pipe_fn_mt(bool acc32) {
+    return acc32 ? (const void*)recur_pipe_kernel<SH, true, true> : (const void*)recur_pipe_kernel<SH, false, true>;
 }
 
 // compiled shapes: the pipelined recurrence (one tile per workgroup)
-const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes) {
+// mt: the several-tiles instantiation (FastRun.tseq > 1)
+const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes, bool mt = false) {
     switch (shape) {
-        case NN_SHAPE_VAD: *waves = PipeCfg<ShapeVad>::WPG; *tile_bytes = sizeof(PipeTile<ShapeVad>); return pipe_fn<ShapeVad>(acc32);
-        case NN_SHAPE_KWS: *waves = PipeCfg<ShapeKws>::WPG; *tile_bytes = sizeof(PipeTile<ShapeKws>); return pipe_fn<ShapeKws>(acc32);
-        case NN_SHAPE_S2I: *waves = PipeCfg<ShapeS2i>::WPG; *tile_bytes = sizeof(PipeTile<ShapeS2i>); return pipe_fn<ShapeS2i>(acc32);
+        case NN_SHAPE_VAD:
+            *waves = PipeCfg<ShapeVad>::WPG;
+            *tile_bytes = sizeof(PipeTile<ShapeVad>);
+            return mt ? pipe_fn_mt<ShapeVad>(acc32) : pipe_fn<ShapeVad>(acc32);
+        case NN_SHAPE_KWS:
+            *waves = PipeCfg<ShapeKws>::WPG;
+            *tile_bytes = sizeof(PipeTile<ShapeKws>);
+            return mt ? pipe_fn_mt<ShapeKws>(acc32) : pipe_fn<ShapeKws>(acc32);
+        case NN_SHAPE_S2I:
+            *waves = PipeCfg<ShapeS2i>::WPG;
+            *tile_bytes = sizeof(PipeTile<ShapeS2i>);
+            return mt ? pipe_fn_mt<ShapeS2i>(acc32) : pipe_fn<ShapeS2i>(acc32);
         default: return nullptr;
     }
 }
@@ -1934,11 +1999,11 @@ int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const Casc
     if (nrow <= 0) return 0;
     int waves = 0;
     size_t tb = 0;
-    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb)) {
+    FastRun rr = *r;   // tiles per workgroup, run back to back through its pipeline
+    rr.tseq = rr.tseq < 1 ? 1 : (rr.tseq > PIPE_KT ? PIPE_KT : rr.tseq);
+    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb, rr.tseq > 1)) {
         CascArgs none;
         memset(&none, 0, sizeof none);
-        FastRun rr = *r;   // tiles per workgroup, run back to back through its pipeline
-        rr.tseq = rr.tseq < 1 ? 1 : (rr.tseq > PIPE_KT ? PIPE_KT : rr.tseq);
         const int tiles = (nrow + 15) / 16;
         return launch(fn, dim3((tiles + rr.tseq - 1) / rr.tseq), dim3(64 * waves), lds, stream, img, &rr,
                       ctl ? ctl : &none);
@@ -1959,10 +2024,11 @@ int nnspk_set_lds_limit(void) {
             int wv = 0;
             size_t tb = 0;
             const void* pipe = pick_pipe(shapes[i], a, &wv, &tb);
-            const void* fns[6] = {pick_proj(shapes[i], a, 1), pick_recur(shapes[i], nrts[i], a),
+            const void* pipe_mt = pick_pipe(shapes[i], a, &wv, &tb, true);
+            const void* fns[7] = {pick_proj(shapes[i], a, 1), pick_recur(shapes[i], nrts[i], a),
                                   pick_recur(NN_SHAPE_GENERIC, nrts[i], a), pipe, pick_proj(shapes[i], a, 2),
-                                  pick_proj(shapes[i], a, 4)};
-            for (int k = 0; k < 6; ++k) {
+                                  pick_proj(shapes[i], a, 4), pipe_mt};
+            for (int k = 0; k < 7; ++k) {
                 if (!fns[k]) continue;
                 hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (e != hipSuccess) return (int)e;
