@@ -324,7 +324,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
         {
             const char *o = getenv("NNSP_R0_ORDER");
-            c->r0_order = o ? atoi(o) : 0;
+            c->r0_order = o ? atoi(o) : 1;
         }
         /* the controller runs inside the nets' pipelined recur kernels when all
          * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
@@ -520,15 +520,16 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
     /* (measured and dropped, profiles/r02/sched: every net's cold front end
      * of a round before any net's NN kernels, VAD's recurrence after S2I's
      * and KWS's, every recur behind all three projs -- each -2..-7 %) */
-    /* round 0 with fused control: VAD (net 1) is launched first and S2I's
-     * and KWS's proj + recur wait for VAD's proj -- every stream starts
-     * with VAD's round, so VAD's cold frames and prefix layers are the
-     * longest chain of the round and get the whole device (paired A/B over
-     * 6 runs, profiles/r03: +1 % cascade frames/s over the plain order) */
-    /* r0_order (NNSP_R0_ORDER, development): 0 the order above; 1 VAD launched
-     * first, nothing waits; 3 S2I and KWS launched first, VAD's recurrence
-     * waits for their proj (so that their prefix layers get CUs before VAD's
-     * 2 048 recurrence workgroups take them all) */
+    /* round 0 with fused control: VAD (net 1) is launched first.  Until round
+     * 4 S2I's and KWS's proj + recur waited for VAD's proj (r0_order 0;
+     * profiles/r03: +1 % then).  With the faster proj and recurrences of
+     * round 4 that wait only delayed S2I's and KWS's proj until VAD's 2 048
+     * recurrence workgroups held every CU (KWS proj 164 -> 524 us, the round's
+     * critical path); without it (r0_order 1) round 0 ends ~70 us earlier:
+     * 1.080 vs 1.062 G (3 runs each), profiles/r04/r0_order/. */
+    /* r0_order (NNSP_R0_ORDER, development): 0 S2I's and KWS's NN wait for
+     * VAD's proj; 1 (default) VAD launched first, nothing waits; 3 S2I and
+     * KWS launched first, VAD's recurrence waits for their proj (1.059 G) */
     static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2}, o_vad_last[3] = {0, 2, 1};
     const int r0 = r == 0 && c->fused && !c->serial;
     const int vad_first = r0 && c->r0_order == 0;
