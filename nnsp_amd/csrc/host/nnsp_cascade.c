@@ -89,6 +89,8 @@ struct nnsp_cascade {
     void *ev_fork, *ev_join[3];
     void *ev_vad_proj;              /* VAD's round-0 prefix FC layers done */
     void *ev_r0proj[3];             /* round-0 prefix FC layers done, per net (r0_order 3) */
+    void *ev_r1proj[3];             /* round-1 prefix FC layers done, per net (ahead_mode 1) */
+    int ahead_mode;                 /* when the look-ahead front end starts (NNSP_AHEAD_MODE, see exec) */
     int r0_order;                   /* round 0's launch order (NNSP_R0_ORDER, see launch_round) */
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
@@ -212,7 +214,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         if ((e = nnspk_event_create(&c->ev_ahead[q][0])) || (e = nnspk_event_create(&c->ev_ahead[q][1]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_vad_proj))) goto fail;
     for (int n = 0; n < 3; ++n)
-        if ((e = nnspk_event_create(&c->ev_r0proj[n]))) goto fail;
+        if ((e = nnspk_event_create(&c->ev_r0proj[n])) || (e = nnspk_event_create(&c->ev_r1proj[n]))) goto fail;
     for (int n = 0; n < 3; ++n) {
         /* each net's rounds run on its batch's own stream: the cascade adds
          * one stream (c->stream) to the three, so on a device with four
@@ -325,6 +327,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         {
             const char *o = getenv("NNSP_R0_ORDER");
             c->r0_order = o ? atoi(o) : 1;
+            const char *am = getenv("NNSP_AHEAD_MODE");
+            c->ahead_mode = am ? atoi(am) : 0;
         }
         /* the controller runs inside the nets' pipelined recur kernels when all
          * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
@@ -367,7 +371,10 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
     }
     nnspk_event_destroy(c->ev_fork);
     nnspk_event_destroy(c->ev_vad_proj);
-    for (int n = 0; n < 3; ++n) nnspk_event_destroy(c->ev_r0proj[n]);
+    for (int n = 0; n < 3; ++n) {
+        nnspk_event_destroy(c->ev_r0proj[n]);
+        nnspk_event_destroy(c->ev_r1proj[n]);
+    }
     for (int q = 0; q < 2; ++q) {
         nnspk_event_destroy(c->ev_ahead[q][0]);
         nnspk_event_destroy(c->ev_ahead[q][1]);
@@ -558,6 +565,7 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
          * the round's critical path; A/B 1.010 vs 0.995 G) */
         if (vad_first && n != 1) TRY(nnspk_stream_wait(st, c->ev_vad_proj));
         void *pd = vad_first && n == 1 ? c->ev_vad_proj : (vad_last && n != 1 ? c->ev_r0proj[n] : NULL);
+        if (r == 1 && c->fused && !c->serial && c->ahead_mode == 1) pd = c->ev_r1proj[n];
         TRY(round_nn(c, a, r, n, T, cur, hist, st, pd, vad_last && n == 1 ? c->ev_r0proj[0] : NULL,
                      vad_last && n == 1 ? c->ev_r0proj[2] : NULL));
     }
@@ -765,8 +773,12 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
                 TRY(nnspk_memset((char *)c->d_zero + (size_t)((k + 1) & 1) * ZERO_STRIDE, 0, ZERO_BYTES, c->stream));
                 behind_launched = 1;
             }
-            if (ahead && !ahead_launched) {
-                for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(c->stream, c->ev_rnd[r & 1][n]));
+            /* ahead_mode (NNSP_AHEAD_MODE): 0 the front end waits for round 0's
+             * end; 1 for round 1's proj (round 1's recurrences are then on
+             * the CUs before its workgroups flood them); 2 for round 1's end */
+            if (ahead && !ahead_launched && r >= (c->ahead_mode ? 1 : 0)) {
+                for (int n = 0; n < 3; ++n)
+                    TRY(nnspk_stream_wait(c->stream, c->ahead_mode == 1 ? c->ev_r1proj[n] : c->ev_rnd[r & 1][n]));
                 const int q = (int)((k + 1) & 1);
                 TRY(ahead_read(c, q, 1)); /* slot q's last front end (two chunks ago) is long done */
                 TRY(nnspk_event_record(c->ev_ahead[q][0], c->stream));

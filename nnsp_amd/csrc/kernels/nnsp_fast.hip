@@ -197,11 +197,15 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
                     }
                 }
             }
+            // ACC32: each row's epilogue constant starts its low-plane
+            // accumulator (mod 2^32 the same sum, as the recurrence's gates), so
+            // the epilogue adds nothing
             v4i ah[CH], al[CH];
 #pragma unroll
             for (int c = 0; c < CH; ++c) {
                 ah[c] = v4i{0, 0, 0, 0};
-                al[c] = v4i{0, 0, 0, 0};
+                al[c] = ACC32 ? v4i{(int32_t)cst[c][0], (int32_t)cst[c][1], (int32_t)cst[c][2], (int32_t)cst[c][3]}
+                              : v4i{0, 0, 0, 0};
                 if (r0 + c < NRT)
 #pragma unroll
                     for (int kt = 0; kt < NKT; ++kt) {
@@ -220,17 +224,17 @@ __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, co
                     for (int i = 0; i < 4; ++i) {
                         const int row = 16 * (r0 + c) + 4 * q + i;
                         if (r0 + c < NRT && (PAD || row < rows)) {
-                            const int32_t acc = (ah[c][i] << 8) + al[c][i];
+                            const int32_t acc = (ah[c][i] << 8) + al[c][i];   // (+ cst: ACC32)
                             int32_t v;
                             if constexpr (decltype(nolsh)::value) {
                                 if (act == ACT_RELU6) {   // relu6_q12's >> 3 folded into the layer shift
-                                    const int32_t u = wadd(acc, (int32_t)cst[c][i]) >> rsh3;
+                                    const int32_t u = acc >> rsh3;
                                     out[sc * out_stride + row] = (int16_t)min(max(u, 0), 24576);
                                     continue;
                                 }
-                                v = wadd(acc, (int32_t)cst[c][i]) >> rsh;
+                                v = acc >> rsh;
                             } else {
-                                v = ep_out<ACC32>(acc, cst[c][i], rsh, lsh);
+                                v = ep_out<ACC32>(acc, ACC32 ? 0 : cst[c][i], rsh, lsh);
                             }
                             if (act == ACT_LINEAR)
                                 reinterpret_cast<int32_t*>(out + sc * out_stride)[row] = v;

@@ -181,12 +181,14 @@ __device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp
     const int sh = m ? 15 - (31 - __clz((int)m)) : 0;
     const int32_t y = sh >= 0 ? wshl(x, sh) : (x >> -sh);
     int32_t kx = (y - 32768) >> 8;
-    const int32_t dx = (y - 32768) - (kx << 8);
+    const int32_t dx = (y - 32768) & 255;   // = (y - 32768) - (kx << 8), kx before the clamp
     kx = kx < 0 ? 0 : (kx > 127 ? 127 : kx);
     const uint32_t pr = logp[kx];
-    int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (((int32_t)(int16_t)(pr >> 16) * dx) >> 15);
-    v = (int32_t)(((int64_t)v * 0x3796) >> 15);
-    return wadd(v, 0x2688 * -sh);
+    // 24-bit multiplies (full rate): |slope| < 2^15, 0 <= dx < 2^8; |v| < 2^16,
+    // so v * 0x3796 < 2^31 -- the int64 product of fixlog10.c is exact in 32
+    int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (__mul24((int32_t)(int16_t)(pr >> 16), dx) >> 15);
+    v = __mul24(v, 0x3796) >> 15;
+    return wadd(v, __mul24(0x2688, -sh));
 }
 
 // 4x4 transpose of the register index m with the lane's row (lane bits 4-5):

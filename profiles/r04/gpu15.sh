@@ -5,6 +5,8 @@
 set -o pipefail
 O=gpurun_out/r04/final; mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests > $O/pytest_final.log 2>&1 || { echo "pytest failed"; tail -30 $O/pytest_final.log; exit 1; }
+tail -1 $O/pytest_final.log
 bash profiles/r04/prof.sh $O/cascade || exit 1
 python3 profiles/r04/summarize.py $O/cascade cascade 32768 100 ref mix $O/pmc_cascade.json > $O/summ.log 2>&1 || { echo "summarize failed"; tail -5 $O/summ.log; exit 1; }
 for i in 1 2 3; do
