@@ -328,7 +328,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
             const char *o = getenv("NNSP_R0_ORDER");
             c->r0_order = o ? atoi(o) : 1;
             const char *am = getenv("NNSP_AHEAD_MODE");
-            c->ahead_mode = am ? atoi(am) : 0;
+            c->ahead_mode = am ? atoi(am) : 1;
         }
         /* the controller runs inside the nets' pipelined recur kernels when all
          * three have compiled shapes (NNSP_CASCADE_CONTROL_KERNEL: a separate
@@ -774,8 +774,12 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
                 behind_launched = 1;
             }
             /* ahead_mode (NNSP_AHEAD_MODE): 0 the front end waits for round 0's
-             * end; 1 for round 1's proj (round 1's recurrences are then on
-             * the CUs before its workgroups flood them); 2 for round 1's end */
+             * end; 1 (default) for round 1's proj, so that round 1's proj runs
+             * on an idle device and its recurrences are on the CUs before the
+             * front end's workgroups flood them -- before, they waited for the
+             * front end to drain and ran after it (~190 us past its end);
+             * 2 for round 1's end.  A/B 1.099 / 1.149 / 1.111 G (modes 0 / 1
+             * / 2, 2 runs each), profiles/r04/ahead_mode/ */
             if (ahead && !ahead_launched && r >= (c->ahead_mode ? 1 : 0)) {
                 for (int n = 0; n < 3; ++n)
                     TRY(nnspk_stream_wait(c->stream, c->ahead_mode == 1 ? c->ev_r1proj[n] : c->ev_rnd[r & 1][n]));
