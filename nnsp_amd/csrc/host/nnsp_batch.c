@@ -347,10 +347,11 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
  * through one pipeline -- its fill and drain (4 iterations) and the weight
  * staging once per workgroup instead of once per tile.  Short segments (a
  * cascade round's window) gain most; NNSP_RECUR_TSEQ=1..4 overrides. */
-static int recur_tseq(const nnsp_segment *seg, int T)
+static int recur_tseq(const nnsp_segment *seg, int T, int shape)
 {
     const char *e = getenv("NNSP_RECUR_TSEQ");   /* (read per launch: tests switch it) */
-    const int env = e ? atoi(e) : 0;
+    int env = e ? atoi(e) : 0;
+    if (shape == NN_SHAPE_VAD && (e = getenv("NNSP_RECUR_TSEQ_VAD")) != NULL) env = atoi(e);   /* development */
     if (env > 0) return env > 4 ? 4 : env;
     const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
     const int steps = (W + 1) / 2;
@@ -421,7 +422,7 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
         f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
         f.ep_lo = b->ep_rec_lo;
         f.ep_n = b->ep_rec_n;
-        f.tseq = recur_tseq(seg, T);
+        f.tseq = recur_tseq(seg, T, b->shape);
         TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, seg->ctl, stream));
     } else {
         NnRun r;
