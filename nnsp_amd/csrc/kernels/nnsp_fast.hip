@@ -32,6 +32,14 @@
 
 using namespace nnsp;
 
+// development probes (NNSP_RECUR_CLOCKS: s_memtime per phase), compiled in
+// only with -DNNSP_PROBES=1 (make PROBES=1; profiles/recur_clocks.py).  Their
+// pointer and bound checks cost the loops SGPRs: built in, the recurrence
+// kernels spilled 40-60 SGPRs to VGPR lanes (10 without them) and read them
+// back with v_readlane in the step loops
+#ifndef NNSP_PROBES
+#define NNSP_PROBES 0
+#endif
 #define TT_BYTES 1024   // LDS copy of nnsp_tbl_tanh1 (tanh_q15s), behind the staged A fragments
 #define P_ASTRIDE 264   // int16 per row of a proj activation buffer
 #define P_UNION 1920    // context frames of a tile: G streams x (32/G + 4) frames x 40 features (int16)
@@ -374,7 +382,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after staging, at the end, and the tiles it ran
     const unsigned pwid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    long long* pwc = (r.dbg_clk && lane == 0 && pwid < 8192u) ? r.dbg_clk + 2048 + 4 * 32768 + 4 * pwid : nullptr;
+    long long* pwc = (NNSP_PROBES && r.dbg_clk && lane == 0 && pwid < 8192u) ? r.dbg_clk + 2048 + 4 * 32768 + 4 * pwid : nullptr;
     if (pwc) pwc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, false);
@@ -389,7 +397,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     // last tile's x stores
     struct Seg { int s, b, L, ph; bool ok; int fr; };
     // development probe (NNSP_RECUR_CLOCKS): s_memtime per phase of wave 0's first tiles
-    long long* clk = (r.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? r.dbg_clk + 12 : nullptr;
+    long long* clk = (NNSP_PROBES && r.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? r.dbg_clk + 12 : nullptr;
     int it = 0;
 #define PCLK(k) \
     if (clk && it < 64) clk[it * 16 + (k)] = (long long)__builtin_amdgcn_s_memtime()
@@ -1203,7 +1211,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // development probe (NNSP_RECUR_CLOCKS, the cascade's round 0 / a batch):
     // per workgroup, wall clock (100 MHz) at the start, after staging and at
     // the end, and where it ran (nnsp_hw_where)
-    long long* wgc = (r.dbg_clk && (!ctl || ca.round == 0) && threadIdx.x == 0 && blockIdx.x < 8192u)
+    long long* wgc = (NNSP_PROBES && r.dbg_clk && (!ctl || ca.round == 0) && threadIdx.x == 0 && blockIdx.x < 8192u)
                          ? r.dbg_clk + NNSP_DCLK_RECUR + 4 * blockIdx.x
                          : nullptr;
     if (wgc) wgc[0] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1482,7 +1490,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
 #define RECUR_CLK_WAVE 0
 #endif
     constexpr int CLKW = RECUR_CLK_WAVE < RGP ? RECUR_CLK_WAVE : 0;
-    long long* clk = (r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 && (g == CLKW || g >= RGP))
+    long long* clk = (NNSP_PROBES && r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 && (g == CLKW || g >= RGP))
                          ? r.dbg_clk + 2 * (g == CLKW ? 0 : g - RGP + 1)
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the

@@ -15,6 +15,10 @@
 #include <stdlib.h>
 
 #include "nnsp_dev.h"
+// development probes (s_memtime per phase): compiled in only with -DNNSP_PROBES=1
+#ifndef NNSP_PROBES
+#define NNSP_PROBES 0
+#endif
 #include "nnsp_kabi.h"
 #include "nnsp_nn.h"
 
@@ -363,7 +367,7 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after the tables, at the end, and the frames it ran
     const unsigned wid0 = blockIdx.x * (unsigned)FE_WPG + (threadIdx.x >> 6);
-    long long* wclk = (a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
+    long long* wclk = (NNSP_PROBES && a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
     fe_tables_load<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
@@ -487,7 +491,7 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
             }
         }
     };
-    long long* fclk = (a.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? a.dbg_clk + 1024 : nullptr;
+    long long* fclk = (NNSP_PROBES && a.dbg_clk && blockIdx.x == 0 && wv == 0 && lane == 0) ? a.dbg_clk + 1024 : nullptr;
 #define FCLK(k) \
     if (fclk && f - fbeg < 64u) fclk[8 * (f - fbeg) + (k)] = (long long)__builtin_amdgcn_s_memtime()
     for (unsigned f = fbeg; f < fend; ++f) {

@@ -28,7 +28,7 @@ STAGES = ["prefetch+window+ring store", "cFFT", "split+power", "Mel MACs", "sums
 
 def isa(src):
     out = os.path.join(tempfile.mkdtemp(), "k.s")
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "--cuda-device-only", "-S",
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-DNNSP_PROBES=1", "--cuda-device-only", "-S",
                     src, "-o", out], check=True, capture_output=True)
     lines = open(out).read().split("\n")
     a = next(i for i, l in enumerate(lines) if l.startswith(SYM + ":"))

@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Development probe: per-phase s_memtime clocks of recur_kernel tile 0
-(NNSP_RECUR_CLOCKS=1).  Prints median cycles per phase of a step."""
+(NNSP_RECUR_CLOCKS=1).  Prints median cycles per phase of a step.
+
+Needs a library built with the probes (make -C nnsp_amd PROBES=1, or
+NNSP_LIB=<a build with PROBES=1>): the default build compiles them out."""
 import ctypes as C
 import os
 import sys
