@@ -47,6 +47,22 @@ using namespace nnsp;
                           // (8: one table staging per 8 waves, 37 KB LDS, three workgroups per CU --
                           // measured slower, shared FE 2.19 -> 2.29 ms; profiles/r03/wpg.sh)
 #endif
+// FE_WPG7=7 (off): the shared front end of the shipped build (72 VGPRs) at
+// seven waves per SIMD -- seven-wave workgroups, 36.4 KB LDS, four per CU.
+// Measured slower (round 4, paired A/B, 3 runs): shared FE 2.02 -> 2.22 ms,
+// cascade 1.158 -> 1.090 G (profiles/r04/fe_seven_waves.jsonl); at 96 % VALU
+// issue a seventh wave adds no issue slots, and the bigger workgroups halve
+// the turnover the nets' rounds get CUs through.
+#ifndef FE_WPG7
+#define FE_WPG7 0
+#endif
+template <int MODE, bool PORT>
+struct FeGeom {
+    static constexpr bool seven = MODE == 1 /* FE_MODE_SHARED */ && !PORT && FE_WPG7 == 7;
+    static constexpr int WPG = seven ? 7 : FE_WPG;     // waves per workgroup
+    static constexpr int MINW = seven ? 7 : 6;         // waves per SIMD the registers must allow
+    static constexpr int PER_CU = seven ? 4 : 24 / FE_WPG;   // resident workgroups per CU
+};
 #ifndef FE_PAIR_DEFAULT
 #define FE_PAIR_DEFAULT 1   // fe_kernel2 (two frames per wave) for the batch mode
 #endif
@@ -349,11 +365,12 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // PORT: the ARM_OPTIMIZED=0 build's front end (row N4: Frac15 window, fft.c's
 // rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
 template <int MODE, bool PORT>
-__global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
+__global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>::MINW)) void fe_kernel(FeArgs a) {
+    constexpr int WPG = FeGeom<MODE, PORT>::WPG;
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
     // contiguous so that the padded T1 transpose may use both
-    __shared__ __attribute__((aligned(16))) int32_t XPs[FE_WPG][FE_X_DW + FE_P_DW];
+    __shared__ __attribute__((aligned(16))) int32_t XPs[WPG][FE_X_DW + FE_P_DW];
     __shared__ __attribute__((aligned(16))) FeTables TB;
     const unsigned nrow = a.n_list_dev ? (unsigned)*a.n_list_dev : (a.list ? (unsigned)a.n_list : (unsigned)a.S);
     const unsigned segW = a.seg_len > 0 && a.seg_len < a.T ? (unsigned)a.seg_len : (unsigned)a.T;
@@ -361,12 +378,12 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
     constexpr bool shared = MODE == FE_MODE_SHARED;
     const unsigned W = cold ? (segW < 2u ? segW : 2u) : segW;
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
-    const unsigned nw = gridDim.x * (unsigned)FE_WPG;
+    const unsigned nw = gridDim.x * (unsigned)WPG;
     const unsigned per = (nfr + nw - 1) / nw;
-    if (blockIdx.x * (unsigned)FE_WPG * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
+    if (blockIdx.x * (unsigned)WPG * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after the tables, at the end, and the frames it ran
-    const unsigned wid0 = blockIdx.x * (unsigned)FE_WPG + (threadIdx.x >> 6);
+    const unsigned wid0 = blockIdx.x * (unsigned)WPG + (threadIdx.x >> 6);
     long long* wclk = (NNSP_PROBES && a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
     fe_tables_load<PORT>(TB, a);
@@ -382,7 +399,7 @@ __global__ __launch_bounds__(64 * FE_WPG, 6) void fe_kernel(FeArgs a) {
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
-    const unsigned wid = blockIdx.x * (unsigned)FE_WPG + (unsigned)wv;
+    const unsigned wid = blockIdx.x * (unsigned)WPG + (unsigned)wv;
     const unsigned fbeg = wid * per;
     const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
     if (wclk) wclk[1] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -1732,7 +1749,11 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     int W = a->seg_len > 0 && a->seg_len < a->T ? a->seg_len : a->T;
     if (a->mode == FE_MODE_COLD && W > 2) W = 2;
     const long long nfr = (long long)nrow * W;
-    long long blocks = (nfr + FE_WPG - 1) / FE_WPG;
+    // seven-wave workgroups for the shared mode of the shipped build (FeGeom)
+    const bool seven = a->mode == FE_MODE_SHARED && !a->port && FeGeom<FE_MODE_SHARED, false>::seven;
+    const int wpg = seven ? FeGeom<FE_MODE_SHARED, false>::WPG : FE_WPG;
+    const int per_cu = seven ? FeGeom<FE_MODE_SHARED, false>::PER_CU : 24 / FE_WPG;
+    long long blocks = (nfr + wpg - 1) / wpg;
     // whole multiples of the resident workgroups (256 CUs x 6 at 80 VGPRs):
     // each wave runs a contiguous frame range, so a partial last wave of
     // workgroups is pure tail
@@ -1744,12 +1765,12 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // workgroup -- eight generations, 67 frames per wave: cascade 3 072
     // workgroups 0.948 G, 4 608 0.980, 6 144 0.986-0.998, 9 216 0.992,
     // 12 288 1.016, 18 432 1.008, 24 576 0.992 G; shared FE 2.16 -> 2.09 ms)
-    const long long cap = 256LL * (24 / FE_WPG) * 8;
+    const long long cap = 256LL * per_cu * 8;
     if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
     if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 8192 / FE_WPG) blocks = 8192 / FE_WPG;
-    const dim3 g((unsigned)blocks), blk(64 * FE_WPG);
+    const dim3 g((unsigned)blocks), blk(64 * wpg);
     hipStream_t st = (hipStream_t)stream;
     // two frames per wave (fe_kernel2): FE_PAIR_DEFAULT = 0 off, 1 the batch
     // mode only (default), 2 the shared mode too.  Measured (A/B on one box):
