@@ -82,6 +82,8 @@ struct FeLane {
 struct FeTables {
     int2 tw[3][3][64];    // per stage, twiddle (k, 2k, 3k) of each lane's butterfly: (cos, sin)
     int4 split[256];      // per bin k: (A_re, A_im, B_re, -) of realCoefA/BQ31 at 16k (PORT: rfft's twiddle)
+    int64_t nc[120];      // FE_MODE_SHARED: -mean * stdR of norm[k], norm[120 + k] (fe_kernel's 32-bit path:
+                          // (feature - mean) * stdR as one v_mad_i64_i32 of feature, stdR and nc)
     int32_t norm[240];    // FE_MODE_SHARED: k < 120 net k/40's mean of Mel bank k%40, 120 <= k < 240 its
                           // stdR (fe_norm_word) -- dense, so that 40 lanes read 40 banks
     uint32_t logp[128];   // log_tayler_coeff (value, slope) pairs
@@ -148,6 +150,7 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
             T.split[k] = make_int4(nnsp_tbl_split[3 * k], nnsp_tbl_split[3 * k + 1], nnsp_tbl_split[3 * k + 2], 0);
     }
     for (int k = threadIdx.x; k < 240; k += blockDim.x) T.norm[k] = fe_norm_word(a, k);
+    for (int k = threadIdx.x; k < 120; k += blockDim.x) T.nc[k] = -(int64_t)fe_norm_word(a, k) * fe_norm_word(a, 120 + k);
     for (int i = threadIdx.x; i < 128; i += blockDim.x)
         T.logp[i] = (uint32_t)(uint16_t)nnsp_tbl_log[2 * i] | ((uint32_t)(uint16_t)nnsp_tbl_log[2 * i + 1] << 16);
     if (threadIdx.x < 64) {
@@ -198,8 +201,10 @@ __device__ __forceinline__ int16_t fe_norm(int32_t lg, int32_t mn, int32_t sr, i
 __device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp) {
     if (x == 0) x = 1;
     const uint32_t m = (uint32_t)x & 0x7FFFFFFFu;
-    const int sh = m ? 15 - (31 - __clz((int)m)) : 0;
-    const int32_t y = sh >= 0 ? wshl(x, sh) : (x >> -sh);
+    // g = -sh of fixlog10.c (sh = 15 - msb(m), 0 for m = 0), |g| <= 15; x << sh
+    // (wrapping) or x >> -sh as one 64-bit shift: the low word of (x:0) >> (32 + g)
+    const int g = m ? 16 - __builtin_clz(m) : 0;
+    const int32_t y = (int32_t)(((int64_t)x << 32) >> (32 + g));
     int32_t kx = (y - 32768) >> 8;
     const int32_t dx = (y - 32768) & 255;   // = (y - 32768) - (kx << 8), kx before the clamp
     kx = kx < 0 ? 0 : (kx > 127 ? 127 : kx);
@@ -208,7 +213,7 @@ __device__ __forceinline__ int32_t log10_q15_lds(int32_t x, const uint32_t* logp
     // so v * 0x3796 < 2^31 -- the int64 product of fixlog10.c is exact in 32
     int32_t v = (int32_t)(int16_t)(pr & 0xffff) + (__mul24((int32_t)(int16_t)(pr >> 16), dx) >> 15);
     v = __mul24(v, 0x3796) >> 15;
-    return wadd(v, __mul24(0x2688, -sh));
+    return wadd(v, __mul24(0x2688, g));
 }
 
 // 4x4 transpose of the register index m with the lane's row (lane bits 4-5):
@@ -644,11 +649,23 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
                 // keep the (mean, stdR) LDS reads here: hoisted out of the frame
                 // loop they would pin 6 VGPRs and cost a wave per SIMD
                 __asm__ volatile("" ::: "memory");
+                // each net's normalisation (feature_module.c:67-73); one
+                // wave-uniform branch for the three
                 int16_t nv[3];
+                if (a.norm32) {   // (lg - mean) * stdR = lg * stdR + nc, exact in 64 bits
 #pragma unroll
-                for (int n = 0; n < 3; ++n) {   // each net's normalisation (feature_module.c:67-73)
-                    const int32_t mn = TB.norm[40 * n + lane], sr = TB.norm[120 + 40 * n + lane];
-                    nv[n] = fe_norm(lg, mn, sr, a.nshift[n], a.norm32);
+                    for (int n = 0; n < 3; ++n) {
+                        const int32_t sr = TB.norm[120 + 40 * n + lane];
+                        const int64_t nc = TB.nc[40 * n + lane];
+                        const int32_t v = (int32_t)((uint64_t)mad_i64_i32(lg, sr, nc) >> a.nshift[n]);
+                        nv[n] = (int16_t)min(max(v, -32768), 32767);   // v_med3_i32
+                    }
+                } else {
+#pragma unroll
+                    for (int n = 0; n < 3; ++n) {
+                        const int32_t mn = TB.norm[40 * n + lane], sr = TB.norm[120 + 40 * n + lane];
+                        nv[n] = fe_norm(lg, mn, sr, a.nshift[n], 0);
+                    }
                 }
                 pv01 = (uint32_t)(uint16_t)nv[0] | ((uint32_t)(uint16_t)nv[1] << 16);
                 pv2 = nv[2];
