@@ -74,6 +74,20 @@ struct FeGeom {
 __device__ int16_t nnsp_zero_pcm[160];   // input frames before a net's reset (FE_MODE_COLD)
 __device__ __forceinline__ int zslot(int c) { return c ^ ((c >> 6) & 2) ^ ((c >> 3) & 4) ^ ((c >> 3) & 8); }
 
+// a wave-uniform offset as such (both halves through readfirstlane): loads
+// and stores at base + offset + lane then take the SGPR-base form with a
+// 32-bit lane offset, no per-lane 64-bit address arithmetic
+__device__ __forceinline__ size_t wave_off(size_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((size_t)hi << 32) | lo;
+}
+// raw buffer descriptor (stride 0, range 2^31 bytes, CDNA3/4 word 3) on a
+// wave-uniform base: loads at a per-lane byte offset with no VALU address math
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pcm_rsrc(const int16_t* base) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<int16_t*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+
 struct FeLane {
     int mj0, mfirst, mcnt;   // Mel segment start bin; first segment and segment count of bank `lane`
 };
@@ -455,14 +469,19 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
         if (!cold && p.t - 2 >= p.b && x0 >= 0) {
             // common case (wave-uniform): frames t-2..t are consecutive in the
             // chunk, so the window is 480 contiguous samples from one pointer
-            const int16_t* q = a.pcm + ((size_t)p.s * a.T + x0) * 160 + o;
-            r[0] = *reinterpret_cast<const uint32_t*>(q);
-            r[1] = *reinterpret_cast<const uint32_t*>(q + 128);
-            r[2] = *reinterpret_cast<const uint32_t*>(q + 256);
+            // buffer loads from a descriptor on the window's first sample (a
+            // wave-uniform base, SALU) at the lane's byte offset: no per-lane
+            // 64-bit address arithmetic per frame
+            const __amdgpu_buffer_rsrc_t rs = pcm_rsrc(a.pcm + wave_off(((size_t)p.s * a.T + x0) * 160));
+            const int vo = 2 * o;
+            // (the rows' byte offsets as SGPR offsets: one lane-offset VGPR)
+            r[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0);
+            r[1] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 256, 0);
+            r[2] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 512, 0);
             // lanes 48..63 (taps 480..511, window coefficient 0) load a
             // dummy in-frame word: a select of the value, not of the address,
             // was a register write behind the frame's pending stores
-            r[3] = *reinterpret_cast<const uint32_t*>(q + (lane < 48 ? 384 : 0));
+            r[3] = __builtin_amdgcn_raw_buffer_load_b32(rs, lane < 48 ? vo + 768 : vo, 0, 0);
             return;
         }
         const int16_t* p0 = frame_ptr(p, p.t - 2);
@@ -504,10 +523,10 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
                 // nring[0] + n * nstride): one base pointer live in the loop
                 // po = s * ring + slot < 2^31 (nnsp_cascade_create); po * 40
                 // does not fit 32 bits past 2^26 ring rows: 64-bit offsets
-                int16_t* r0 = a.nring[0] + ((size_t)po * 40u + (unsigned)lane);
-                r0[0] = (int16_t)(pv01 & 0xffff);
-                r0[nstride] = (int16_t)(pv01 >> 16);
-                r0[2 * nstride] = (int16_t)pv2;
+                int16_t* r0 = a.nring[0] + wave_off((size_t)po * 40u);   // po: the same in every lane
+                r0[lane] = (int16_t)(pv01 & 0xffff);
+                (r0 + nstride)[lane] = (int16_t)(pv01 >> 16);
+                (r0 + 2 * nstride)[lane] = (int16_t)pv2;
             } else {
                 a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
@@ -633,12 +652,22 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
         FCLK(4);
         // ---- log10 (fixlog10.c:53-61), normalise (feature_module.c:67-73)
         if (lane < 40) {
-            int64_t mac = 0;
-            // a bank spans at most FE_MEL_MAXSEG lane segments (the table is
-            // generated that way; tests/test_tables.py checks it): unrolled
+            // a bank spans at most FE_MEL_MAXSEG = 3 lane segments, lanes
+            // mfirst.. (tests/test_tables.py checks the table); a missing one
+            // reads lane 63's partial sum, which is zero (no segment there, also
+            // checked): three unconditional reads instead of masked adds
+            // (the shared mode of the shipped build; the other instantiations
+            // keep the masked adds: their registers are at the 80-VGPR limit)
+            static_assert(FE_MEL_MAXSEG == 3, "fe_kernel: bank sums of three segments");
+            int64_t mac;
+            if constexpr (shared && !PORT) {
+                mac = Mp[L.mfirst] + Mp[L.mcnt > 1 ? L.mfirst + 1 : 63] + Mp[L.mcnt > 2 ? L.mfirst + 2 : 63];
+            } else {
+                mac = 0;
 #pragma unroll
-            for (int k = 0; k < FE_MEL_MAXSEG; ++k)
-                if (k < L.mcnt) mac += Mp[L.mfirst + k];
+                for (int k = 0; k < FE_MEL_MAXSEG; ++k)
+                    if (k < L.mcnt) mac += Mp[L.mfirst + k];
+            }
             const int32_t lg = log10_q15_lds(sat32_shr15(mac), TB.logp);
             if (MODE == FE_MODE_BATCH && a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
             if constexpr (shared) {
@@ -801,7 +830,7 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
         const int o = 2 * lane;
         const int x0 = shared ? p.t - 2 : p.t - 2 - a.lookback;
         if (p.t - 2 >= p.b && x0 >= 0) {
-            const int16_t* q = a.pcm + ((size_t)p.s * a.T + x0) * 160 + o;
+            const int16_t* q = a.pcm + wave_off(((size_t)p.s * a.T + x0) * 160) + o;
             r[0] = *reinterpret_cast<const uint32_t*>(q);
             r[1] = *reinterpret_cast<const uint32_t*>(q + 128);
             r[2] = *reinterpret_cast<const uint32_t*>(q + 256);
@@ -846,10 +875,10 @@ __global__ __launch_bounds__(256, 4) void fe_kernel2(FeArgs a) {
     auto flush1 = [&](bool pend, unsigned po, uint32_t pv01, int32_t pv2) {
         if (pend && lane < 40) {
             if constexpr (shared) {
-                int16_t* r0 = a.nring[0] + ((size_t)po * 40u + (unsigned)lane);
-                r0[0] = (int16_t)(pv01 & 0xffff);
-                r0[nstride] = (int16_t)(pv01 >> 16);
-                r0[2 * nstride] = (int16_t)pv2;
+                int16_t* r0 = a.nring[0] + wave_off((size_t)po * 40u);   // po: the same in every lane
+                r0[lane] = (int16_t)(pv01 & 0xffff);
+                (r0 + nstride)[lane] = (int16_t)(pv01 >> 16);
+                (r0 + 2 * nstride)[lane] = (int16_t)pv2;
             } else {
                 a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
