@@ -1815,7 +1815,14 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
-    if (a->mode == FE_MODE_COLD && a->n_list_dev && blocks > 8192 / FE_WPG) blocks = 8192 / FE_WPG;
+    if (a->mode == FE_MODE_COLD && a->n_list_dev) {
+        // (NNSP_COLD_FE_BLOCKS, development: another cap for the device-sized lists)
+        static const long long cold_cap = [] {
+            const char* e = getenv("NNSP_COLD_FE_BLOCKS");
+            return e && atoll(e) > 0 ? atoll(e) : 8192LL / FE_WPG;
+        }();
+        if (blocks > cold_cap) blocks = cold_cap;
+    }
     const dim3 g((unsigned)blocks), blk(64 * wpg);
     hipStream_t st = (hipStream_t)stream;
     // two frames per wave (fe_kernel2): FE_PAIR_DEFAULT = 0 off, 1 the batch
