@@ -408,6 +408,15 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             f.gpt = b->shape == NN_SHAPE_GENERIC ? 1 : (steps <= 4 ? 4 : (steps <= 8 ? 2 : 1));
         }
         int blocks = b->proj_blocks;
+        {   /* (NNSP_PROJ_LATE_BLOCKS, development: a smaller persistent grid for the
+             * cascade's later rounds, whose device-sized lists are short) */
+            static int late = -1;
+            if (late < 0) {
+                const char *e = getenv("NNSP_PROJ_LATE_BLOCKS");
+                late = e && atoi(e) > 0 ? atoi(e) : 0;
+            }
+            if (late && seg->n_list_dev && seg->round > 0 && blocks > late) blocks = late;
+        }
         if (seg->list && !seg->n_list_dev) {   /* size the grid to the listed streams */
             const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
             const long long pt = (long long)seg->n_list * ((W / 2 + 1 + 15) / 16);

@@ -482,6 +482,7 @@ static int round_nn(nnsp_cascade *c, CascArgs *a, int r, int n, int T, int32_t *
     seg.proj_done = proj_done;
     seg.recur_wait[0] = recur_wait0;
     seg.recur_wait[1] = recur_wait1;
+    seg.round = r;
     seg.list = c->d_list[r & 1][n];
     seg.n_list_dev = cur + n;
     seg.seg_begin = c->d_seg_begin;
@@ -536,12 +537,16 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
      * 1.080 vs 1.062 G (3 runs each), profiles/r04/r0_order/. */
     /* r0_order (NNSP_R0_ORDER, development): 0 S2I's and KWS's NN wait for
      * VAD's proj; 1 (default) VAD launched first, nothing waits; 3 S2I and
-     * KWS launched first, VAD's recurrence waits for their proj (1.059 G) */
+     * KWS launched first, VAD's recurrence waits for their proj (1.059 G);
+     * 4 KWS, S2I, VAD and 5 VAD, KWS, S2I, nothing waits */
     static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2}, o_vad_last[3] = {0, 2, 1};
+    static const int o_kws_first[3] = {2, 0, 1}, o_vad_kws[3] = {1, 2, 0};
     const int r0 = r == 0 && c->fused && !c->serial;
     const int vad_first = r0 && c->r0_order == 0;
     const int vad_last = r0 && c->r0_order == 3;
-    const int *order = vad_last ? o_vad_last : (r0 ? o_vad : o_plain);
+    const int *order = vad_last ? o_vad_last
+                     : (r0 && c->r0_order == 4 ? o_kws_first
+                        : (r0 && c->r0_order == 5 ? o_vad_kws : (r0 ? o_vad : o_plain)));
     for (int i = 0; i < 3; ++i) {
         const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];

@@ -96,6 +96,7 @@ typedef struct {
     void *proj_done;           /* non-NULL: recorded on the stream once the prefix FC layers are done
                                   (split path: between proj and recur; fused kernel: after it) */
     void *recur_wait[2];       /* split path: events the recurrence waits for after proj (NULL: none) */
+    int round;                 /* cascade round (0: the chunk's first) */
 } nnsp_segment;
 
 int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int32_t *logits,
