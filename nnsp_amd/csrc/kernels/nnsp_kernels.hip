@@ -1811,7 +1811,16 @@ int nnspk_launch_fe(const FeArgs* a, void* stream) {
     // workgroup -- eight generations, 67 frames per wave: cascade 3 072
     // workgroups 0.948 G, 4 608 0.980, 6 144 0.986-0.998, 9 216 0.992,
     // 12 288 1.016, 18 432 1.008, 24 576 0.992 G; shared FE 2.16 -> 2.09 ms)
-    const long long cap = 256LL * per_cu * 8;
+    // (round 4, the final front end -- 72 VGPRs, ~307 VALU per frame -- paired
+    // A/B over two sweeps, profiles/r04/fe_gens/: shared FE 1.99 ms at eight
+    // generations, 1.95 at six, 1.96 at ten and twelve; cascade 1.171 / 1.183 /
+    // 1.178 / 1.179 G: six generations, 9 216 workgroups, since then)
+    // (NNSP_FE_GENS, development: another number of generations)
+    static const long long gens = [] {
+        const char* e = getenv("NNSP_FE_GENS");
+        return e && atoll(e) > 0 ? atoll(e) : 6LL;
+    }();
+    const long long cap = 256LL * per_cu * gens;
     if (blocks > cap) blocks = cap;
     // cold frames (<= 2 per reset, device-sized list): enough workgroups for
     // about one frame per wave -- their latency sits on each round's critical path
