@@ -355,7 +355,12 @@ static int recur_tseq(const nnsp_segment *seg, int T, int shape)
     if (env > 0) return env > 4 ? 4 : env;
     const int W = seg->seg_len > 0 && seg->seg_len < T ? seg->seg_len : T;
     const int steps = (W + 1) / 2;
-    return steps <= 8 ? 4 : (steps <= 16 ? 2 : 1);
+    /* short segments: VAD 4 tiles per workgroup, S2I and KWS 2 (their
+     * whole-CU pipelines: at 8 NN steps S2I's NN 1.35 -> 1.09 ms, KWS's 1.00 ->
+     * 0.94 ms per chunk; synthetic-weight cascade 0.691 -> 0.701 G, paired,
+     * profiles/r04/synth_tseq/) */
+    if (steps <= 8 && shape == NN_SHAPE_VAD) return 4;
+    return steps <= 16 ? 2 : 1;
 }
 
 int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, const nnsp_segment *seg,
