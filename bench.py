@@ -207,7 +207,7 @@ def dropin_cpu_baseline(net: str, pcm, lib: str | None) -> dict:
             "sample": f"1 stream x {len(pcm)} frames of the speech wav, {reps} passes, one C call per pass"}
 
 
-def dropin_latency(args) -> dict:
+def dropin_latency(args, lib: str | None, build: str | None) -> dict:
     """The drop-in API's single-stream cost: the
     reference's NNSPClass_exec (nn_speech.c:74-127) called frame by frame on
     one stream, as an unchanged single-stream application calls it
@@ -226,7 +226,6 @@ def dropin_latency(args) -> dict:
     T = 1000
     pcm = np.ascontiguousarray(z["speech"][:T * 160].reshape(T, 160), np.int16)
     out = {}
-    lib, build = native_oracle() if not args.no_cpu_baseline else (None, None)
     for net in ("vad", "kws", "s2i"):
         h = _lib.NetHandle(get_net(net, "ref"))
         thr, cnt = np.array([THRESH_PROB], np.int16), np.array([THRESH_CNTS], np.int16)
@@ -271,6 +270,18 @@ def make_engine(net: str, S: int, T: int, acc32: bool, weights: str, window: int
     return NNSPBatch(get_net(net, weights), S, T, acc32=acc32, arm_optimized=arm_optimized)
 
 
+def chunk_step(eng, cascade: bool, T: int, buf, nxt, ran, trig, out3, lookahead: bool = True) -> None:
+    """One timed step: a T-frame chunk of every stream (device buffers).  The
+    cascade writes per frame the NNSP_ID that ran, its trigger and outputs, and
+    the next chunk's front end runs ahead, overlapped with this chunk's nets
+    (tests/test_gpu_benchloop.py runs this same function for parity)."""
+    if cascade:
+        eng.exec_device(buf.data_ptr(), T, ran.data_ptr(), trig.data_ptr(), out3.data_ptr(),
+                        next_ptr=nxt.data_ptr() if (nxt is not None and lookahead) else None, next_T=T)
+    else:
+        eng.exec_device(buf.data_ptr(), T, trig.data_ptr())
+
+
 def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     """Create, warm up and time one workload on this rank's shard."""
     import numpy as np
@@ -298,13 +309,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     ran = torch.empty((S, T), dtype=torch.int8, device="cuda")
 
     def step(buf, nxt=None):
-        if cascade:   # per frame: the NNSP_ID that ran, its trigger and outputs; the
-            # next chunk's front end runs ahead, overlapped with this chunk's nets
-            eng.exec_device(buf.data_ptr(), T, ran.data_ptr(), trig.data_ptr(), out3.data_ptr(),
-                            next_ptr=nxt.data_ptr() if (nxt is not None and not args.no_lookahead) else None,
-                            next_T=T)
-        else:
-            eng.exec_device(buf.data_ptr(), T, trig.data_ptr())
+        chunk_step(eng, cascade, T, buf, nxt, ran, trig, out3, lookahead=not args.no_lookahead)
 
     eng.sync()
     torch.cuda.synchronize()
@@ -462,6 +467,52 @@ def load_profile(args, S: int, weights: str) -> dict | None:
     return None
 
 
+def rank_shard(args, rank: int, world: int) -> tuple[int, int]:
+    """(first global stream, streams) of this rank (nnsp_amd.shard)."""
+    if args.scaling == "weak":
+        per = args.streams or (32768 if args.net == "cascade" else 8192)
+        return shard_streams(rank, world, per_rank=per)
+    return shard_streams(rank, world, total=args.total_streams)
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """``bench.py --gpus N`` started as one plain process: run it again as N
+    ranks under torch.distributed.run (one process per GPU, rendezvous on
+    127.0.0.1) and return their exit status.  Called before this process has
+    touched the GPU; the ranks inherit stdout, where rank 0 writes the one
+    JSON line."""
+    import socket
+
+    with socket.socket() as s:   # a free port for the rendezvous
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    sys.stdout.flush()
+    return subprocess.run(cmd).returncode
+
+
+def print_rank_plan(args, rank: int, world: int, launched: bool, json_fd: int) -> None:
+    """--dry-run: every rank reports its device and stream shard over a gloo
+    group; rank 0 prints them as one JSON line.  Nothing touches the GPU."""
+    s0, S = rank_shard(args, rank, world)
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    me = {"rank": rank, "local_rank": local, "device": local, "first_stream": s0, "streams": S, "pid": os.getpid()}
+    plan = [me]
+    if launched:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo")
+        plan = [None] * world
+        dist.all_gather_object(plan, me)
+        dist.destroy_process_group()
+    if rank == 0:
+        line = {"dry_run": True, "n_gpus": world, "launched_by": "torch.distributed.run" if launched
+                else "plain process", "scaling": args.scaling, "net": args.net, "frames_per_step": args.frames,
+                "ranks": plan}
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -497,23 +548,37 @@ def main() -> None:
     ap.add_argument("--dropin-latency", action="store_true",
                     help="time the drop-in NNSPClass_exec per frame on one stream (GPU) against the oracle on one "
                          "core; prints its own JSON line instead of the throughput line")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks and print their stream-shard plan as one JSON line; no GPU work")
     args = ap.parse_args()
     if args.dropin_latency:
+        # gcc runs before this process touches the GPU (a fork/exec of a
+        # process holding a HIP context is unsafe on this pool)
+        lib, build = native_oracle() if not args.no_cpu_baseline else (None, None)
         import torch
 
         torch.cuda.set_device(0)
-        res = dropin_latency(args)
+        res = dropin_latency(args, lib, build)
         print(json.dumps({"metric": "drop-in NNSPClass_exec latency per 10 ms frame, one stream",
                           "unit": "us/frame", "higher_is_better": False, "nets": res}))
         return
 
     rank, world, local, launched = dist_env()
+    if launched and world != args.gpus:
+        sys.exit(f"bench.py: launched with WORLD_SIZE={world} but --gpus {args.gpus}; the two must agree")
+    if not launched and args.gpus > 1:
+        # one process per GPU: start the ranks as children before anything here
+        # touches the GPU, forward their one JSON line, exit with their status
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     # stdout carries the one JSON line and nothing else: libraries that print
     # banners there (RCCL prints its version at process-group init) write to
     # stderr instead, the line goes to the saved descriptor
     sys.stdout.flush()
     json_fd = os.dup(1)
     os.dup2(2, 1)
+    if args.dry_run:
+        print_rank_plan(args, rank, world, launched, json_fd)
+        return
     # the CPU baseline runs on rank 0 at N=1 only; its pool exists before the GPU does
     pool, cpu = cpu_pool() if rank == 0 and world == 1 and not args.no_cpu_baseline else (None, None)
     import torch
@@ -531,11 +596,7 @@ def main() -> None:
     from nnsp_amd.engine import device_info
 
     _lib.check(_lib.lib().nnsp_set_device(local if launched else 0), "set_device")
-    if args.scaling == "weak":
-        per = args.streams or (32768 if args.net == "cascade" else 8192)
-        s0, S = shard_streams(rank, world, per_rank=per)
-    else:
-        s0, S = shard_streams(rank, world, total=args.total_streams)
+    s0, S = rank_shard(args, rank, world)
     res = run_workload(args, S, s0, args.weights, dist)
     elapsed, frames = reduce_run(dist, res["elapsed"], res["frames"],
                                  device="cuda" if args.dist_backend == "nccl" else "cpu")

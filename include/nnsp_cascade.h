@@ -135,6 +135,45 @@ int nnsp_cascade_last_rounds(nnsp_cascade *c, int max_rounds, int32_t *lists, fl
 /* current_pos_seq of every stream -> host int8 [S]. */
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
 
+/* Whole-stream state export / import between chunks: checkpoint / resume, or
+ * moving streams between cascades (shards) of the same nets and parameters.
+ * One blob of nnsp_cascade_state_bytes() bytes per stream holds what the
+ * reference keeps per stream -- one nnCntrlClass, its PcmBufClass and the
+ * three NNSPClass / FeatureClass / NeuralNetClass states
+ * (evb/src/nnCntrlClass.h:35-45, PcmBufClass.h:9-16, nn_speech.h):
+ *
+ *   nnsp_cascade_stream_hdr                       32 B (below)
+ *   PCM history  int16 [H][160]   the stream's last H frames, oldest first
+ *                                 (PcmBufClass's voice buffer as far back as
+ *                                 the look-backs reach: H = max(frs_vbufBk) + 1)
+ *   STFT tail    int16 [320]      the last two frames (the shared front end's
+ *                                 stftModule.dataBuffer before the next frame)
+ *   look-back features int16 [3][H - 1][40]   per NNSP_ID, the normalised
+ *                                 log-Mel of frames -(H-1) .. -1, which KWS and
+ *                                 S2I read frs_vbufBk frames back
+ *   3 x nnsp_batch blob           per NNSP_ID, nnsp_batch_get_state's layout:
+ *                                 that net's STFT tail, normFeatContext slots
+ *                                 1..5, LSTM h and c, post-processing state
+ *
+ * get waits for the cascade's work; set drops a look-ahead front end (the next
+ * call recomputes its own).  Blobs carry H and a magic number; set refuses
+ * blobs from a cascade with other look-backs (NNSP_EINVAL). */
+typedef struct {
+    uint32_t magic;               /* NNSP_CASCADE_STATE_MAGIC */
+    uint16_t hist_frames;         /* H */
+    uint16_t version;             /* 1 */
+    int16_t current_pos_seq;      /* nnCntrlClass */
+    uint16_t cnt_timeout_kws;
+    uint16_t cnt_timeout_s2i;
+    int16_t reserved0;
+    int8_t frames_since_reset;    /* frames the current net ran since its reset (0, 1, 2 = 2 or more) */
+    int8_t reserved1[15];
+} nnsp_cascade_stream_hdr;
+#define NNSP_CASCADE_STATE_MAGIC 0x3153434eu   /* "NCS1" */
+size_t nnsp_cascade_state_bytes(const nnsp_cascade *c);
+int nnsp_cascade_get_state(nnsp_cascade *c, void *host, int first, int count);
+int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int count);
+
 #ifdef __cplusplus
 }
 #endif

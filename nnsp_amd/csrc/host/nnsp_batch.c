@@ -520,31 +520,59 @@ size_t nnsp_batch_state_bytes(const nnsp_batch *b)
     return 320 * 2 + 200 * 2 + (size_t)nls * b->hs * 6 + sizeof(NnPost);
 }
 
+static StateSeg plain_seg(const void *base, size_t stride, size_t bytes, size_t off)
+{
+    StateSeg g;
+    memset(&g, 0, sizeof g);
+    g.base = (unsigned long long)(uintptr_t)base;
+    g.stride = stride;
+    g.rows = 1;
+    g.row_bytes = (uint32_t)bytes;
+    g.wrap = 1;
+    g.off = (uint32_t)off;
+    return g;
+}
+
+int nnsp_batch_state_segs(const nnsp_batch *b, StateSeg *seg, size_t off, size_t *end)
+{
+    const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
+    const size_t hb = (size_t)nls * b->hs * 2, cb = (size_t)nls * b->hs * 4;
+    seg[0] = plain_seg(b->d_tail, 640, 640, off);
+    seg[1] = plain_seg(b->d_prev5, 400, 400, off + 640);
+    seg[2] = plain_seg(b->d_h, hb, hb, off + 1040);
+    seg[3] = plain_seg(b->d_c, cb, cb, off + 1040 + hb);
+    seg[4] = plain_seg(b->d_post, sizeof(NnPost), sizeof(NnPost), off + 1040 + hb + cb);
+    *end = off + nnsp_batch_state_bytes(b);
+    return 5;
+}
+
+int nnsp_state_xfer(StateCopy *sc, void *host, void *stream)
+{
+    if (sc->count == 0) return 0;
+    void *d = NULL;
+    const size_t n = (size_t)sc->count * sc->per;
+    int e = nnspk_malloc(&d, n);
+    if (e) return e;
+    if (!sc->to_blob) e = nnspk_h2d(d, host, n, stream);
+    if (!e) e = nnspk_launch_state_copy(sc, d, stream);
+    if (!e && sc->to_blob) e = nnspk_d2h(host, d, n, stream);
+    if (!e) e = nnspk_sync(stream);
+    nnspk_free(d);
+    return e;
+}
+
 static int state_xfer(nnsp_batch *b, void *host, int first, int count, int to_dev)
 {
     if (!b || !host || first < 0 || count < 0 || first + count > b->S) return NNSP_EINVAL;
-    const int nls = b->im.img.n_lstm ? b->im.img.n_lstm : 1;
-    const size_t per = nnsp_batch_state_bytes(b);
-    uint8_t *h = (uint8_t *)host;
-    for (int i = 0; i < count; ++i) {
-        const size_t s = (size_t)(first + i);
-        uint8_t *p = h + per * i;
-        struct { void *dev; size_t n; } seg[5] = {
-            {b->d_tail + s * 320, 640},
-            {b->d_prev5 + s * 200, 400},
-            {b->d_h + s * nls * b->hs, (size_t)nls * b->hs * 2},
-            {b->d_c + s * nls * b->hs, (size_t)nls * b->hs * 4},
-            {b->d_post + s, sizeof(NnPost)},
-        };
-        for (int k = 0; k < 5; ++k) {
-            if (to_dev)
-                TRY(nnspk_h2d(seg[k].dev, p, seg[k].n, b->stream));
-            else
-                TRY(nnspk_d2h(p, seg[k].dev, seg[k].n, b->stream));
-            p += seg[k].n;
-        }
-    }
-    return nnspk_sync(b->stream);
+    StateCopy sc;
+    memset(&sc, 0, sizeof sc);
+    size_t end = 0;
+    sc.nseg = nnsp_batch_state_segs(b, sc.seg, 0, &end);
+    sc.per = end;
+    sc.first = first;
+    sc.count = count;
+    sc.to_blob = !to_dev;
+    return nnsp_state_xfer(&sc, host, b->stream);
 }
 
 int nnsp_batch_get_state(nnsp_batch *b, void *host, int first, int count)

@@ -785,9 +785,12 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
              * front end to drain and ran after it (~190 us past its end);
              * 2 for round 1's end.  A/B 1.099 / 1.149 / 1.111 G (modes 0 / 1
              * / 2, 2 runs each), profiles/r04/ahead_mode/ */
-            if (ahead && !ahead_launched && r >= (c->ahead_mode ? 1 : 0)) {
+            /* (ahead implies fused && !serial: the only mode in which round 1
+             * records ev_r1proj and every round records ev_rnd) */
+            const int am = c->fused && !c->serial ? c->ahead_mode : 0;
+            if (ahead && !ahead_launched && r >= (am ? 1 : 0)) {
                 for (int n = 0; n < 3; ++n)
-                    TRY(nnspk_stream_wait(c->stream, c->ahead_mode == 1 ? c->ev_r1proj[n] : c->ev_rnd[r & 1][n]));
+                    TRY(nnspk_stream_wait(c->stream, am == 1 ? c->ev_r1proj[n] : c->ev_rnd[r & 1][n]));
                 const int q = (int)((k + 1) & 1);
                 TRY(ahead_read(c, q, 1)); /* slot q's last front end (two chunks ago) is long done */
                 TRY(nnspk_event_record(c->ev_ahead[q][0], c->stream));
@@ -963,4 +966,101 @@ int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos)
         for (int s = 0; s < c->S; ++s) pos[s] = (int8_t)h[s].pos;
     free(h);
     return e;
+}
+
+/* ---- per-stream state export / import (include/nnsp_cascade.h) ---- */
+_Static_assert(sizeof(nnsp_cascade_stream_hdr) == 32, "nnsp_cascade_stream_hdr: 32 bytes");
+_Static_assert(sizeof(CascState) == 8, "CascState: the header's 8 bytes at offset 8");
+
+size_t nnsp_cascade_state_bytes(const nnsp_cascade *c)
+{
+    if (!c) return 0;
+    size_t n = sizeof(nnsp_cascade_stream_hdr) + (size_t)c->H * 320 + 640 + 3 * (size_t)(c->H - 1) * 80;
+    for (int i = 0; i < 3; ++i) n += nnsp_batch_state_bytes(c->net[i]);
+    return n;
+}
+
+/* the segments of a stream's blob; valid between chunks (after any work) */
+static void cascade_state_segs(const nnsp_cascade *c, StateCopy *sc)
+{
+    const size_t H = (size_t)c->H;
+    size_t off = 0;
+    int k = 0;
+    StateSeg *g = sc->seg;
+    memset(g, 0, sizeof sc->seg);
+    /* controller state at header offset 8 (CascState: pos, cnt_kws, cnt_s2i, pad) and frames since the reset at 16 */
+    g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_st, sizeof(CascState), 0, 1, sizeof(CascState), 0, 1, 8, 0};
+    g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_fresh, 1, 0, 1, 1, 0, 1, 16, 0};
+    off = sizeof(nnsp_cascade_stream_hdr);
+    /* the history the next chunk reads: d_hist[chunk % 3] */
+    g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_hist[c->chunk % 3], H * 320, 0, 1, (uint32_t)(H * 320), 0, 1,
+                        (uint32_t)off, 0};
+    off += H * 320;
+    g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_stail, 640, 0, 1, 640, 0, 1, (uint32_t)off, 0};
+    off += 640;
+    /* ring slots abs0 - (H - 1) .. abs0 - 1, oldest first */
+    for (int n = 0; n < 3; ++n) {
+        if (H > 1)
+            g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_nring[n], (unsigned long long)c->ring * 80, 80,
+                                (uint32_t)(H - 1), 80, (uint32_t)((c->abs0 - (int)(H - 1) + c->ring) % c->ring),
+                                (uint32_t)c->ring, (uint32_t)off, 0};
+        off += (H - 1) * 80;
+    }
+    for (int n = 0; n < 3; ++n) k += nnsp_batch_state_segs(c->net[n], g + k, off, &off);
+    sc->nseg = k;
+    sc->per = off;
+}
+
+static int cascade_quiesce(nnsp_cascade *c)
+{
+    TRY(nnspk_sync(c->stream));
+    for (int n = 0; n < 3; ++n) TRY(nnspk_sync(c->ns[n]));
+    TRY(book_take(c));
+    for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
+    return 0;
+}
+
+int nnsp_cascade_get_state(nnsp_cascade *c, void *host, int first, int count)
+{
+    if (!c || !host || first < 0 || count < 0 || first + count > c->S) return NNSP_EINVAL;
+    TRY(cascade_quiesce(c));
+    StateCopy sc;
+    memset(&sc, 0, sizeof sc);
+    cascade_state_segs(c, &sc);
+    sc.first = first;
+    sc.count = count;
+    sc.to_blob = 1;
+    memset(host, 0, (size_t)count * sc.per);
+    TRY(nnsp_state_xfer(&sc, host, c->stream));
+    for (int i = 0; i < count; ++i) {
+        nnsp_cascade_stream_hdr *h = (nnsp_cascade_stream_hdr *)((char *)host + (size_t)i * sc.per);
+        h->magic = NNSP_CASCADE_STATE_MAGIC;
+        h->hist_frames = (uint16_t)c->H;
+        h->version = 1;
+    }
+    return 0;
+}
+
+int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int count)
+{
+    if (!c || !host || first < 0 || count < 0 || first + count > c->S) return NNSP_EINVAL;
+    StateCopy sc;
+    memset(&sc, 0, sizeof sc);
+    cascade_state_segs(c, &sc);
+    for (int i = 0; i < count; ++i) {
+        const nnsp_cascade_stream_hdr *h = (const nnsp_cascade_stream_hdr *)((const char *)host + (size_t)i * sc.per);
+        if (h->magic != NNSP_CASCADE_STATE_MAGIC || h->hist_frames != c->H || h->version != 1) {
+            nnsp_set_error("nnsp_cascade_set_state: blob %d is not a state of a cascade with %d history frames", i,
+                           c->H);
+            return NNSP_EINVAL;
+        }
+    }
+    TRY(cascade_quiesce(c));
+    cascade_state_segs(c, &sc);
+    sc.first = first;
+    sc.count = count;
+    sc.to_blob = 0;
+    TRY(nnsp_state_xfer(&sc, (void *)host, c->stream));
+    c->pre_pcm = NULL; /* a look-ahead front end ran on the old state: the next call recomputes */
+    return 0;
 }

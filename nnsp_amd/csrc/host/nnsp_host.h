@@ -106,6 +106,13 @@ int nnsp_batch_run(nnsp_batch *b, const int16_t *pcm, int T, int16_t *trig, int3
 int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, const nnsp_segment *seg,
                       void *stream);
 
+/* per-stream state blobs (StateCopy): the batch's segments appended at blob
+ * offset off (returns the count appended, sets *end past them), and the
+ * gather / scatter of streams first .. first + count - 1 through a device
+ * staging buffer to / from host [count][sc->per] */
+int nnsp_batch_state_segs(const nnsp_batch *b, StateSeg *seg, size_t off, size_t *end);
+int nnsp_state_xfer(StateCopy *sc, void *host, void *stream);
+
 void nnsp_set_error(const char *fmt, ...);
 const char *nnsp_last_error(void);
 

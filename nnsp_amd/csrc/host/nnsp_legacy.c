@@ -199,8 +199,11 @@ static img_node *img_find(const void *k0, const void *k1, const void *k2, const 
     return NULL;
 }
 
+/* blob (may be NULL): the tables' host copy, owned by the new entry -- freed
+ * here when the entry cannot be built */
 static img_node *img_add(const void *k0, const void *k1, const void *k2, const void *k3, const int *ik,
-                         uint64_t bytes, const nnsp_layer_desc *L, int nl, int out_linear)
+                         uint64_t bytes, const nnsp_layer_desc *L, int nl, int out_linear, uint8_t *blob,
+                         size_t blob_n)
 {
     int count = 0;
     img_node *last = NULL, *before_last = NULL;
@@ -210,7 +213,11 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
         last = n;
     }
     if (count >= IMG_MAX && last) { /* evict the least recently used (nothing in flight uses it) */
-        CK(nnspk_sync(G.stream));
+        const int se = nnspk_sync(G.stream);
+        if (se) {
+            free(blob);
+            fail(se, "nnspk_sync");
+        }
         if (before_last) before_last->next = NULL;
         else g_imgs = NULL;
         nnsp_image_free(&last->im);
@@ -218,7 +225,10 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
         free(last);
     }
     img_node *n = (img_node *)calloc(1, sizeof *n);
-    if (!n) fail(NNSP_ENOMEM, "image cache entry");
+    if (!n) {
+        free(blob);
+        fail(NNSP_ENOMEM, "image cache entry");
+    }
     n->key[0] = k0; n->key[1] = k1; n->key[2] = k2; n->key[3] = k3;
     memcpy(n->ikey, ik, sizeof n->ikey);
     n->bytes = bytes;
@@ -227,9 +237,12 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
     if (e) {
         nnsp_image_free(&n->im);
         free(n);
+        free(blob);
         fail(e, "nnsp_image_build/upload");
     }
     n->out_linear = out_linear;
+    n->blob = blob;
+    n->blob_n = blob_n;
     n->next = g_imgs;
     g_imgs = n;
     return n;
@@ -317,10 +330,7 @@ static img_node *net_image(const NeuralNetClass *net)
     uint8_t *blob = (uint8_t *)malloc(nb ? nb : 1);
     if (!blob) fail(NNSP_ENOMEM, "image cache tables copy");
     tables_copy(blob, L, nl);
-    n = img_add(net, NULL, NULL, NULL, ik, 0, L, nl, lin);
-    n->blob = blob;
-    n->blob_n = nb;
-    return n;
+    return img_add(net, NULL, NULL, NULL, ik, 0, L, nl, lin, blob, nb);
 }
 
 /* LSTM h/c of a NeuralNetClass <-> device rows [l][hs] (hs: the widest
@@ -419,7 +429,7 @@ static int run_layer(int type, int acc32, int16_t *p_output, int8_t *p_kernel, i
     const int ik[8] = {type, acc32, dim_output, dim_input, qk, qb, qi, (qir << 4) | d.act};
     const uint64_t bytes = layer_bytes_hash(1469598103934665603ULL, &d) ^ (d.portable ? 0x9e3779b97f4a7c15ULL : 0);
     img_node *n = img_find(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes);
-    if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes, &d, 1, d.act == 3);
+    if (!n) n = img_add(p_kernel, p_kernel_rec, p_bias, (void *)(intptr_t)0x1a7e, ik, bytes, &d, 1, d.act == 3, NULL, 0);
     int16_t in_pad[NN_MAX_K];
     memset(in_pad, 0, sizeof in_pad);
     memcpy(in_pad, input, (size_t)dim_input * 2);

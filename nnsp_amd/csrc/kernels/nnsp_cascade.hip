@@ -196,9 +196,52 @@ __global__ __launch_bounds__(256) void hist_roll_kernel(int16_t* dst, const int1
     }
 }
 
+// Per-stream state blobs (StateCopy, nnsp_kabi.h): one workgroup per stream,
+// its threads over each segment's bytes -- dwords when the row and both ends
+// are 4-byte aligned (all but the controller's 1-byte frames-since-reset).
+__global__ __launch_bounds__(256) void state_copy_kernel(StateCopy sc, uint8_t* blob) {
+    for (int i = blockIdx.x; i < sc.count; i += gridDim.x) {
+        const unsigned long long s = (unsigned long long)(sc.first + i);
+        uint8_t* b = blob + (size_t)i * sc.per;
+        for (int k = 0; k < sc.nseg; ++k) {
+            const StateSeg& g = sc.seg[k];
+            const bool w4 = ((g.row_bytes | g.off | g.base | g.stride | g.row_pitch) & 3) == 0;
+            const uint32_t unit = w4 ? 4 : 1, per_row = g.row_bytes / unit;
+            for (uint32_t u = threadIdx.x; u < g.rows * per_row; u += blockDim.x) {
+                const uint32_t r = u / per_row, o = (u - r * per_row) * unit;
+                uint8_t* dev = reinterpret_cast<uint8_t*>(g.base + s * g.stride +
+                                                          (unsigned long long)((g.row0 + r) % g.wrap) * g.row_pitch) + o;
+                uint8_t* bl = b + g.off + (size_t)r * g.row_bytes + o;
+                if (w4) {
+                    if (sc.to_blob)
+                        *reinterpret_cast<uint32_t*>(bl) = *reinterpret_cast<const uint32_t*>(dev);
+                    else
+                        *reinterpret_cast<uint32_t*>(dev) = *reinterpret_cast<const uint32_t*>(bl);
+                } else {
+                    if (sc.to_blob)
+                        *bl = *dev;
+                    else
+                        *dev = *bl;
+                }
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int nnspk_launch_state_copy(const StateCopy* sc, void* blob, void* stream) {
+    if (sc->count <= 0) return 0;
+    if (sc->nseg < 0 || sc->nseg > NNSP_STATE_SEGS) return ok(hipErrorInvalidValue);
+    for (int k = 0; k < sc->nseg; ++k)
+        if (!sc->seg[k].wrap || sc->seg[k].off + (unsigned long long)sc->seg[k].rows * sc->seg[k].row_bytes > sc->per)
+            return ok(hipErrorInvalidValue);
+    const int blocks = sc->count < 4096 ? sc->count : 4096;
+    hipLaunchKernelGGL(state_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, *sc, (uint8_t*)blob);
+    return ok(hipGetLastError());
+}
 
 int nnspk_launch_casc_begin(const CascArgs* a, void* stream) {
     if (a->S <= 0) return 0;

@@ -1175,9 +1175,8 @@ static_assert(PIPE_KT == 4, "the post wave describes one tile per 16 lanes");
 //   * the final h, c of a tile: stored to HBM by the LSTM waves at its last
 //     step; for a stream whose net was reset (known to the post wave 4
 //     iterations later) the FC waves overwrite them with the zero state when
-//     they roll the tile's feature context.  The LSTM waves' wait for the x
-//     rows they load at the next step (vector memory completes in order) has
-//     completed those stores before then;
+//     they roll the tile's feature context, after an explicit vmcnt(0) wait
+//     and a barrier behind the loop;
 //   * post-processing and controller state: per tile in LDS (loaded once for
 //     all tiles at the start), the post wave switches at the tile's first step
 //     and stores the tile's state and bookkeeping at its last.
@@ -1751,6 +1750,12 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     if constexpr (!MT) {
         if (post_w) post_end(0);
         __syncthreads();
+    } else {
+        // the earlier tiles' final h / c went out from the LSTM waves at their
+        // last step; the zero state of reset streams below must land after
+        // them: every wave's stores complete (vmcnt(0)) before the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
     }
     // ---- the tiles' ends, after the loop (inside it, their pointers and
     //      counters cost every role's loop SGPRs, spilled to VGPR lanes).
@@ -1768,9 +1773,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // LSTM state: the last tile's from LDS (step total-1 wrote h[total & 1]);
     // the earlier tiles' went out from the LSTM waves at their last step.  A
     // stream whose net was reset gets the zero state
-    // (NeuralNetClass_setDefault) -- over what the LSTM waves stored: their
-    // wait for the x rows of two steps later completed those stores (vector
-    // memory completes in order)
+    // (NeuralNetClass_setDefault) -- over what the LSTM waves stored, which
+    // completed before the barrier above (MT)
     const int tl = nk - 1;
     const int hb = total & 1;
     for (int idx = tid; idx < 16 * N; idx += TD) {

@@ -343,6 +343,25 @@ int nnspk_launch_casc_reset(CascState *st, int16_t *hist, int hist_frames, int16
 int nnspk_launch_hist_roll(int16_t *dst, const int16_t *src, const int16_t *pcm, int S, int T,
                            int hist_frames, void *stream);
 
+/* ---- per-stream state export / import (nnsp_batch_get_state, nnsp_cascade_get_state) ----
+ * A stream's blob is a list of segments.  Segment k of stream s is `rows` rows
+ * of `row_bytes` bytes: row r lies at base + s * stride + ((row0 + r) % wrap) *
+ * row_pitch on the device (wrap: a ring's slot count; 1 for plain arrays) and
+ * at off + r * row_bytes in the blob.  The kernel gathers the blobs of streams
+ * first .. first + count - 1 into blob [count][per] (to_blob) or scatters them
+ * back. */
+#define NNSP_STATE_SEGS 24
+typedef struct {
+    unsigned long long base, stride, row_pitch;
+    uint32_t rows, row_bytes, row0, wrap, off, pad_;
+} StateSeg;
+typedef struct {
+    StateSeg seg[NNSP_STATE_SEGS];
+    int32_t nseg, first, count, to_blob;
+    unsigned long long per;
+} StateCopy;
+int nnspk_launch_state_copy(const StateCopy *sc, void *blob, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -107,6 +107,11 @@ struct FeTables {
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
 };   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
 static_assert(sizeof(FeTables) % 16 == 0, "FeTables: copied as 16-byte chunks");
+// fe_kernel's LDS (the tables + FE_WPG frame buffers), granted in 512-byte
+// blocks, must let 24 / FE_WPG workgroups share a CU's 160 KB: the launch
+// bounds (six waves per SIMD) and the grid's generations assume that many
+static_assert(((sizeof(FeTables) + FE_WPG * (FE_X_DW + FE_P_DW) * 4 + 511) / 512) * 512 * (24 / FE_WPG) <= 160 * 1024,
+              "fe_kernel: LDS per workgroup no longer fits 24 / FE_WPG workgroups per CU");
 
 // the per-net normalisation constants (norm[]; with the Mel pad at 264 the
 // tables and buffers stay within 160 KB / 6)

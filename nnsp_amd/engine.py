@@ -205,6 +205,20 @@ class NNSPCascade:
             _lib.check(n, "nnsp_cascade_last_rounds")
         return lists[:n], fe[:n], nn[:n]
 
+    def get_state(self, first: int = 0, count: int | None = None) -> np.ndarray:
+        """Per-stream state blobs [count][state_bytes] (include/nnsp_cascade.h:
+        header, PCM history, STFT tail, look-back features, 3 net states)."""
+        count = self.S - first if count is None else count
+        per = _lib.lib().nnsp_cascade_state_bytes(self.h)
+        buf = np.zeros((count, per), np.uint8)
+        _lib.check(_lib.lib().nnsp_cascade_get_state(self.h, _lib.ptr(buf), first, count), "nnsp_cascade_get_state")
+        return buf
+
+    def set_state(self, buf: np.ndarray, first: int = 0) -> None:
+        buf = np.ascontiguousarray(buf, np.uint8)
+        _lib.check(_lib.lib().nnsp_cascade_set_state(self.h, _lib.ptr(buf), first, buf.shape[0]),
+                   "nnsp_cascade_set_state")
+
     def positions(self) -> np.ndarray:
         pos = np.zeros(self.S, np.int8)
         _lib.check(_lib.lib().nnsp_cascade_positions(self.h, _lib.ptr(pos)), "positions")

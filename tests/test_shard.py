@@ -67,3 +67,52 @@ def test_gloo_world2_matches_unsharded(tmp_path, mode):
     for k, name in enumerate(("ran", "det", "o3")):
         np.testing.assert_array_equal(z[name], np.concatenate([r[k] for r in ref], axis=1), err_msg=name)
     assert (z["ran"] != 1).any(), "no stream left VAD: the comparison is vacuous"
+
+
+def _bench_dry_run(args, env=None):
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run"] + args,
+                       env=env, timeout=180, capture_output=True, text=True)
+    return r
+
+
+@pytest.mark.parametrize("gpus,scaling", [(2, "weak"), (2, "strong"), (4, "weak")])
+def test_bench_gpus_n_launches_n_ranks(gpus, scaling):
+    """``python bench.py --gpus N`` (a plain launch, as the driver may start it)
+    runs N ranks under torch.distributed.run itself; --dry-run makes each rank
+    report its device and stream shard over gloo without touching a GPU.
+    stdout carries exactly one JSON line."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = _bench_dry_run(["--gpus", str(gpus), "--scaling", scaling], env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    plan = __import__("json").loads(lines[0])
+    assert plan["n_gpus"] == gpus and plan["launched_by"] == "torch.distributed.run"
+    ranks = plan["ranks"]
+    assert [p["rank"] for p in ranks] == list(range(gpus))
+    assert sorted(p["device"] for p in ranks) == list(range(gpus))
+    assert len({p["pid"] for p in ranks}) == gpus, "the ranks must be separate processes"
+    covered = []
+    for p in ranks:
+        assert (p["first_stream"], p["streams"]) == shard_streams(
+            p["rank"], gpus, **({"per_rank": 32768} if scaling == "weak" else {"total": 262144}))
+        covered += list(range(p["first_stream"], p["first_stream"] + p["streams"]))
+    assert len(covered) == len(set(covered)), "shards overlap"
+    assert len(covered) == (32768 * gpus if scaling == "weak" else 262144)
+
+
+def test_bench_n1_plan_and_world_mismatch():
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = _bench_dry_run([], env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plan = __import__("json").loads(r.stdout)
+    assert plan["n_gpus"] == 1 and plan["launched_by"] == "plain process"
+    assert plan["ranks"][0]["first_stream"] == 0 and plan["ranks"][0]["streams"] == 32768
+    # under torch.distributed.run, a world size that disagrees with --gpus is refused
+    env.update(RANK="0", WORLD_SIZE="2", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+    r = _bench_dry_run(["--gpus", "4"], env)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
