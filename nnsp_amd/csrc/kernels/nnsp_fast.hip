@@ -44,7 +44,19 @@ using namespace nnsp;
 #define P_ASTRIDE 264   // int16 per row of a proj activation buffer
 #define P_UNION 1920    // context frames of a tile: G streams x (32/G + 4) frames x 40 features (int16)
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
-#define R_CW 128        // int32 per row of the c buffer
+#define R_CW 128        // int32 per row of the c buffer (before cstride)
+
+// int32 row stride of a [16 streams][units] cell-state buffer: twice an odd
+// number, so that the 32 lanes of a ds_read_b32 / ds_write_b32 lane group
+// (q = 0, 1 or 2, 3 and the 16 streams sc) reaching unit 4 rt + q of row sc
+// hit bank (stride * sc + 4 rt + q) mod 32 -- all 32 distinct (MI355X_MICROARCH
+// LDS table: b32 accesses bank by dword mod 32 in two groups of 32 lanes).  A
+// stride of 64 (KWS) put the 16 streams of a unit on one bank: 16-way
+// conflicts on every cell-state load and store (round 4 PMC: 5.0 conflict
+// cycles per LDS instruction in KWS's recurrence)
+__host__ __device__ constexpr int cstride(int units) {
+    return ((units + 1) / 2) % 2 ? (units + 1) / 2 * 2 : (units + 1) / 2 * 2 + 2;
+}
 
 // ---------------------------------------------------------------------------
 // Net shapes.  NRT == 0: generic (read from the NnLayer table at run time).
@@ -816,7 +828,7 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
 template <class SH>
 struct alignas(16) RecTile {
     static constexpr int RS = SH::generic ? R_STRIDE : 64 * SH::NKR + 8;
-    static constexpr int CW = SH::generic ? R_CW : (SH::NW + 3) / 4 * 4;
+    static constexpr int CW = cstride(SH::generic ? R_CW : SH::NW);
     int16_t h[2][16][RS];     // LSTM h, ping-pong across steps
     int16_t act[2][16][RS];   // tail wave: FC activations, ping-pong across layers
     int32_t c[16][CW];
@@ -1128,7 +1140,7 @@ struct PipeCfg {
 template <class SH>
 struct alignas(16) PipeTile {
     static constexpr int RS = 64 * SH::NKR + 8;
-    static constexpr int CW = (SH::NW + 3) / 4 * 4;
+    static constexpr int CW = cstride(SH::NW);
     int16_t h[2][16][RS];
     int16_t a2[2][16][RS];
     int16_t a3[2][16][RS];
@@ -1153,6 +1165,7 @@ struct alignas(16) PipeTile {
     int16_t po[2][16][4];
 };
 static_assert(PIPE_KT == 4, "the post wave describes one tile per 16 lanes");
+static_assert(cstride(28) == 30 && cstride(64) == 66 && cstride(72) == 74 && cstride(128) == 130, "cstride");
 
 //
 // Fused control (cascade, ca.st non-NULL): the post wave also runs the
