@@ -404,6 +404,11 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
           "valu_busy": fe_prof.get("valu_busy"),
           "valu_busy_how": "SQ_ACTIVE_INST_VALU x 4 / (1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs), the kernel's PMC pass",
           "valu_insts_per_frame": (fe_prof["SQ_INSTS_VALU"] / fe_frames) if fe_prof.get("SQ_INSTS_VALU") else None,
+          # issue-cost-weighted: the instructions' measured SIMD cycles, not one quad-cycle each
+          # (profiles/fe_valu_mix.json from profiles/r05/fe_valu_mix.py: per-opcode microbench costs x the
+          # frame loop's static mix -> average cycles per VALU instruction) x SQ_INSTS_VALU over the
+          # launch's SIMD-cycles
+          **fe_occupancy(fe_prof),
           "clock_ghz_pmc": fe_prof.get("clock_ghz")}
     # NN: MACs x 2 ops x inferences / the NN kernels' device time
     if cascade:
@@ -453,6 +458,21 @@ def roofline_blocks(args, res: dict, info: dict, profile: dict | None) -> tuple[
                "frac": nn["frac"], "traffic": nn_traffic, "avg_launch_ms": nn_ms, "work": nn["work"]}
         return dom, {"fe": fe, "nn": nn}
     return fe, {"nn": nn}
+
+
+def fe_occupancy(fe_prof: dict) -> dict:
+    try:
+        with open(os.path.join(ROOT, "profiles", "fe_valu_mix.json")) as f:
+            mix = json.load(f)
+        avg = float(mix["avg_cycles_per_valu"])
+        simd_cycles = 1024 * fe_prof["GRBM_GUI_ACTIVE"] / 8
+        occ = fe_prof["SQ_INSTS_VALU"] * avg / simd_cycles
+    except Exception:
+        return {"valu_occupancy": None}
+    return {"valu_occupancy": occ, "valu_avg_issue_cycles": avg,
+            "valu_occupancy_how": "SQ_INSTS_VALU x avg SIMD cycles per VALU instruction (frame-loop opcode mix x "
+                                  "microbench issue costs, profiles/fe_valu_mix.json) / (1024 SIMDs x "
+                                  "GRBM_GUI_ACTIVE / 8 XCDs)"}
 
 
 def load_profile(args, S: int, weights: str) -> dict | None:

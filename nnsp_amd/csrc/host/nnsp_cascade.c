@@ -84,6 +84,8 @@ struct nnsp_cascade {
                                        chunk k counts into block k & 1 and clears block (k + 1) & 1 */
     void *stream;                   /* front end, control; the nets' work forks off it */
     void *ns[3];                    /* per net id: segment features + NN of a round */
+    void *own_ns[3];                /* per net id: a cascade-owned high-priority stream used as ns[n]
+                                       (NNSP_NET_PRIO bit n, development), else NULL */
     void *ev[2];
     void *ev_fe[2];                 /* shared front end */
     void *ev_fork, *ev_join[3];
@@ -221,6 +223,14 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
          * hardware queues (HIP's default) the look-ahead front end on
          * c->stream never shares an in-order queue with a net's rounds */
         c->ns[n] = nets[n]->stream;
+        {   /* NNSP_NET_PRIO (development): bit n = net n's rounds on a high-priority stream of the
+             * cascade's own, so that its workgroups are dispatched ahead of the other nets' */
+            const char *pe = getenv("NNSP_NET_PRIO");
+            if (pe && (atoi(pe) >> n) & 1) {
+                if ((e = nnspk_stream_create_prio(&c->own_ns[n], 1))) goto fail;
+                c->ns[n] = c->own_ns[n];
+            }
+        }
         if ((e = nnspk_event_create(&c->ev_join[n])) || (e = nnspk_event_create(&c->ev_rnd[0][n])) ||
             (e = nnspk_event_create(&c->ev_rnd[1][n])))
             goto fail;
@@ -385,7 +395,11 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
         nnspk_event_destroy(c->ev_rnd[1][n]);
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i) nnspk_event_destroy(c->ev_t[r][n][i]);
-        c->ns[n] = NULL; /* the batch's stream, owned by the batch */
+        c->ns[n] = NULL; /* the batch's stream, owned by the batch (or own_ns[n]) */
+        if (c->own_ns[n]) {
+            nnspk_sync(c->own_ns[n]);
+            nnspk_stream_destroy(c->own_ns[n]);
+        }
     }
     nnspk_stream_destroy(c->stream);
     nnspk_event_destroy(c->ev_book);

@@ -289,6 +289,7 @@ const char *nnspk_error_string(int e);
 int nnspk_stream_create(void **s);
 /* high != 0: the device's greatest stream priority (its kernels' workgroups
  * are dispatched ahead of normal-priority streams' when both wait) */
+int nnspk_stream_create_prio(void **s, int high);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
 int nnspk_event_destroy(void *e);

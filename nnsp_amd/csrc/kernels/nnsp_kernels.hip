@@ -2043,6 +2043,12 @@ int nnspk_set_device(int d) { return ok(hipSetDevice(d)); }
 int nnspk_get_device(int* d) { return ok(hipGetDevice(d)); }
 const char* nnspk_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 int nnspk_stream_create(void** s) { return ok(hipStreamCreateWithFlags((hipStream_t*)s, hipStreamNonBlocking)); }
+int nnspk_stream_create_prio(void** s, int high) {
+    int least = 0, greatest = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (e != hipSuccess) return ok(e);
+    return ok(hipStreamCreateWithPriority((hipStream_t*)s, hipStreamNonBlocking, high ? greatest : least));
+}
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }
