@@ -40,7 +40,8 @@ using namespace nnsp;
 #ifndef NNSP_PROBES
 #define NNSP_PROBES 0
 #endif
-#define TT_BYTES 1024   // LDS copy of nnsp_tbl_tanh1 (tanh_q15s), behind the staged A fragments
+#define TT_BYTES ACT_BYTES   // LDS copy of nnsp_tbl_act (act_q15) at LDS offset 0, before the staged A fragments
+                               // (a compile-time address: the lookups need no base add)
 #define P_ASTRIDE 264   // int16 per row of a proj activation buffer
 #define P_UNION 1920    // context frames of a tile: G streams x (32/G + 4) frames x 40 features (int16)
 #define R_STRIDE 136    // int16 per row of recur h / activation buffers
@@ -162,7 +163,7 @@ __device__ __forceinline__ void stage_weights(uint8_t* dst, const uint8_t* src, 
 // columns of the next layer (recur's stage buffers).
 template <bool ACC32, int NRT, int NKT, int ACT, int ROWS, int MAXKT, bool PAD = false>
 __device__ __forceinline__ void fc_layer(const NnLayer& Ly, const uint8_t* A, const EpRow* ep, const int16_t* in,
-                                         int in_stride, int16_t* out, int out_stride, const int16_t* tt, int lane) {
+                                         int in_stride, int16_t* out, int out_stride, const uint8_t* tt, int lane) {
     const int nrt = NRT > 0 ? NRT : Ly.nrt;
     const int nkt = NKT > 0 ? NKT : Ly.nkt;
     const int act = ACT >= 0 ? ACT : Ly.act;
@@ -360,8 +361,8 @@ __device__ int32_t nnsp_proj_neg1 = -1;   // the list entry of a tile slot past 
 template <class SH, bool ACC32, int GT>
 __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) {   // <= 128 VGPRs: 4 waves per SIMD
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t* W = smem;                                           // staged A fragments
-    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    uint8_t* W = smem + TT_BYTES;                                           // staged A fragments
+    const uint8_t* tt = smem;   // act_q15 tables
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
     constexpr bool GEN = SH::generic;
     using PW = ProjWave<SH, GEN ? 1 : GT>;
@@ -398,7 +399,8 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
     if (pwc) pwc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, false);
-    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
+    for (int i = threadIdx.x; i < TT_BYTES / 16; i += blockDim.x)
+        reinterpret_cast<int4*>(smem)[i] = reinterpret_cast<const int4*>(nnsp_tbl_act)[i];
     __syncthreads();
     if (pwc) pwc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     int ntile_run = 0;
@@ -858,15 +860,16 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
     // tile = 16 consecutive entries of the stream list (identity when list == NULL)
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
     if ((int)(blockIdx.x * (blockDim.x / (64 * RW))) * 16 >= nrow) return;   // whole workgroup past the list
-    uint8_t* W = smem;
-    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    uint8_t* W = smem + TT_BYTES;
+    const uint8_t* tt = smem;   // act_q15 tables
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
     using RT = RecTile<SH>;
     constexpr int R_STRIDE_ = RT::RS;
     RT* tiles = reinterpret_cast<RT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true);
-    for (int i = threadIdx.x; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
+    for (int i = threadIdx.x; i < TT_BYTES / 16; i += blockDim.x)
+        reinterpret_cast<int4*>(smem)[i] = reinterpret_cast<const int4*>(nnsp_tbl_act)[i];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int tpw = blockDim.x / (64 * RW);
     const int tl = wv / RW, g = wv - tl * RW;   // tile in workgroup, wave in tile
@@ -967,11 +970,11 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
                                     const int64_t pre = x + hx + er[i].cst;
                                     v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                                 }
-                                gt[i] = i == 1 ? tanh_q15s(v, tt) : sigmoid_q15s(v, tt);
+                                gt[i] = (int16_t)(i == 1 ? act_q15<0>(v, tt) : act_q15<1>(v >> 1, tt));
                             }
                             const int32_t c_old = R.c[sc][u];
                             const int32_t c_new = sat32(((int64_t)gt[0] * gt[1] + (int64_t)gt[2] * c_old) >> 15);
-                            const int16_t hv = sat16(((int32_t)tanh_q15s(c_new, tt) * gt[3]) >> 15);
+                            const int16_t hv = sat16((act_q15<0>(c_new, tt) * gt[3]) >> 15);
                             if (active) R.c[sc][u] = c_new;
                             R.h[cur ^ 1][sc][u] = active ? hv : R.h[cur][sc][u];   // h after all groups (T6)
                         }
@@ -1229,13 +1232,14 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     if (wgc) wgc[0] = (long long)__builtin_amdgcn_s_memrealtime();
     constexpr int TD = 64 * CF::NWV;
     const int tid = (int)threadIdx.x;
-    uint8_t* W = smem;
-    int16_t* tt = reinterpret_cast<int16_t*>(smem + r.a_lds_bytes);
+    uint8_t* W = smem + TT_BYTES;
+    const uint8_t* tt = smem;   // act_q15 tables
     EpRow* ep = reinterpret_cast<EpRow*>(smem + r.a_lds_bytes + TT_BYTES);
     PT& R = *reinterpret_cast<PT*>(smem + r.a_lds_bytes + TT_BYTES + ep_bytes(r.ep_n));
     stage_weights(W, img.A + r.a_off, r.a_lds_bytes);
     stage_ep(ep, img, r.ep_lo, r.ep_n, true, true);
-    for (int i = tid; i < TT_BYTES / 2; i += blockDim.x) tt[i] = nnsp_tbl_tanh1[i];
+    for (int i = tid; i < TT_BYTES / 16; i += blockDim.x)
+        reinterpret_cast<int4*>(smem)[i] = reinterpret_cast<const int4*>(nnsp_tbl_act)[i];
     if (wgc) wgc[1] = (long long)__builtin_amdgcn_s_memrealtime();
     const int lane = tid & 63;
     const int g = __builtin_amdgcn_readfirstlane(tid >> 6);   // < RGP: LSTM wave; then stages
@@ -1603,7 +1607,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                 if constexpr (decltype(nolsh)::value) {
                                     const int32_t u = wadd(hx, (int32_t)cst[k][i]);
                                     if (i != 1) {   // sigmoid_q15's >> 1 folded into the layer shift
-                                        gt[i] = (int16_t)((tanh_q15s(u >> rsh1, tt) >> 1) + 16384);
+                                        gt[i] = (int16_t)act_q15<1>(u >> rsh1, tt);
                                         continue;
                                     }
                                     v = u >> rsh;
@@ -1613,10 +1617,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                     const int64_t pre = (int64_t)hx + cst[k][i];
                                     v = sat32(__builtin_expect(lsh > 0, 0) ? shift64(pre, lsh) : (pre >> rsh));
                                 }
-                                gt[i] = i == 1 ? tanh_q15s(v, tt) : sigmoid_q15s(v, tt);
+                                gt[i] = (int16_t)(i == 1 ? act_q15<0>(v, tt) : act_q15<1>(v >> 1, tt));
                             }
                             c_new[k] = cell_q15(gt[0], gt[1], gt[2], c_old[k]);
-                            hv[k] = sat16(((int32_t)tanh_q15s(c_new[k], tt) * gt[3]) >> 15);
+                            hv[k] = sat16((act_q15<0>(c_new[k], tt) * gt[3]) >> 15);
                         }
                     }
                 };

@@ -61,9 +61,9 @@ __device__ __forceinline__ int32_t affine_out(int64_t pre, int16_t b, const NnLa
 __device__ __forceinline__ int16_t act16(int act, int32_t v, const int16_t* tt) {
     return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15(v, tt) : sigmoid_q15(v, tt));
 }
-// the same on the re-indexed table nnsp_tbl_tanh1 (the split NN kernels' LDS copy)
-__device__ __forceinline__ int16_t act16s(int act, int32_t v, const int16_t* tt1) {
-    return act == ACT_RELU6 ? relu6_q12(v) : (act == ACT_TANH ? tanh_q15s(v, tt1) : sigmoid_q15s(v, tt1));
+// the same on the affine tables (act_q15; the split NN kernels' LDS copy at tb)
+__device__ __forceinline__ int16_t act16s(int act, int32_t v, const uint8_t* tb) {
+    return act == ACT_RELU6 ? relu6_q12(v) : (int16_t)(act == ACT_TANH ? act_q15<0>(v, tb) : act_q15<1>(v >> 1, tb));
 }
 
 // 8 features [8*part, 8*part + 8) of stream s at chunk frame t of a segment
