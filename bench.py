@@ -319,14 +319,15 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    fe_ms, nn_ms, rounds, sched = 0.0, 0.0, 0, 0
+    fe_ms, nn_ms, rounds, sched, dev_ms = 0.0, 0.0, 0, 0, 0.0
     t0 = time.perf_counter()
     for i in range(K):
         step(bufs[W + i], bufs[W + i + 1])
         if cascade:
-            r, f, _ = eng.last_stats()
+            r, f, cms = eng.last_stats()   # cms: HIP events from the chunk's start to its rounds' end
             rounds += r
             sched += f
+            dev_ms += cms
             fe_ms += eng.fe_stats()       # shared log-Mel, one launch (HIP events on the cascade's stream)
         else:
             f, n = eng.last_timing()      # HIP events on the batch's stream around fe / proj+recur
@@ -340,6 +341,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     out = {"elapsed": elapsed, "frames": S * T * K, "fe_ms": fe_ms / K, "S": S}
     if cascade:
         out["rounds_per_step"] = rounds / K
+        out["chunk_device_ms"] = dev_ms / K
         out["nn_frames_per_step"] = sched / K
         # one extra, untimed chunk instrumented: the nets' work serialised on
         # one stream with HIP events around each net's cold front end and NN
@@ -667,6 +669,10 @@ def main() -> None:
         }
         if args.net == "cascade":
             out["cascade"] = {"rounds_per_step": res["rounds_per_step"], "window": res["window"],
+                              # from the chunk's first event to its rounds' end on the device; the rest of
+                              # ms_per_step is the host's turn-around between chunks (and the counter copy)
+                              "chunk_device_ms": res["chunk_device_ms"],
+                              "host_gap_ms": elapsed / args.steps * 1e3 - res["chunk_device_ms"],
                               "lookahead_front_end": not args.no_lookahead,
                               "speculation_overhead": res["nn_frames_per_step"] / (S * args.frames) - 1.0,
                               "instrumented_chunk": res["instrumented"],

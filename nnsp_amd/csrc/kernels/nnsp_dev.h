@@ -51,6 +51,17 @@ __device__ __forceinline__ int32_t cell_q15(int32_t a, int32_t b, int32_t c, int
     return sat32_shr15(mad_i64_i32(c, d, (int64_t)(a * b)));
 }
 
+// The same for the LSTM's own gate ranges: i, f in [0, 32767] (sigmoid_fix
+// outputs) and g in [-32767, 32767] (tanh_fix) with ANY int32 c.  Then
+// |f*c + i*g| <= 32767 * 2^31 + 32767^2, and >> 15 stays within
+// [-2147450879, 2147450878]: lstm.c's saturation never binds (f < 1 in Q15
+// shrinks any c), so the cell is one v_mad_i64_i32 and one funnel shift
+// (tests/test_cell_q15.py checks the bound and the equality)
+__device__ __forceinline__ int32_t cell_q15_gates(int32_t i, int32_t g, int32_t f, int32_t c) {
+    const int64_t x = mad_i64_i32(f, c, (int64_t)(i * g));
+    return (int32_t)__builtin_amdgcn_alignbit((uint32_t)(x >> 32), (uint32_t)x, 15);
+}
+
 // SMMLAR / SMMULR contribution: floor((x*c + 2^31) / 2^32)
 __device__ __forceinline__ int32_t rnd_add(int32_t x, int32_t c) {
     return (int32_t)(((int64_t)x * c + 0x80000000LL) >> 32);

@@ -1619,7 +1619,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                                 }
                                 gt[i] = (int16_t)(i == 1 ? act_q15<0>(v, tt) : act_q15<1>(v >> 1, tt));
                             }
-                            c_new[k] = cell_q15(gt[0], gt[1], gt[2], c_old[k]);
+                            c_new[k] = cell_q15_gates(gt[0], gt[1], gt[2], c_old[k]);
                             hv[k] = sat16((act_q15<0>(c_new[k], tt) * gt[3]) >> 15);
                         }
                     }

@@ -46,3 +46,23 @@ def test_sat32_shr15_any_int64():
     x = np.concatenate([edges, rng.integers(-2**63, 2**63 - 1, 1 << 20, dtype=np.int64),
                         rng.integers(-2**48, 2**48, 1 << 20, dtype=np.int64)])
     np.testing.assert_array_equal(_cell_q15(x), _sat32_ref(x))
+
+
+def test_cell_without_saturation_for_lstm_gate_ranges():
+    """cell_q15_gates (nnsp_dev.h, recur_pipe_kernel): for the gates' own
+    ranges -- i, f in [0, 32767] (sigmoid_fix) and g in [-32767, 32767]
+    (tanh_fix) -- and any int32 cell state, lstm.c's sat32((i*g + f*c) >> 15)
+    never saturates, so the plain shift equals it."""
+    i = np.array([0, 1, 16384, 32766, 32767], np.int64)
+    g = np.array([-32767, -32766, -1, 0, 1, 32766, 32767], np.int64)
+    c = np.array([-2**31, -2**31 + 1, -2**30, -1, 0, 1, 2**30, 2**31 - 2, 2**31 - 1], np.int64)
+    a, b, f, cc = np.meshgrid(i, g, i, c, indexing="ij")
+    x = (a * b + f * cc).ravel()
+    assert (x >> 15).max() <= 2147450878 and (x >> 15).min() >= -2147450879
+    np.testing.assert_array_equal(x >> 15, _sat32_ref(x))
+    rng = np.random.default_rng(3)
+    n = 1 << 20
+    a, f = rng.integers(0, 32768, n), rng.integers(0, 32768, n)
+    b, cc = rng.integers(-32767, 32768, n), rng.integers(-2**31, 2**31, n)
+    x = a * b + f * cc
+    np.testing.assert_array_equal(x >> 15, _sat32_ref(x))
