@@ -316,6 +316,8 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     for i in range(W):
         step(bufs[i], bufs[i + 1])
     eng.sync()
+    if cascade:   # the cascade keeps running totals in C: nothing but the chunks in the timed loop
+        eng.totals_reset()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -323,19 +325,18 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     t0 = time.perf_counter()
     for i in range(K):
         step(bufs[W + i], bufs[W + i + 1])
-        if cascade:
-            r, f, cms = eng.last_stats()   # cms: HIP events from the chunk's start to its rounds' end
-            rounds += r
-            sched += f
-            dev_ms += cms
-            fe_ms += eng.fe_stats()       # shared log-Mel, one launch (HIP events on the cascade's stream)
-        else:
+        if not cascade:
             f, n = eng.last_timing()      # HIP events on the batch's stream around fe / proj+recur
             fe_ms += f
             nn_ms += n
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if cascade:   # K chunks: rounds, frames scheduled, the shared log-Mel's device ms (one launch per chunk,
+        # HIP events on the cascade's stream), each chunk's device ms from its start to its rounds' end
+        tot = eng.totals()
+        assert tot["chunks"] == K, tot
+        rounds, sched, fe_ms, dev_ms = tot["rounds"], tot["frames_run"], tot["fe_ms"], tot["chunk_ms"]
     if dist:
         dist.barrier()
     out = {"elapsed": elapsed, "frames": S * T * K, "fe_ms": fe_ms / K, "S": S}

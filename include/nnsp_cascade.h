@@ -132,6 +132,16 @@ int nnsp_cascade_last_fe_stats(nnsp_cascade *c, float *ms);
  * a negative error code. */
 int nnsp_cascade_last_rounds(nnsp_cascade *c, int max_rounds, int32_t *lists, float *fe_ms, float *nn_ms);
 
+/* Running totals since create or the last nnsp_cascade_totals_reset, for a
+ * caller that times many chunks and reads statistics once afterwards: chunks
+ * taken, rounds, frames scheduled on the nets, the shared front end's device
+ * ms, and the device ms from each chunk's start to its rounds' end.  Any
+ * output may be NULL; a chunk counts once its counters are taken (the next
+ * call, a getter or nnsp_cascade_sync). */
+int nnsp_cascade_totals(nnsp_cascade *c, long long *chunks, long long *rounds, long long *frames_run,
+                        double *fe_ms, double *chunk_ms);
+int nnsp_cascade_totals_reset(nnsp_cascade *c);
+
 /* current_pos_seq of every stream -> host int8 [S]. */
 int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
 

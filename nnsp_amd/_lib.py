@@ -120,6 +120,8 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_last_stats": (I, [P, C.POINTER(I), C.POINTER(C.c_longlong), C.POINTER(C.c_float)]),
         "nnsp_cascade_positions": (I, [P, P]),
         "nnsp_cascade_state_bytes": (C.c_size_t, [P]),
+        "nnsp_cascade_totals": (I, [P, P, P, P, P, P]),
+        "nnsp_cascade_totals_reset": (I, [P]),
         "nnsp_cascade_get_state": (I, [P, P, I, I]),
         "nnsp_cascade_set_state": (I, [P, P, I, I]),
         "nnsp_cascade_last_rounds": (I, [P, I, P, P, P]),

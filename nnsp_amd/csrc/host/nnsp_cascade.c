@@ -97,6 +97,10 @@ struct nnsp_cascade {
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
+    /* running totals since create / nnsp_cascade_totals_reset (nnsp_cascade_totals) */
+    long long tot_chunks, tot_rounds;
+    unsigned long long tot_frames;
+    double tot_fe_ms, tot_chunk_ms;
     const int16_t *pre_pcm;         /* the chunk whose shared front end the last call ran ahead */
     int pre_T;
     /* look-ahead front end of chunk q (events by chunk parity q & 1: around
@@ -682,6 +686,15 @@ static int book_take(nnsp_cascade *c)
         TRY(ahead_read(c, (int)((c->chunk - 1) & 1), 0));
         c->sfe_ms = c->ahead_ms[(c->chunk - 1) & 1];
     }
+    {   /* running totals: read once after a timed loop instead of per chunk */
+        float cms = 0.f;
+        TRY(nnspk_event_elapsed(&cms, c->ev[0], c->ev[1]));
+        c->tot_chunks++;
+        c->tot_rounds += c->last_rounds;
+        c->tot_frames += c->book_frames[0] + c->book_frames[1] + c->book_frames[2];
+        c->tot_fe_ms += c->sfe_ms;
+        c->tot_chunk_ms += cms;
+    }
     memcpy(c->rc, rc, sizeof c->rc);
     memset(c->rfe, 0, sizeof c->rfe);
     memset(c->rnn, 0, sizeof c->rnn);
@@ -1076,5 +1089,28 @@ int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int cou
     sc.to_blob = 0;
     TRY(nnsp_state_xfer(&sc, (void *)host, c->stream));
     c->pre_pcm = NULL; /* a look-ahead front end ran on the old state: the next call recomputes */
+    return 0;
+}
+
+int nnsp_cascade_totals(nnsp_cascade *c, long long *chunks, long long *rounds, long long *frames_run, double *fe_ms,
+                        double *chunk_ms)
+{
+    if (!c) return NNSP_EINVAL;
+    TRY(book_take(c));
+    if (chunks) *chunks = c->tot_chunks;
+    if (rounds) *rounds = c->tot_rounds;
+    if (frames_run) *frames_run = (long long)c->tot_frames;
+    if (fe_ms) *fe_ms = c->tot_fe_ms;
+    if (chunk_ms) *chunk_ms = c->tot_chunk_ms;
+    return 0;
+}
+
+int nnsp_cascade_totals_reset(nnsp_cascade *c)
+{
+    if (!c) return NNSP_EINVAL;
+    TRY(book_take(c));
+    c->tot_chunks = c->tot_rounds = 0;
+    c->tot_frames = 0;
+    c->tot_fe_ms = c->tot_chunk_ms = 0.0;
     return 0;
 }

@@ -182,6 +182,18 @@ class NNSPCascade:
         _lib.check(_lib.lib().nnsp_cascade_last_stats(self.h, C.byref(r), C.byref(f), C.byref(ms)), "stats")
         return r.value, f.value, ms.value
 
+    def totals(self) -> dict:
+        """Running totals since create / totals_reset (nnsp_cascade_totals)."""
+        ch, r, f = C.c_longlong(), C.c_longlong(), C.c_longlong()
+        fe, cm = C.c_double(), C.c_double()
+        _lib.check(_lib.lib().nnsp_cascade_totals(self.h, C.byref(ch), C.byref(r), C.byref(f), C.byref(fe),
+                                                  C.byref(cm)), "totals")
+        return {"chunks": ch.value, "rounds": r.value, "frames_run": f.value, "fe_ms": fe.value,
+                "chunk_ms": cm.value}
+
+    def totals_reset(self) -> None:
+        _lib.check(_lib.lib().nnsp_cascade_totals_reset(self.h), "totals_reset")
+
     def net_stats(self, name: str) -> tuple[int, float, float, int]:
         """(frames scheduled, fe ms, nn ms, launches) of one net in the last chunk."""
         f, fe, nn, n = C.c_longlong(), C.c_float(), C.c_float(), C.c_int()
