@@ -37,7 +37,10 @@ static int net_shape(const NnImage *g)
     if (L[0].N != N || L[1].K != N || L[2].K != N || L[2].N != N || L[3].K != N || L[3].N != N || L[4].K != N)
         return NN_SHAPE_GENERIC;
     for (int i = 0; i < 3; ++i)
-        if (N == known[i][1] && L[4].N == known[i][2]) return known[i][0];
+        if (N == known[i][1] && L[4].N == known[i][2])
+            /* the 2-output shapes compile binary post-processing only: an s2i
+             * post-processing (nn_id 0) on them takes the generic kernels */
+            return known[i][2] < 41 && g->nn_id == 0 ? NN_SHAPE_GENERIC : known[i][0];
     return NN_SHAPE_GENERIC;
 }
 

@@ -1696,10 +1696,16 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
             if (lane < 16 && active && cut < 0) {
                 // logits read from LDS where the post-processing uses them
                 // (s2i: 7, and 2 x 17 only on a detection) -- no register copy
-                if (SH::NOUT >= 41 && img.nn_id == 0)
-                    post_proc_s2i_lds(ps, img, f32);
-                else
-                    post_proc(ps, img, LdsLogits{f32});
+                // the 2-output shapes only run with binary post-processing
+                // (net_shape, nnsp_batch.c): no s2i path in their loops
+                if constexpr (SH::NOUT >= 41) {
+                    if (img.nn_id == 0)
+                        post_proc_s2i_lds(ps, img, f32);
+                    else
+                        post_proc(ps, img, LdsLogits{f32});
+                } else {
+                    post_proc_binary(ps, img, LdsLogits{f32});
+                }
             }
             if (clk && j < 64) clk[j * 16 + 3] = (long long)__builtin_amdgcn_s_memtime();
             if (lane < 16 && active && cut < 0) {

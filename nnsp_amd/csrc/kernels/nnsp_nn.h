@@ -182,6 +182,23 @@ __device__ __forceinline__ void post_proc_s2i_lds(PostState& ps, const NnImage& 
     ps.argmax_last = (int16_t)am;
 }
 
+// binary_post_proc (nn_speech.c:193-227; T7: logits overwritten by exp2 values)
+template <typename LG>
+__device__ __forceinline__ void post_proc_binary(PostState& ps, const NnImage& img, const LG& lg) {
+    // the larger logit's difference to the max is 0, and compute_pwr2(0)
+    // is the constant 32723 (0x5a82 + 0x1fd7 + 0x057a): only the other
+    // logit's exp2 is computed -- the post wave is the slowest stage of
+    // the binary nets' recurrence pipeline
+    const int32_t l0 = lg[0], l1 = lg[1];
+    const bool first = l0 >= l1;   // on a tie both differences are 0
+    const int32_t eo = pwr2_q15(sat32(((int64_t)(first ? wsub(l1, l0) : wsub(l0, l1)) * 0xB8AA) >> 15));
+    const int32_t e[2] = {first ? 32723 : eo, first ? eo : 32723};
+    const int32_t den = wadd(e[0], e[1]);
+    const int32_t lim = (int32_t)(((int64_t)(32768 - img.thresh_prob) * den) >> 15);
+    ps.counts[0] = e[0] <= lim ? (int16_t)(ps.counts[0] + 1) : (int16_t)0;
+    ps.trigger = ps.counts[0] >= img.th_count ? 1 : 0;
+}
+
 template <typename LG>
 __device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, const LG& lg) {
     if (img.nn_id == 0) {  // s2i_post_proc
@@ -210,19 +227,8 @@ __device__ __forceinline__ void post_proc(PostState& ps, const NnImage& img, con
             for (int i = 0; i < 7; ++i) ps.counts[i] = 0;
         }
         ps.argmax_last = (int16_t)am;
-    } else {  // binary_post_proc (T7: logits overwritten by exp2 values)
-        // the larger logit's difference to the max is 0, and compute_pwr2(0)
-        // is the constant 32723 (0x5a82 + 0x1fd7 + 0x057a): only the other
-        // logit's exp2 is computed -- the post wave is the slowest stage of
-        // the binary nets' recurrence pipeline
-        const int32_t l0 = lg[0], l1 = lg[1];
-        const bool first = l0 >= l1;   // on a tie both differences are 0
-        const int32_t eo = pwr2_q15(sat32(((int64_t)(first ? wsub(l1, l0) : wsub(l0, l1)) * 0xB8AA) >> 15));
-        const int32_t e[2] = {first ? 32723 : eo, first ? eo : 32723};
-        const int32_t den = wadd(e[0], e[1]);
-        const int32_t lim = (int32_t)(((int64_t)(32768 - img.thresh_prob) * den) >> 15);
-        ps.counts[0] = e[0] <= lim ? (int16_t)(ps.counts[0] + 1) : (int16_t)0;
-        ps.trigger = ps.counts[0] >= img.th_count ? 1 : 0;
+    } else {
+        post_proc_binary(ps, img, lg);
     }
 }
 
