@@ -301,17 +301,17 @@ __device__ __forceinline__ int16_t sigmoid_q15s(int32_t x, const int16_t* tbl1) 
     return (int16_t)((tanh_q15s(x >> 1, tbl1) >> 1) + 16384);
 }
 // tanh_fix / sigmoid_fix (activation.c:31-83) as one v_mad_i32_i24 on the
-// affine tables of tables.act_affine_tables (nnsp_tbl_act), staged in LDS at
-// tb: per half-segment j = bb >> 9 of bb = min(|x| + 512, 164352), 16 bytes
+// affine table of tables.act_affine_table (nnsp_tbl_act), staged in LDS at tb:
+// per half-segment j = bb >> 9 of bb = min(|x| + 512, 164352), 16 bytes
 // (A_pos, b_pos, A_neg, b_neg); z = A + (bb & 511) * b is the reference's
 // interpolation numerator with the sign, activation.c's max(., 0) and its
 // saturation at 5 * 2^15 folded in.  F 0: tanh = z >> 15; F 1: sigmoid of the
-// pre-shifted input w (sigmoid_fix(v) with w = v >> 1) = z >>> 16.  About 11
-// VALU against 16 / 18 for tanh_q15s / sigmoid_q15s; checked exhaustively in
-// tests/test_tables.py (test_act_affine_tables_match_activation_c)
-#define ACT_ENTRIES 328
-#define ACT_FN_BYTES (ACT_ENTRIES * 16)
-#define ACT_BYTES (2 * ACT_FN_BYTES)
+// pre-shifted input w (sigmoid_fix(v) with w = v >> 1) = (z + 2^30) >>> 16.
+// 12 / 13 VALU against 16 / 18 for tanh_q15s / sigmoid_q15s (one 5 KB table:
+// a second, sigmoid-ready one would take S2I's recurrence past 160 KB of LDS);
+// checked exhaustively in tests/test_tables.py
+#define ACT_ENTRIES 322
+#define ACT_BYTES (ACT_ENTRIES * 16)
 template <int F>
 __device__ __forceinline__ int32_t act_q15(int32_t x, const uint8_t* tb) {
     const uint32_t sgn = (uint32_t)x >> 31;
@@ -319,9 +319,9 @@ __device__ __forceinline__ int32_t act_q15(int32_t x, const uint8_t* tb) {
     uint32_t bb = xs + 512u + sgn;
     bb = bb < 164352u ? bb : 164352u;
     const uint32_t off = ((bb >> 5) & 0x1ff0u) | (sgn << 3);
-    const int2 e = *reinterpret_cast<const int2*>(tb + F * ACT_FN_BYTES + off);
+    const int2 e = *reinterpret_cast<const int2*>(tb + off);
     const int32_t z = __mul24((int32_t)(bb & 511u), e.y) + e.x;
-    return F == 0 ? (z >> 15) : (int32_t)((uint32_t)z >> 16);
+    return F == 0 ? (z >> 15) : (int32_t)(((uint32_t)z + (1u << 30)) >> 16);
 }
 __device__ __forceinline__ int16_t relu6_q12(int32_t x) {   // :6-17
     int32_t v = x >> 3;

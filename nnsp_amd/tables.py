@@ -97,27 +97,26 @@ def tanh_interp_shifted() -> np.ndarray:
     return np.concatenate([[[-512, 32767]], t, pad]).reshape(-1).astype(np.int16)
 
 
-ACT_ENTRIES = 328   # half-segments j = (|x| + 512) >> 9 <= 321 after the clamp, padded to a multiple of 8
+ACT_ENTRIES = 322   # half-segments j = (|x| + 512) >> 9 <= 321 after the clamp
 
 
-def act_affine_tables() -> np.ndarray:
+def act_affine_table() -> np.ndarray:
     """tanh_fix / sigmoid_fix (activation.c:31-83) as one multiply-add per
-    lookup (nnsp_dev.h act_q15): int32 [2 functions][ACT_ENTRIES][4] =
-    (A_pos, b_pos, A_neg, b_neg) per half-segment j = bb >> 9 of
-    bb = |x| + 512, with bb clamped to 164352 (|x| >= 5 * 2^15 lands on
-    j = 321, dx = 0: activation.c's saturation to 32767 -- with 1024-wide
-    entries it would fall mid-entry) and dx = bb & 511.  Entry j is half
-    (j & 1) of tanh_interp_shifted's entry j >> 1: A = val << 15 + (j & 1) *
-    512 * slope, b = slope, so z = A + dx * b is the reference's
-    val * 2^15 + dx1024 * slope exactly.  Per the sign of x:
-      tanh    (function 0): z >> 15 (arithmetic).  Negative x: the negated
-              result, -floor(z / 2^15) = floor((32767 - z) / 2^15), i.e.
-              A_neg = 32767 - A, b_neg = -b.  Entry 0 (|x| < 512) takes
-              A = -2^24 + 512, which gives |x| - 1 for |x| >= 1 and 0 at x = 0
-              -- activation.c's max(., 0) -- so no clamp of the result.
-      sigmoid (function 1): 16384 + (tanh(w) >> 1) of the pre-shifted input
-              w: the nested floors fold into z >>> 16 with A + 2^30 (positive)
-              and 2^30 + 32767 - A, -b (negative); z is non-negative below 2^32.
+    lookup (nnsp_dev.h act_q15): int32 [ACT_ENTRIES][4] = (A_pos, b_pos, A_neg,
+    b_neg) per half-segment j = bb >> 9 of bb = |x| + 512, with bb clamped to
+    164352 (|x| >= 5 * 2^15 lands on j = 321, dx = 0: activation.c's saturation
+    to 32767 -- with 1024-wide entries it would fall mid-entry) and
+    dx = bb & 511.  Entry j is half (j & 1) of tanh_interp_shifted's entry
+    j >> 1: A = val << 15 + (j & 1) * 512 * slope, b = slope, so
+    z = A + dx * b is the reference's val * 2^15 + dx1024 * slope exactly.
+      tanh:    z >> 15 (arithmetic).  Negative x takes the negated result,
+               -floor(z / 2^15) = floor((32767 - z) / 2^15): A_neg = 32767 - A,
+               b_neg = -b.  Entry 0 (|x| < 512) starts at A = -2^24 + 512, which
+               gives |x| - 1 for |x| >= 1 and 0 at x = 0 -- activation.c's
+               max(., 0) -- so the result needs no clamp.
+      sigmoid: 16384 + (tanh(w) >> 1) of the pre-shifted input w is
+               (z + 2^30) >>> 16 with the same z (nested floors; the sum is
+               non-negative and below 2^32), for either sign.
     tests/test_tables.py checks both against activation.c's definitions."""
     t = tanh_interp_shifted().astype(np.int64).reshape(-1, 2)
     j = np.arange(ACT_ENTRIES)
@@ -129,9 +128,7 @@ def act_affine_tables() -> np.ndarray:
     sat = j >= 321
     A[sat] = 32767 << 15
     b[sat] = 0
-    tanh = np.stack([A, b, 32767 - A, -b], 1)
-    sig = np.stack([A + (1 << 30), b, (1 << 30) + 32767 - A, -b], 1)
-    out = np.stack([tanh, sig])
+    out = np.stack([A, b, 32767 - A, -b], 1)
     return (out & 0xFFFFFFFF).astype(np.uint32).view(np.int32)
 
 
@@ -241,7 +238,7 @@ def header_text() -> str:
         _c_array("int16_t", "nnsp_tbl_log", log_interp()),
         _c_array("int16_t", "nnsp_tbl_tanh", tanh_interp()),
         _c_array("int16_t", "nnsp_tbl_tanh1", tanh_interp_shifted()),
-        _c_array("int32_t", "nnsp_tbl_act", act_affine_tables(), 8),
+        _c_array("int32_t", "nnsp_tbl_act", act_affine_table(), 8),
         _c_array("int32_t", "nnsp_tbl_tw256", cfft256_twiddles(), 6),
         _c_array("int32_t", "nnsp_tbl_split", rfft512_split_coefs(), 6),
         _c_array("int32_t", "nnsp_tbl_melseg", mel_segments(), 4),
