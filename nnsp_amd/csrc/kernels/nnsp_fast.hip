@@ -1113,7 +1113,10 @@ template <class SH>
 struct PipeCfg {
     // LSTM waves: <= 2 row tiles each (4 tiles each on 4 waves would let KWS's
     // workgroups fit two per CU, but spills ~250 B per lane at 128 VGPRs)
-    static constexpr int LW = SH::NRT <= 8 ? 4 : (SH::NRT + 1) / 2;
+#ifndef PIPE_LW_SMALL
+#define PIPE_LW_SMALL 4   // LSTM waves of a net with <= 8 row tiles (VAD's 7)
+#endif
+    static constexpr int LW = SH::NRT == 0 ? 4 : (SH::NRT <= 8 ? (PIPE_LW_SMALL < SH::NRT ? PIPE_LW_SMALL : SH::NRT) : (SH::NRT + 1) / 2);
     static constexpr int RPW = (SH::NRT + LW - 1) / LW;      // LSTM row tiles per wave
     // the last FC layer and the post-processing on waves of their own (a
     // 5-stage pipeline) for the 2-output nets; S2I keeps them on one wave: a
@@ -1133,8 +1136,8 @@ struct PipeCfg {
 #ifndef PIPE_SMALL_WG_PER_CU
 #define PIPE_SMALL_WG_PER_CU 2
 #endif
-    static constexpr int MINW = WPG <= 8 ? PIPE_SMALL_WG_PER_CU * ((WPG + 3) / 4) : (WPG + 3) / 4;
-    static_assert(WPG <= 16, "recur_pipe_kernel: at most 4 waves per SIMD");
+    static constexpr int MINW = SH::NRT <= 8 ? (PIPE_SMALL_WG_PER_CU * WPG + 3) / 4 : (WPG + 3) / 4;
+    static_assert(WPG <= 16, "recur_pipe_kernel: at most 16 waves per workgroup");
 };
 
 // tiles one workgroup can run back to back through its pipeline (FastRun.tseq)
