@@ -316,7 +316,10 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     for i in range(W):
         step(bufs[i], bufs[i + 1])
     eng.sync()
-    if cascade:   # the cascade keeps running totals in C: nothing but the chunks in the timed loop
+    # the cascade keeps running totals in C: nothing but the chunks in the timed loop (an older library
+    # under NNSP_LIB, development A/B, has no totals: its statistics are read per step as before)
+    totals = cascade and _lib.has("nnsp_cascade_totals")
+    if totals:
         eng.totals_reset()
     if dist:
         dist.barrier()
@@ -325,6 +328,9 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     t0 = time.perf_counter()
     for i in range(K):
         step(bufs[W + i], bufs[W + i + 1])
+        if cascade and not totals:
+            r, f, cms = eng.last_stats()
+            rounds, sched, dev_ms, fe_ms = rounds + r, sched + f, dev_ms + cms, fe_ms + eng.fe_stats()
         if not cascade:
             f, n = eng.last_timing()      # HIP events on the batch's stream around fe / proj+recur
             fe_ms += f
@@ -332,7 +338,7 @@ def run_workload(args, S: int, s0: int, weights: str, dist=None) -> dict:
     eng.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if cascade:   # K chunks: rounds, frames scheduled, the shared log-Mel's device ms (one launch per chunk,
+    if totals:   # K chunks: rounds, frames scheduled, the shared log-Mel's device ms (one launch per chunk,
         # HIP events on the cascade's stream), each chunk's device ms from its start to its rounds' end
         tot = eng.totals()
         assert tot["chunks"] == K, tot
