@@ -89,6 +89,32 @@ __device__ __forceinline__ bool casc_step(const CascArgs& a, CascState& st, int 
     return rst;
 }
 
+// casc_step for a wave-uniform net n with the per-lane decisions as selects:
+// the branchy form put every per-lane condition behind exec-mask branches (the
+// post wave of the binary nets ran ~200 scalar instructions per step, most of
+// them exec-mask saves and restores).  Same state transitions as casc_step.
+__device__ __forceinline__ bool casc_step_sel(const CascArgs& a, CascState& st, int n, int16_t det) {
+    const int pos = st.pos;
+    const int fwd = wrap_inc(pos, a.len_seq);
+    if (n == 1) {   // vad (nnCntrlClass.c:238-262): a detection moves on and resets
+        st.pos = (int16_t)(det ? fwd : pos);
+        return det != 0;
+    }
+    const int to = n == 0 ? a.timeout_s2i : a.timeout_kws;
+    const int cnt = wrap_inc(n == 0 ? st.cnt_s2i : st.cnt_kws, to);
+    const bool move = det || cnt == to - 1;
+    // s2i moves forward; kws forward on a detection, back on its timeout
+    const int np = n == 0 || det ? fwd : (pos == 0 ? a.len_seq - 1 : pos - 1);
+    const bool rst = move && (det || n != seq_at(a, np));
+    const uint16_t c2 = (uint16_t)(rst ? 0 : cnt);
+    if (n == 0)
+        st.cnt_s2i = c2;
+    else
+        st.cnt_kws = c2;
+    st.pos = (int16_t)(move ? np : pos);
+    return rst;
+}
+
 // NNSPClass_reset's post-processing part (nn_speech.c:57-72)
 template <class P>
 __device__ __forceinline__ void post_reset(P& p) {

@@ -1715,13 +1715,20 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 // the controller for frames t and t + 1; their outputs go to
                 // the slot, and another wave stores them next iteration (the
                 // stores and their address arithmetic off this wave, the
-                // pipeline's slowest)
+                // pipeline's slowest).  As selects (casc_step_sel): frame t + 1
+                // steps the controller only when frame t did not reset the net
+                // and t + 1 is inside the segment
                 wfl = 1;
-                if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) {
-                    cut = t;
+                if (ctl) {
+                    const bool r0 = nnsp::casc_step_sel(ca, cst, r.net_id, ps.trigger);
+                    const CascState c1 = cst;
+                    const bool two = !r0 && t + 1 < e;
+                    const bool r1 = nnsp::casc_step_sel(ca, cst, r.net_id, ps.trigger);
+                    cst = two ? cst : c1;
+                    cut = r0 ? t : (two && r1 ? t + 1 : -1);
+                    wfl = two ? 3 : 1;
                 } else if (t + 1 < e) {
                     wfl = 3;
-                    if (ctl && nnsp::casc_step(ca, cst, r.net_id, ps.trigger)) cut = t + 1;
                 }
             }
             if (clk && j < 64) clk[j * 16 + 4] = (long long)__builtin_amdgcn_s_memtime();
