@@ -641,8 +641,12 @@ __global__ __launch_bounds__(512, 4) void proj_kernel(NnImage img, FastRun r) { 
                 int16_t* U = &P.uni[CB][0];
                 const int16_t* in = U + kr * FR * 40 + 80 * jr - 80 * sc;
                 const NnLayer& L0 = img.L[0];
-                fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4>(L0, W + (L0.a_off - r.a_off), ep + (L0.ep_off - r.ep_lo),
-                                                              in, 80, U, PW::AS, tt, lane);
+                // PAD: the last row tile's padding rows (N .. 16 R0 - 1) are
+                // computed and stored too, with no per-value branch; the x
+                // store below writes those columns as zeros
+                fc_layer<ACC32, SH::R0, 4, ACT_TANH, SH::NW, 4, true>(L0, W + (L0.a_off - r.a_off),
+                                                                    ep + (L0.ep_off - r.ep_lo), in, 80, U, PW::AS,
+                                                                    tt, lane);
                 wave_lds_sync();
                 PCLK(2);
                 // ---- the LSTM's input x of every row to HBM, already in the
@@ -1122,7 +1126,14 @@ struct PipeCfg {
     // 5-stage pipeline) for the 2-output nets; S2I keeps them on one wave: a
     // 13th wave would cap the kernel at 128 VGPRs, and the spills cost more
     // than the split gains (profiles/recur_clocks.py)
-    static constexpr int SPLIT = SH::NOUT <= 2 ? 1 : 0;
+#ifndef PIPE_S2I_SPLIT
+#define PIPE_S2I_SPLIT 0
+#endif
+    static constexpr int SPLIT = SH::NOUT <= 2 ? 1 : PIPE_S2I_SPLIT;
+    // the wide nets' FC stages are as long as the LSTM step: the post wave's
+    // frame outputs are stored by the two FC waves (frame t / t + 1) instead of
+    // the FC-linear wave
+    static constexpr bool STORE_FC12 = SH::NOUT > 2;
     static constexpr int NWV = LW + 3 + SPLIT;               // waves per tile
     // tiles per workgroup (the kernel supports several, sharing the staged
     // weights): one.  Two VAD tiles per workgroup (16 waves, so that every
@@ -1258,8 +1269,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // the waves that store the post wave's frame outputs one iteration later:
     // the stage with the most slack (FC linear); S2I, whose FC stages are as
     // long as its LSTM step, splits them over its two FC waves (frame t / t + 1)
-    const bool store_w = SPL ? g == RGP + 2 : (g == RGP || g == RGP + 1);
-    const int store_bits = SPL ? 3 : (g == RGP ? 1 : 2);
+    constexpr bool SFC = CF::STORE_FC12;
+    const bool store_w = SFC ? (g == RGP || g == RGP + 1) : g == RGP + 2;
+    const int store_bits = SFC ? (g == RGP ? 1 : 2) : 3;
     // ---- the tiles' descriptors (post wave, lane = 16 x tile + stream) and
     //      their pipeline steps: the most NN steps of the tile's streams
     if (post_w) {
@@ -1659,19 +1671,19 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                     fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
                         L2, W + (L2.a_off - r.a_off), ep + (L2.ep_off - r.ep_lo), &R.h[cur][0][0], RS, &R.a2[cur][0][0],
                         RS, tt, lane);
-                if (!SPL) flush(cur ^ 1);
+                if (SFC) flush(cur ^ 1);
             } else if constexpr (role == 2) {   // stage 2: step j-2
                 if (j >= 2 && j - 2 < total)
                     fc_layer<ACC32, SH::R2, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
                         L3, W + (L3.a_off - r.a_off), ep + (L3.ep_off - r.ep_lo), &R.a2[cur ^ 1][0][0], RS,
                         &R.a3[cur][0][0], RS, tt, lane);
-                if (!SPL) flush(cur ^ 1);
+                if (SFC) flush(cur ^ 1);
             } else {   // stage 3 (split): step j-3
                 if (j >= 3 && j - 3 < total)
                     fc_layer<ACC32, SH::R3, SH::NKR, ACT_LINEAR, SH::NOUT, SH::NKR, true>(
                         L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                         &R.a4[cur][0][0], RS, tt, lane);
-                flush(cur ^ 1);   // the post wave's outputs of the previous iteration
+                if (!SFC) flush(cur ^ 1);   // the post wave's outputs of the previous iteration
             }
         } else {   // post: step jp = j-3-SPL
           int wfl = 0;   // frames of this step to store (bits: t, t + 1)
