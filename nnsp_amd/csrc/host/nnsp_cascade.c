@@ -83,6 +83,11 @@ struct nnsp_cascade {
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation), per chunk parity:
                                        chunk k counts into block k & 1 and clears block (k + 1) & 1 */
     void *stream;                   /* front end, control; the nets' work forks off it */
+    void *bstream;                  /* early return: the chunk's join and counter copy, beside the look-ahead
+                                       front end on c->stream */
+    int early;                      /* return once the rounds are done, before the look-ahead front end ends
+                                       (the next call's round 0 waits for it on the device) */
+    int early_prev;                 /* the last call returned early */
     void *ns[3];                    /* per net id: segment features + NN of a round */
     void *own_ns[3];                /* per net id: a cascade-owned high-priority stream used as ns[n]
                                        (NNSP_NET_PRIO bit n, development), else NULL */
@@ -213,6 +218,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     }
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
+    if ((e = nnspk_stream_create(&c->bstream))) goto fail;
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
@@ -352,6 +358,10 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         for (int i = 0; i < 3; ++i)
             if (nets[i]->shape == NN_SHAPE_GENERIC) c->fused = 0;
         c->timing = getenv("NNSP_CASCADE_TIMING") != NULL;
+        {
+            const char *er = getenv("NNSP_EARLY_RETURN");
+            c->early = er ? atoi(er) != 0 : 0;
+        }
         c->debug = getenv("NNSP_CASCADE_DEBUG") != NULL;
         const char *w = getenv("NNSP_CASCADE_WINDOW");
         if (w && atoi(w) >= 0) {
@@ -405,7 +415,9 @@ void nnsp_cascade_destroy(nnsp_cascade *c)
             nnspk_stream_destroy(c->own_ns[n]);
         }
     }
+    if (c->bstream) nnspk_sync(c->bstream);
     nnspk_stream_destroy(c->stream);
+    nnspk_stream_destroy(c->bstream);
     nnspk_event_destroy(c->ev_book);
     nnspk_host_free(c->h_book);
     free(c);
@@ -772,6 +784,9 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     const int begin_on_vad = c->fused && !c->serial;
     void *bst = begin_on_vad ? c->ns[1] : c->stream;
     if (begin_on_vad && !ahead_done) TRY(nnspk_stream_wait(bst, c->ev_fe[1]));
+    /* early return: the previous call returned before the look-ahead front end
+     * of this chunk had finished -- round 0 waits for it on the device */
+    if (ahead_done && c->early_prev) TRY(nnspk_stream_wait(bst, c->ev_ahead[k & 1][1]));
     TRY(nnspk_launch_casc_begin(&a, bst));
     DBG(bst, "casc_begin", -1, -1);
     if (ahead_done) TRY(nnspk_event_record(c->ev[0], c->stream));   /* c->stream is idle: about now */
@@ -828,13 +843,22 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
                 ahead_launched = 1;
             }
         }
-        TRY(join_rounds(c, r));
-        TRY(nnspk_event_record(c->ev[1], c->stream)); /* the rounds' end (complete at the sync below) */
+        /* early return (with a look-ahead front end running on c->stream): the
+         * join and the counter copy on the book stream, so that they do not
+         * queue behind the front end */
+        const int er = c->early && ahead_launched;
+        void *js = er ? c->bstream : c->stream;
+        if (er) {
+            for (int n = 0; n < 3; ++n) TRY(nnspk_stream_wait(js, c->ev_rnd[(r - 1) & 1][n]));
+        } else {
+            TRY(join_rounds(c, r));
+        }
+        TRY(nnspk_event_record(c->ev[1], js)); /* the rounds' end (complete at the sync below) */
         /* all the chunk's counters in one copy (the next round's list lengths
          * among them): if no round is left they are final, and the
          * bookkeeping needs no further host wait */
-        TRY(nnspk_d2h(c->h_book, c->d_frames, ZERO_BYTES, c->stream));
-        TRY(nnspk_event_record(c->ev_book, c->stream));
+        TRY(nnspk_d2h(c->h_book, c->d_frames, ZERO_BYTES, js));
+        TRY(nnspk_event_record(c->ev_book, js));
         /* polled, not a blocking stream synchronisation: the wake-up of a
          * blocking wait sits between this chunk's last kernel and the next
          * chunk's first (everything on c->stream is before ev_book); the
@@ -842,7 +866,9 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
          * only through the rounds' tail (A/B: 1.004 vs 0.997 G) */
         /* without a look-ahead front end to sleep through, the whole chunk is
          * still ahead: a blocking wait, not a core spinning for milliseconds */
-        if (ahead_launched) {
+        if (er) {   /* the rounds' end, not the front end's: polled */
+            TRY(nnspk_event_spin(c->ev_book));
+        } else if (ahead_launched) {
             TRY(nnspk_event_sync(c->ev_ahead[(k + 1) & 1][1]));
             TRY(nnspk_event_spin(c->ev_book));
         } else {
@@ -854,6 +880,7 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     }
     c->launched = r;
     c->chunk_open = 0;
+    c->early_prev = c->early && ahead_launched;
     c->abs0 = (c->abs0 + T) % c->ring;
     c->chunk = k + 1;
     if (ahead_launched) {
@@ -932,6 +959,7 @@ int nnsp_cascade_sync(nnsp_cascade *c)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
+    TRY(nnspk_sync(c->bstream));
     TRY(book_take(c));
     for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
     return 0;
@@ -1041,6 +1069,7 @@ static void cascade_state_segs(const nnsp_cascade *c, StateCopy *sc)
 static int cascade_quiesce(nnsp_cascade *c)
 {
     TRY(nnspk_sync(c->stream));
+    TRY(nnspk_sync(c->bstream));
     for (int n = 0; n < 3; ++n) TRY(nnspk_sync(c->ns[n]));
     TRY(book_take(c));
     for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
