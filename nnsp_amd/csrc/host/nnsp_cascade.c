@@ -80,6 +80,7 @@ struct nnsp_cascade {
     int32_t *d_last_round;          /* last round a stream was listed for (+1) */
     int32_t *d_cuts;                /* segments cut by a net switch in the chunk */
     void *d_fetab;                  /* the shared / cold front end's tables, prebuilt */
+    int fe_sched;                   /* the shared front end's frame schedule (FE_SCHED_*) */
     void *d_zero;                   /* frames, counts, last_round, rcount (one allocation), per chunk parity:
                                        chunk k counts into block k & 1 and clears block (k + 1) & 1 */
     void *stream;                   /* front end, control; the nets' work forks off it */
@@ -263,6 +264,16 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_nring[0], 3 * S * (size_t)c->ring * 40 * 2))) goto fail;
     for (int i = 1; i < 3; ++i) c->d_nring[i] = c->d_nring[0] + (size_t)i * S * c->ring * 40;
     if ((e = nnspk_malloc((void **)&c->d_stail, S * 640))) goto fail;
+    {   /* the shared front end's frame schedule (FE_SCHED_*; NNSP_FE_SCHED, development) */
+        const char *fs = getenv("NNSP_FE_SCHED");
+        c->fe_sched = fs ? atoi(fs) : FE_SCHED_GUIDED;
+        const char *fg = getenv("NNSP_FE_GUIDE"); /* "twelfths,divisor" of the guided schedule */
+        if (fg && c->fe_sched == FE_SCHED_GUIDED) {
+            int g12 = 0, dv = 0;
+            if (sscanf(fg, "%d,%d", &g12, &dv) == 2 && g12 > 0 && g12 < 12 && dv > 0 && dv < 256)
+                c->fe_sched |= (g12 << 8) | (dv << 16);
+        }
+    }
     /* (rounded up to whole dwords: proj DMAs the dword holding a stream's byte) */
     if ((e = nnspk_malloc((void **)&c->d_fresh, ((size_t)S + 3) & ~(size_t)3))) goto fail;
     for (int i = 0; i < 3; ++i) {
@@ -626,6 +637,7 @@ static int shared_fe(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *
     FeArgs fa;
     memset(&fa, 0, sizeof fa);
     fa.tb_img = c->d_fetab;
+    fa.sched = c->fe_sched;
     (void)ahead;
     fa.pcm = pcm;
     fa.tail = tail;

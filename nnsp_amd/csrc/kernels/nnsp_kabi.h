@@ -82,12 +82,14 @@ typedef struct {
                                  workgroup 0, its first 64 frames: dbg_clk[1024 + 8 * frame + phase] */
     int32_t norm32;           /* 1: every normalisation's (feature - mean) * stdR >> shift provably fits
                                  int32 (nnsp_norm_fits32): the 32-bit clamp path */
-    int32_t pad3_;
+    int32_t sched;            /* FE_MODE_SHARED: frame schedule (FE_SCHED_*, fe_kernel) */
     /* non-NULL: the workgroup's constant tables (twiddles, split, normalisation,
      * log, window, Mel) prebuilt for this mode / build by nnspk_build_fe_tables,
      * copied with 16-byte loads instead of being derived per workgroup */
     const void *tb_img;
 } FeArgs;
+#define FE_SCHED_EQUAL 0   /* equal contiguous ranges per wave */
+#define FE_SCHED_GUIDED 1  /* the last-dispatched third of the waves on quarter ranges */
 
 /* feature_module.c:67-73 in 32 bits: |log10 output| < 2^18 (|table| * 0x3796 >> 15
  * plus 15 * 0x2688), so with m = max |mean|, r = max |stdR| the 64-bit

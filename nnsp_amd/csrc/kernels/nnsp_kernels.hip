@@ -404,7 +404,34 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
     const unsigned nfr = nrow * W;   // host guarantees < 2^31
     const unsigned nw = gridDim.x * (unsigned)WPG;
     const unsigned per = (nfr + nw - 1) / nw;
-    if (blockIdx.x * (unsigned)WPG * per >= nfr) return;   // no frame for this workgroup (device-sized lists)
+    // Each wave runs one contiguous frame range.  Guided (shared mode,
+    // a.sched == FE_SCHED_GUIDED): the last third of the waves -- dispatched
+    // last, in blockIdx order -- run a quarter share each and the others 4/3
+    // of one.  With equal shares the launch ended on the last-dispatched
+    // waves' whole ranges: ~0.3 ms over which the resident waves ran out one
+    // by one (wave timeline, profiles/r05/fe_sched/); the quarter shares fill
+    // those slots until the long ranges end, and end within ~0.1 ms.
+    // (development: a.sched bits 8-15 the tail waves in twelfths of the grid,
+    // 16-23 the share divisor; 0: 4 / 12 and 4)
+    const bool guided = shared && (a.sched & 0xff) == FE_SCHED_GUIDED;
+    const unsigned g12 = ((unsigned)a.sched >> 8) & 0xffu, gdv = ((unsigned)a.sched >> 16) & 0xffu;
+    const unsigned tw = guided ? nw * (g12 ? (g12 < 12u ? g12 : 11u) : 4u) / 12u : 0u, bw = nw - tw;
+    const unsigned dv = gdv ? gdv : 4u;
+    const unsigned Pb = guided ? (unsigned)(((unsigned long long)dv * nfr + (unsigned long long)dv * bw + tw - 1) /
+                                            ((unsigned long long)dv * bw + tw))
+                               : per;
+    const unsigned Ps = (Pb + dv - 1u) / dv;
+    auto range_of = [&](unsigned w, unsigned& b, unsigned& e) {
+        const unsigned long long s = w < bw ? (unsigned long long)w * Pb : (unsigned long long)bw * Pb + (unsigned long long)(w - bw) * Ps;
+        const unsigned long long t = s + (w < bw ? Pb : Ps);
+        b = s < nfr ? (unsigned)s : nfr;
+        e = t < nfr ? (unsigned)t : nfr;
+    };
+    {
+        unsigned b0, e0;
+        range_of(blockIdx.x * (unsigned)WPG, b0, e0);
+        if (b0 >= nfr) return;   // no frame for this workgroup (device-sized lists)
+    }
     // development probe (NNSP_RECUR_CLOCKS): per wave, wall clock (100 MHz) at
     // the start, after the tables, at the end, and the frames it ran
     const unsigned wid0 = blockIdx.x * (unsigned)WPG + (threadIdx.x >> 6);
@@ -424,8 +451,8 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
     __syncthreads();
     const unsigned wid = blockIdx.x * (unsigned)WPG + (unsigned)wv;
-    const unsigned fbeg = wid * per;
-    const unsigned fend = fbeg + per < nfr ? fbeg + per : nfr;
+    unsigned fbeg, fend;
+    range_of(wid, fbeg, fend);
     if (wclk) wclk[1] = (long long)__builtin_amdgcn_s_memrealtime();
     // frame f = (row i, k): stream s, segment start b, t = b + k (valid below
     // T); walked incrementally (no per-frame division)

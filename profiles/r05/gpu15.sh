@@ -1,0 +1,13 @@
+#!/bin/bash
+# shared front end schedule: static ranges / dynamic blocks with a fixed share / dynamic with the share
+# lifted once every wave has started; then wave timelines at five generations (every wave recorded)
+set -o pipefail
+O=gpurun_out/r05/g15; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_benchloop.py tests/test_gpu_cascade.py > $O/pytest.log 2>&1 || { echo "pytest failed"; tail -40 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash profiles/r05/ab2.sh fesched "NNSP_FE_DYN=0 NNSP_FE_OPEN=0 -" 4 || exit 1
+for V in NNSP_FE_DYN=0 NNSP_FE_OPEN=0 NNSP_FE_OPEN=1; do
+  env NNSP_FE_GENS=5 $V NNSP_LIB=abtest/probes2/nnsp_amd/libnnsp_mi355x.so timeout -k 10 200 python profiles/r03/wg_timeline.py 32768 $O/wg_$V.npz > $O/wg_$V.txt 2>&1 || { echo "wg_timeline failed"; tail -5 $O/wg_$V.txt; exit 1; }
+done
+echo all-ok
