@@ -97,18 +97,33 @@ def test_cascade_control_kernel(th, monkeypatch):
     assert _check(oc, gc, _pcm(S, sum(chunks), 12), chunks) > 50
 
 
+KNOB_VALUE = {"NNSP_CASCADE_WINDOW": "7", "NNSP_FE_SCHED": "0", "NNSP_FE_GUIDE": "6,8"}
+
+
 @pytest.mark.parametrize("knob", ["NNSP_CASCADE_SERIAL", "NNSP_CASCADE_DEBUG", "NNSP_CASCADE_TIMING",
-                                  "NNSP_CASCADE_WINDOW", "NNSP_RECUR_CLOCKS"])
+                                  "NNSP_CASCADE_WINDOW", "NNSP_RECUR_CLOCKS", "NNSP_FE_SCHED", "NNSP_FE_GUIDE",
+                                  "NNSP_EARLY_RETURN"])
 def test_cascade_development_knobs_keep_results(knob, monkeypatch):
     """The library's remaining environment switches are development aids --
     every net on one stream (SERIAL), a synchronisation after every launch
     (DEBUG), per-round event timing (TIMING), a fixed round window (WINDOW),
-    the s_memtime probes of the NN and front-end kernels (RECUR_CLOCKS): none
-    may change a result."""
-    monkeypatch.setenv(knob, "7" if knob == "NNSP_CASCADE_WINDOW" else "1")
+    the s_memtime probes of the NN and front-end kernels (RECUR_CLOCKS), the
+    shared front end's frame schedule (FE_SCHED: equal ranges; FE_GUIDE:
+    another guided split), the early return (EARLY_RETURN): none may change a
+    result."""
+    monkeypatch.setenv(knob, KNOB_VALUE.get(knob, "1"))
     S, chunks = 90, [100, 37, 1, 63]
     oc, gc, _ = _build(TH["lively"], S, max(chunks), False, (1, 2, 0), 80, 60, 80, 50)
     assert _check(oc, gc, _pcm(S, sum(chunks), 13), chunks) > 30
+
+
+@pytest.mark.parametrize("S", [1, 3, 17])
+def test_cascade_tiny_grids(S):
+    """Fewer frames than front-end waves (most waves of the guided schedule get
+    an empty range), 1- and 2-frame chunks, a single stream."""
+    chunks = [5, 1, 2, 9, 40]
+    oc, gc, _ = _build(TH["lively"], S, max(chunks), False, (1, 2, 0), 3, 7, 2, 5)
+    _check(oc, gc, _pcm(S, sum(chunks), 21 + S), chunks)
 
 
 @pytest.mark.parametrize("ctl", ["fused", "kernel"])
