@@ -219,7 +219,6 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     }
     const size_t S = (size_t)c->S, T = (size_t)c->Tmax;
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
-    if ((e = nnspk_stream_create(&c->bstream))) goto fail;
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
     if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
@@ -372,6 +371,9 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         {
             const char *er = getenv("NNSP_EARLY_RETURN");
             c->early = er ? atoi(er) != 0 : 0;
+            /* its book stream only when used: HIP has four hardware queues per
+             * process (GPU_MAX_HW_QUEUES), and the cascade and its nets hold four */
+            if (c->early && (e = nnspk_stream_create(&c->bstream))) goto fail;
         }
         c->debug = getenv("NNSP_CASCADE_DEBUG") != NULL;
         const char *w = getenv("NNSP_CASCADE_WINDOW");
@@ -971,7 +973,7 @@ int nnsp_cascade_sync(nnsp_cascade *c)
 {
     if (!c) return NNSP_EINVAL;
     TRY(nnspk_sync(c->stream));
-    TRY(nnspk_sync(c->bstream));
+    if (c->bstream) TRY(nnspk_sync(c->bstream));
     TRY(book_take(c));
     for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
     return 0;
@@ -1081,7 +1083,7 @@ static void cascade_state_segs(const nnsp_cascade *c, StateCopy *sc)
 static int cascade_quiesce(nnsp_cascade *c)
 {
     TRY(nnspk_sync(c->stream));
-    TRY(nnspk_sync(c->bstream));
+    if (c->bstream) TRY(nnspk_sync(c->bstream));
     for (int n = 0; n < 3; ++n) TRY(nnspk_sync(c->ns[n]));
     TRY(book_take(c));
     for (int q = 0; q < 2; ++q) TRY(ahead_read(c, q, 1));
