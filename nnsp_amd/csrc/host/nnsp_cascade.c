@@ -356,7 +356,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->serial = getenv("NNSP_CASCADE_SERIAL") != NULL;
         {
             const char *o = getenv("NNSP_R0_ORDER");
-            c->r0_order = o ? atoi(o) : 1;
+            c->r0_order = o ? atoi(o) : 6;
             const char *am = getenv("NNSP_AHEAD_MODE");
             c->ahead_mode = am ? atoi(am) : 1;
         }
@@ -571,25 +571,32 @@ static int launch_round(nnsp_cascade *c, CascArgs *a, int r, const int16_t *pcm,
     /* (measured and dropped, profiles/r02/sched: every net's cold front end
      * of a round before any net's NN kernels, VAD's recurrence after S2I's
      * and KWS's, every recur behind all three projs -- each -2..-7 %) */
-    /* round 0 with fused control: VAD (net 1) is launched first.  Until round
+    /* round 0 with fused control: until round 5, VAD (net 1) was launched first.  Until round
      * 4 S2I's and KWS's proj + recur waited for VAD's proj (r0_order 0;
      * profiles/r03: +1 % then).  With the faster proj and recurrences of
      * round 4 that wait only delayed S2I's and KWS's proj until VAD's 2 048
      * recurrence workgroups held every CU (KWS proj 164 -> 524 us, the round's
      * critical path); without it (r0_order 1) round 0 ends ~70 us earlier:
      * 1.080 vs 1.062 G (3 runs each), profiles/r04/r0_order/. */
+    /* round 5: S2I first (r0_order 6, the default since; its recurrence is the
+     * round's critical chain, trace in profiles/r05/chunk_trace): 1.2602 vs
+     * 1.2554 G, every one of 6 pairs, and 4 of 4 in another pass
+     * (profiles/r05/r0_order/).  casc_begin stays on VAD's stream: on S2I's or
+     * KWS's it measured 1.09 vs 1.21 G (profiles/r05/r0_order/begin_net/) */
     /* r0_order (NNSP_R0_ORDER, development): 0 S2I's and KWS's NN wait for
-     * VAD's proj; 1 (default) VAD launched first, nothing waits; 3 S2I and
+     * VAD's proj; 1 VAD launched first, nothing waits; 3 S2I and
      * KWS launched first, VAD's recurrence waits for their proj (1.059 G);
-     * 4 KWS, S2I, VAD and 5 VAD, KWS, S2I, nothing waits */
+     * 4 KWS, S2I, VAD, 5 VAD, KWS, S2I, 6 S2I, VAD, KWS and 7 S2I, KWS, VAD,
+     * nothing waits */
     static const int o_plain[3] = {0, 1, 2}, o_vad[3] = {1, 0, 2}, o_vad_last[3] = {0, 2, 1};
     static const int o_kws_first[3] = {2, 0, 1}, o_vad_kws[3] = {1, 2, 0};
     const int r0 = r == 0 && c->fused && !c->serial;
     const int vad_first = r0 && c->r0_order == 0;
     const int vad_last = r0 && c->r0_order == 3;
-    const int *order = vad_last ? o_vad_last
+    const int *order = vad_last || (r0 && c->r0_order == 7) ? o_vad_last
                      : (r0 && c->r0_order == 4 ? o_kws_first
-                        : (r0 && c->r0_order == 5 ? o_vad_kws : (r0 ? o_vad : o_plain)));
+                        : (r0 && c->r0_order == 5 ? o_vad_kws
+                           : (r0 && c->r0_order == 6 ? o_plain : (r0 ? o_vad : o_plain))));
     for (int i = 0; i < 3; ++i) {
         const int n = order[i];
         void *st = c->serial ? c->stream : c->ns[n];
