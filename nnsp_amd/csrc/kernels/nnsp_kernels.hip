@@ -1057,12 +1057,12 @@ struct alignas(16) NnLds {
 };
 
 __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
-                              int16_t* out, const int16_t* tt, int lane) {
+                              int16_t* out, const int16_t* tt, int lane, int rt0, int rstep) {
     v4i bh[NN_KT], bl[NN_KT];
     load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bh, bl);
     const int sc = lane & 15, q = lane >> 4;
     const uint8_t* A = img.A + Ly.a_off;
-    for (int rt = 0; rt < Ly.nrt; ++rt) {
+    for (int rt = rt0; rt < Ly.nrt; rt += rstep) {
         v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
         for (int kt = 0; kt < NN_KT; ++kt)
@@ -1092,7 +1092,7 @@ __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16
 // for a padding stream) stays in HBM: lane (sc, q) owns units 4*rt + q.
 __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
                                 int16_t* out, const int16_t* hbuf, int32_t* cg, const int16_t* tt,
-                                int lane, bool commit) {
+                                int lane, bool commit, int rt0, int rstep) {
     v4i bxh[NN_KT], bxl[NN_KT], bhh[NN_KT], bhl[NN_KT];
     load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
     load_b<NN_KT>(hbuf, NN_ASTRIDE, Ly.nkt_r, lane, bhh, bhl);
@@ -1100,7 +1100,7 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
     const uint8_t* A = img.A + Ly.a_off;
     const uint8_t* Ar = img.A + Ly.ar_off;
     const int acc32 = Ly.acc32;
-    for (int rt = 0; rt < Ly.nrt; ++rt) {
+    for (int rt = rt0; rt < Ly.nrt; rt += rstep) {
         v4i xh = {0, 0, 0, 0}, xl = {0, 0, 0, 0}, hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
 #pragma unroll
         for (int kt = 0; kt < NN_KT; ++kt)
@@ -1142,36 +1142,47 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
     }
 }
 
-__global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
+// One workgroup per 16-stream tile, NN_WAVES_MAX waves at most: wave w runs
+// row tiles w, w + waves, ... of every layer (an LSTM row tile holds whole
+// units, so the waves' units and cell states are disjoint), wave 0 the
+// context staging's share, the outputs and the post-processing.  A single
+// stream (the drop-in NNSPClass_exec) runs its layers on eight waves: one
+// wave walked every row tile's weight loads and MFMAs in sequence, ~30-75 us
+// of the call's 54-97 us (rocprofv3, profiles/r05/dropin_nn/).
+#define NN_WAVES_MAX 8
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) {
     __shared__ NnLds sm;
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int nwv = (int)(blockDim.x >> 6);
+    const bool w0 = wv == 0;
     const int sc = lane & 15;
     const int s0 = blockIdx.x * 16;
     const int s = s0 + sc;
     const bool valid = s < r.S;
-    for (int i = lane; i < 384; i += 64) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
+    for (int i = threadIdx.x; i < 384; i += blockDim.x) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
     // LSTM state rows (neural_nets.c:27-42 layout: h int16[N], c int32[N]) of
     // stream gs, layer l: r.h / r.c + (gs * n_lstm + l) * hs
     const size_t hs = (size_t)r.hs;
     PostState ps = {};
-    if (lane < 16 && valid && r.post) ps = reinterpret_cast<const PostState*>(r.post)[s];
-    if (lane < 16) sm.slides[lane] = (valid && r.post) ? ps.slides : 1;
-    wave_lds_sync();
+    if (w0 && lane < 16 && valid && r.post) ps = reinterpret_cast<const PostState*>(r.post)[s];
+    if (w0 && lane < 16) sm.slides[lane] = (valid && r.post) ? ps.slides : 1;
+    __syncthreads();
     const int phase = r.mode == NN_MODE_DIRECT ? 0 : 1 - sm.slides[sc];
     const int T = r.mode == NN_MODE_DIRECT ? 1 : r.T;
     const int nsteps = (T + 1) / 2;
     const int nl = r.nl_run;
-    if (lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
+    if (w0 && lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
 
     for (int j = 0; j < nsteps; ++j) {
         const int t = 2 * j + phase;
         const bool active = valid && t < T;
-        if (lane < 16) sm.active[lane] = active;
+        if (w0 && lane < 16) sm.active[lane] = active;
         // ---- context window V[t..t+5], V = prev5 ++ feats (feature_module.c:54-57)
         {
-            const int q = lane >> 4;
+            const int q = (int)(threadIdx.x >> 4) & 3, qs = 4 * nwv, q0 = q + 4 * wv;
             const int nch = r.mode == NN_MODE_DIRECT ? (img.L[0].K + 7) / 8 : 30;
-            for (int cch = q; cch < nch; cch += 4) {
+            for (int cch = q0; cch < nch; cch += qs) {
                 const int m = cch / 5, part = cch - 5 * m;
                 int4 v = make_int4(0, 0, 0, 0);
                 if (active) {
@@ -1188,7 +1199,7 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
                 *reinterpret_cast<int4*>(&sm.act[0][sc][8 * cch]) = v;
             }
         }
-        wave_lds_sync();
+        __syncthreads();
         int lst = 0;
         for (int i = 0; i < nl; ++i) {
             const NnLayer& Ly = img.L[i];
@@ -1200,29 +1211,29 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
                 // must be visible to these loads: an explicit workgroup-scope
                 // fence rather than reliance on in-order vector memory
                 __threadfence_block();
-                for (int idx = lane; idx < 16 * N; idx += 64) {   // stage h (the previous step's)
+                for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {   // stage h (the previous step's)
                     const int st = idx / N, u = idx - st * N, gs = s0 + st;
                     sm.h[st][u] = gs < r.S ? r.h[((size_t)gs * img.n_lstm + lst) * hs + u] : (int16_t)0;
                 }
-                wave_lds_sync();
+                __syncthreads();
                 int32_t* cg = valid ? r.c + ((size_t)s * img.n_lstm + lst) * hs : nullptr;
-                lstm_layer_mfma(img, Ly, in, out, &sm.h[0][0], cg, sm.tanh_tbl, lane, active);
-                wave_lds_sync();
+                lstm_layer_mfma(img, Ly, in, out, &sm.h[0][0], cg, sm.tanh_tbl, lane, active, wv, nwv);
+                __syncthreads();
                 // h_state := output after all groups (lstm.c:205-206)
-                for (int idx = lane; idx < 16 * N; idx += 64) {
+                for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
                     const int st = idx / N, u = idx - st * N, gs = s0 + st;
                     if (sm.active[st]) r.h[((size_t)gs * img.n_lstm + lst) * hs + u] = out[st * NN_ASTRIDE + u];
                 }
                 ++lst;
             } else {
-                fc_layer_mfma(img, Ly, in, out, sm.tanh_tbl, lane);
+                fc_layer_mfma(img, Ly, in, out, sm.tanh_tbl, lane, wv, nwv);
             }
-            wave_lds_sync();
+            __syncthreads();
         }
         const int16_t* fin = &sm.act[nl & 1][sc][0];
         const int nout = img.L[nl - 1].N;
         const bool lin = img.L[nl - 1].act == ACT_LINEAR;
-        if (active && r.logits) {
+        if (w0 && active && r.logits) {
             // each lane group q copies a quarter of its stream's outputs
             const int q = lane >> 4;
             if (r.mode == NN_MODE_DIRECT) {
@@ -1239,7 +1250,7 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
                     dst[o] = lin ? reinterpret_cast<const int32_t*>(fin)[o] : (int32_t)fin[o];
             }
         }
-        if (r.mode != NN_MODE_DIRECT && lane < 16 && active) {
+        if (w0 && r.mode != NN_MODE_DIRECT && lane < 16 && active) {
             const LogitRow lg = {fin, lin};
             post_proc(ps, img, lg);
             if (r.trig) {
@@ -1247,9 +1258,9 @@ __global__ __launch_bounds__(64) void nn_kernel(NnImage img, NnRun r) {
                 if (t + 1 < T) r.trig[(size_t)s * T + t + 1] = ps.trigger;
             }
         }
-        wave_lds_sync();
+        __syncthreads();
     }
-    if (r.mode != NN_MODE_DIRECT && lane < 16 && valid && r.post) {
+    if (w0 && r.mode != NN_MODE_DIRECT && lane < 16 && valid && r.post) {
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
@@ -1931,7 +1942,11 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
 int nnspk_launch_nn(const NnImage* img, const NnRun* r, void* stream) {
     if (r->S <= 0) return 0;
     if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);   // h / c row stride unset
-    hipLaunchKernelGGL(nn_kernel, dim3((r->S + 15) / 16), dim3(64), 0, (hipStream_t)stream, *img, *r);
+    // few tiles (the drop-in single stream): eight waves per tile share each
+    // layer's row tiles; many: one wave per tile, many tiles per CU
+    const int tiles = (r->S + 15) / 16;
+    const int waves = tiles <= 32 ? NN_WAVES_MAX : 1;
+    hipLaunchKernelGGL(nn_kernel, dim3(tiles), dim3(64 * waves), 0, (hipStream_t)stream, *img, *r);
     return ok(hipGetLastError());
 }
 
