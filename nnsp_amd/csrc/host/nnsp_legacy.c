@@ -38,8 +38,13 @@ static struct {
     jmp_buf jb;
     int sticky;  /* first error since nnsp_legacy_clear(); 0 = none */
     int port;    /* 1: the reference's ARM_OPTIMIZED=0 build (row N4); 2: not yet read */
-    uint8_t *hpin;  /* pinned host staging of NNSPClass_exec: one upload, one download per frame */
+    uint8_t *hpin;  /* pinned host staging of NNSPClass_exec (NNSP_DROPIN_COPY=1: one upload, one download) */
     size_t hpin_cap;
+    /* the same staging in mapped, coherent host memory: the front-end kernel
+     * reads the call's inputs from it and the NN kernel writes the results to
+     * it, in place of the two copies (NNSP_DROPIN_COPY=1: the copies) */
+    uint8_t *hmap, *hmap_dev;
+    int copy;
     void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
 } G = {.port = 2};
 
@@ -92,6 +97,11 @@ static int gctx(void)
     if ((e = nnspk_malloc((void **)&G.arena, G.cap))) return e;
     G.hpin_cap = 64u << 10;
     if ((e = nnspk_host_alloc((void **)&G.hpin, G.hpin_cap))) return e;
+    {
+        const char *cp = getenv("NNSP_DROPIN_COPY");
+        G.copy = cp && atoi(cp) != 0;
+    }
+    if (!G.copy && (e = nnspk_host_alloc_mapped((void **)&G.hmap, (void **)&G.hmap_dev, G.hpin_cap))) return e;
     G.ready = 1;
     return 0;
 }
@@ -893,11 +903,14 @@ static void post_unpack(NNSPClass *p, const NnPost *q)
 
 static size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
 
-/* One frame as a GPU batch of one stream.  Everything the call reads goes up
- * in one copy from a pinned staging buffer, everything it returns comes back
- * in one (per frame: one upload, the front end, the NN, one download, one
- * synchronisation; separate small copies from pageable memory made a frame
- * ~160-250 us, bench.py --dropin-latency). */
+/* One frame as a GPU batch of one stream.  Everything the call reads and
+ * returns sits in one staging buffer of mapped host memory: the front-end
+ * kernel copies the inputs to device memory before its frame, the NN kernel
+ * copies the results back after its layers (per frame: two launches and one
+ * synchronisation).  NNSP_DROPIN_COPY=1: a pinned buffer with one upload and
+ * one download around the launches (round 5 before this; separate small
+ * copies from pageable memory made a frame ~160-250 us, bench.py
+ * --dropin-latency). */
 static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
 {
     FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
@@ -919,7 +932,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     const size_t o_feat = o_c + al16(rows * hs * 4), o_log = o_feat + 80, o_trig = o_log + 160;
     const size_t total = al16(o_trig + 2);
     if (total > G.hpin_cap) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
-    uint8_t *hp = G.hpin;
+    uint8_t *hp = G.copy ? G.hpin : G.hmap;
     memcpy(hp + o_pcm, rawPCM, 320);
     memcpy(hp + o_tail, fe->state_stftModule.dataBuffer + 160, 640);
     memcpy(hp + o_mean, fe->pt_norm_mean, 160);
@@ -940,9 +953,14 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
             }
     }
     uint8_t *d = (uint8_t *)dscratch(total);
-    CK(nnspk_h2d(d, hp, o_feat, G.stream));
+    if (G.copy) CK(nnspk_h2d(d, hp, o_feat, G.stream));
     FeArgs a;
     memset(&a, 0, sizeof a);
+    if (!G.copy) { /* (o_feat: a multiple of 16) */
+        a.in_src = G.hmap_dev;
+        a.in_dst = d;
+        a.in_bytes = (int32_t)o_feat;
+    }
     a.pcm = (const int16_t *)(d + o_pcm);
     a.tail = (const int16_t *)(d + o_tail);
     a.S = 1; a.T = 1;
@@ -971,8 +989,13 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     r.c = (int32_t *)(d + o_c);
     r.post = d + o_post;
     r.trig = (int16_t *)(d + o_trig);
+    if (!G.copy) { /* (o_post and total: multiples of 16) */
+        r.out_src = d + o_post;
+        r.out_dst = G.hmap_dev + o_post;
+        r.out_bytes = (int32_t)(total - o_post);
+    }
     CK(nnspk_launch_nn(&img, &r, G.stream));
-    CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
+    if (G.copy) CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
     fin();
     memcpy(&ps, hp + o_post, sizeof ps);
     {

@@ -87,6 +87,12 @@ typedef struct {
      * log, window, Mel) prebuilt for this mode / build by nnspk_build_fe_tables,
      * copied with 16-byte loads instead of being derived per workgroup */
     const void *tb_img;
+    /* one-workgroup launches (the drop-in call): before anything else, the
+     * workgroup copies in_bytes (a multiple of 16) from in_src (mapped host
+     * memory) to in_dst in place of a separate host-to-device copy */
+    const void *in_src;
+    void *in_dst;
+    int32_t in_bytes, pad4_;
 } FeArgs;
 #define FE_SCHED_EQUAL 0   /* equal contiguous ranges per wave */
 #define FE_SCHED_GUIDED 1  /* the last-dispatched third of the waves on quarter ranges */
@@ -157,6 +163,12 @@ typedef struct {
     int32_t *logits;          /* STREAM: [S][T][nout] (NN frames only); DIRECT: [S][out_stride] */
     int32_t out_stride;
     int32_t hs;               /* h / c elements per LSTM row (>= the widest LSTM, multiple of 8) */
+    /* one-workgroup launches (the drop-in call): after everything else, the
+     * workgroup copies out_bytes (a multiple of 16) from out_src to out_dst
+     * (mapped host memory) in place of a separate device-to-host copy */
+    const void *out_src;
+    void *out_dst;
+    int32_t out_bytes, pad_;
 } NnRun;
 
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
@@ -278,6 +290,9 @@ int nnspk_memset(void *p, int v, size_t n, void *stream);
 int nnspk_h2d(void *d, const void *h, size_t n, void *stream);
 int nnspk_d2h(void *h, const void *d, size_t n, void *stream);
 int nnspk_host_alloc(void **p, size_t n);   /* pinned host memory (asynchronous copies) */
+/* pinned, coherent host memory that kernels read and write in place (*dev: the
+ * address kernels use) */
+int nnspk_host_alloc_mapped(void **p, void **dev, size_t n);
 int nnspk_host_free(void *p);
 int nnspk_event_sync(void *e);
 int nnspk_event_done(void *e);              /* 1: the event has completed (no wait) */

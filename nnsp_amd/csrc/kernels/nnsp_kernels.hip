@@ -437,6 +437,13 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
     const unsigned wid0 = blockIdx.x * (unsigned)WPG + (threadIdx.x >> 6);
     long long* wclk = (NNSP_PROBES && a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    // the drop-in call's inputs, from mapped host memory (one workgroup; the
+    // waves read them -- mean / stdR first -- only after this barrier)
+    if (a.in_bytes) {
+        for (int i = threadIdx.x; i < a.in_bytes / 16; i += blockDim.x)
+            reinterpret_cast<int4*>(a.in_dst)[i] = reinterpret_cast<const int4*>(a.in_src)[i];
+        __syncthreads();
+    }
     fe_tables_load<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1264,6 +1271,12 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRu
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
+    if (r.out_bytes) {   // the drop-in call's results, to mapped host memory (one workgroup)
+        __threadfence();
+        __syncthreads();
+        for (int i = threadIdx.x; i < r.out_bytes / 16; i += blockDim.x)
+            reinterpret_cast<int4*>(r.out_dst)[i] = reinterpret_cast<const int4*>(r.out_src)[i];
+    }
 }
 
 // prev5 := last 5 frames of V = prev5 ++ feats[b..T) after the segment; one
@@ -2071,6 +2084,11 @@ int nnspk_d2d(void* d, const void* s, size_t n, void* stream) {
 int nnspk_sync(void* stream) { return ok(hipStreamSynchronize((hipStream_t)stream)); }
 int nnspk_host_alloc(void** p, size_t n) { return ok(hipHostMalloc(p, n ? n : 16, hipHostMallocDefault)); }
 int nnspk_host_free(void* p) { return p ? ok(hipHostFree(p)) : 0; }
+int nnspk_host_alloc_mapped(void** p, void** dev, size_t n) {
+    hipError_t e = hipHostMalloc(p, n ? n : 16, hipHostMallocMapped | hipHostMallocCoherent);
+    if (e != hipSuccess) return ok(e);
+    return ok(hipHostGetDevicePointer(dev, *p, 0));
+}
 int nnspk_event_sync(void* e) { return ok(hipEventSynchronize((hipEvent_t)e)); }
 int nnspk_event_done(void* e) { return hipEventQuery((hipEvent_t)e) == hipSuccess; }
 int nnspk_event_spin(void* e) {
