@@ -438,12 +438,11 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
     long long* wclk = (NNSP_PROBES && a.dbg_clk && (threadIdx.x & 63) == 0 && wid0 < 32768u) ? a.dbg_clk + 2048 + 4 * wid0 : nullptr;
     if (wclk) wclk[0] = (long long)__builtin_amdgcn_s_memrealtime();
     // the drop-in call's inputs, from mapped host memory (one workgroup; the
-    // waves read them -- mean / stdR first -- only after this barrier)
-    if (a.in_bytes) {
+    // waves read them only after the barrier behind the tables, whose loads
+    // overlap these)
+    if (a.in_bytes)
         for (int i = threadIdx.x; i < a.in_bytes / 16; i += blockDim.x)
             reinterpret_cast<int4*>(a.in_dst)[i] = reinterpret_cast<const int4*>(a.in_src)[i];
-        __syncthreads();
-    }
     fe_tables_load<PORT>(TB, a);
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -454,9 +453,10 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
     int64_t* Mp = reinterpret_cast<int64_t*>(X);
     FeLane L;
     fe_lane_init(L, lane);
+    __syncthreads();
+    // (after the barrier: the drop-in call copies them in above)
     const int32_t mean = lane < 40 ? a.mean[lane] : 0;
     const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
-    __syncthreads();
     const unsigned wid = blockIdx.x * (unsigned)WPG + (unsigned)wv;
     unsigned fbeg, fend;
     range_of(wid, fbeg, fend);
