@@ -904,9 +904,9 @@ static void post_unpack(NNSPClass *p, const NnPost *q)
 static size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
 
 /* One frame as a GPU batch of one stream.  Everything the call reads and
- * returns sits in one staging buffer of mapped host memory: the front-end
- * kernel copies the inputs to device memory before its frame, the NN kernel
- * copies the results back after its layers (per frame: two launches and one
+ * returns sits in one staging buffer of mapped host memory; one kernel
+ * (dropin_kernel) copies the inputs to device memory, runs the front end and
+ * the NN, and copies the results back (per frame: one launch and one
  * synchronisation).  NNSP_DROPIN_COPY=1: a pinned buffer with one upload and
  * one download around the launches (round 5 before this; separate small
  * copies from pageable memory made a frame ~160-250 us, bench.py
@@ -978,7 +978,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         CK(nnspk_build_fe_tables(&G.fetab[a.port], &ta, G.stream));
     }
     a.tb_img = G.fetab[a.port];
-    CK(nnspk_launch_fe(&a, G.stream));
+    if (G.copy) CK(nnspk_launch_fe(&a, G.stream));
     NnRun r;
     memset(&r, 0, sizeof r);
     r.S = 1; r.T = 1; r.mode = NN_MODE_STREAM; r.nl_run = img.nl;
@@ -994,8 +994,12 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         r.out_dst = G.hmap_dev + o_post;
         r.out_bytes = (int32_t)(total - o_post);
     }
-    CK(nnspk_launch_nn(&img, &r, G.stream));
-    if (G.copy) CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
+    if (G.copy) {
+        CK(nnspk_launch_nn(&img, &r, G.stream));
+        CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
+    } else {   /* the front end and the NN in one launch */
+        CK(nnspk_launch_dropin(&a, &img, &r, G.stream));
+    }
     fin();
     memcpy(&ps, hp + o_post, sizeof ps);
     {

@@ -247,6 +247,9 @@ int nnspk_build_fe_tables(void **out, const FeArgs *a, void *stream);
 int nnspk_launch_nring_fill(int16_t *const nring[3], const int32_t *const nmean[3], const int32_t *const nstdR[3],
                             const int32_t nshift[3], int ring, const uint8_t *mask, int S, void *stream);
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
+/* the drop-in call's front end (FE_MODE_BATCH, one stream, one frame) and NN
+ * (NN_MODE_STREAM, T = 1) in one launch */
+int nnspk_launch_dropin(const FeArgs *a, const NnImage *img, const NnRun *r, void *stream);
 int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
                           int n_list, const int32_t *seg_begin, int seg_len, void *stream);
 int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, const int32_t *list,

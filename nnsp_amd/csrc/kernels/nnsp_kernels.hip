@@ -388,9 +388,10 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // 80-VGPR budget of six waves per SIMD without the shared mode's ring writes.
 // PORT: the ARM_OPTIMIZED=0 build's front end (row N4: Frac15 window, fft.c's
 // rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
-template <int MODE, bool PORT>
-__global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>::MINW)) void fe_kernel(FeArgs a) {
-    constexpr int WPG = FeGeom<MODE, PORT>::WPG;
+// fe_body: the kernel's work on WPG waves (fe_kernel: FeGeom's; the drop-in
+// call's fused kernel: eight)
+template <int MODE, bool PORT, int WPG>
+__device__ __forceinline__ void fe_body(FeArgs a) {
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
     // contiguous so that the padded T1 transpose may use both
@@ -752,6 +753,10 @@ __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>
         wclk[3] = (long long)(fend - fbeg) | (nnsp_hw_where() << 32);
     }
 #undef FCLK
+}
+template <int MODE, bool PORT>
+__global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>::MINW)) void fe_kernel(FeArgs a) {
+    fe_body<MODE, PORT, FeGeom<MODE, PORT>::WPG>(a);
 }
 // ---- two frames per wave (FE_MODE_BATCH / FE_MODE_SHARED) -----------------
 // The same per-frame arithmetic as fe_kernel, with two frames' instruction
@@ -1157,7 +1162,7 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
 // wave walked every row tile's weight loads and MFMAs in sequence, ~30-75 us
 // of the call's 54-97 us (rocprofv3, profiles/r05/dropin_nn/).
 #define NN_WAVES_MAX 8
-__global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) {
+__device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
     __shared__ NnLds sm;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1277,6 +1282,17 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRu
         for (int i = threadIdx.x; i < r.out_bytes / 16; i += blockDim.x)
             reinterpret_cast<int4*>(r.out_dst)[i] = reinterpret_cast<const int4*>(r.out_src)[i];
     }
+}
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) { nn_body(img, r); }
+
+// The drop-in call (NNSPClass_exec, one stream, one frame) in one launch: the
+// front end on eight waves (wave 0 has the frame), then the NN; the barrier
+// makes the front end's feature row visible to the NN's staging
+template <bool PORT>
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r) {
+    fe_body<FE_MODE_BATCH, PORT, NN_WAVES_MAX>(a);
+    __syncthreads();
+    nn_body(img, r);
 }
 
 // prev5 := last 5 frames of V = prev5 ++ feats[b..T) after the segment; one
@@ -1949,6 +1965,16 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
         f.nshift[n] = nshift[n];
     }
     hipLaunchKernelGGL(nring_fill_kernel, dim3(S), dim3(256), 0, (hipStream_t)stream, f, ring, mask, S);
+    return ok(hipGetLastError());
+}
+
+int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, void* stream) {
+    if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
+    if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
+    if (a->port)
+        hipLaunchKernelGGL(dropin_kernel<true>, dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+    else
+        hipLaunchKernelGGL(dropin_kernel<false>, dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
     return ok(hipGetLastError());
 }
 
