@@ -165,10 +165,14 @@ typedef struct {
     int32_t hs;               /* h / c elements per LSTM row (>= the widest LSTM, multiple of 8) */
     /* one-workgroup launches (the drop-in call): after everything else, the
      * workgroup copies out_bytes (a multiple of 16) from out_src to out_dst
-     * (mapped host memory) in place of a separate device-to-host copy */
+     * (mapped host memory) in place of a separate device-to-host copy; then,
+     * if done is non-NULL (mapped host memory too), stores done_seq to it with
+     * system-scope release: a host polling that word sees the results without
+     * waiting for the stream (the kernel's end and its completion signal) */
     const void *out_src;
     void *out_dst;
-    int32_t out_bytes, pad_;
+    int32_t out_bytes, done_seq;
+    uint32_t *done;
 } NnRun;
 
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
@@ -302,6 +306,8 @@ int nnspk_event_done(void *e);              /* 1: the event has completed (no wa
 int nnspk_event_spin(void *e);              /* wait for the event by polling it (no sleep / wake-up latency) */
 int nnspk_d2d(void *d, const void *s, size_t n, void *stream);
 int nnspk_sync(void *stream);
+int nnspk_stream_spin(void *stream);  /* wait for the stream by polling it (no sleep / wake-up latency) */
+int nnspk_stream_done(void *stream);  /* 1: complete, 0: work pending, < 0: minus the error code */
 int nnspk_device_count(int *n);
 int nnspk_set_device(int d);
 int nnspk_get_device(int *d);

@@ -1281,6 +1281,12 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
         __syncthreads();
         for (int i = threadIdx.x; i < r.out_bytes / 16; i += blockDim.x)
             reinterpret_cast<int4*>(r.out_dst)[i] = reinterpret_cast<const int4*>(r.out_src)[i];
+        if (r.done) {   // every wave's result stores complete at system scope, then the completion word
+            __threadfence_system();
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(r.done, (uint32_t)r.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 __global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) { nn_body(img, r); }
@@ -2114,6 +2120,17 @@ int nnspk_host_alloc_mapped(void** p, void** dev, size_t n) {
     hipError_t e = hipHostMalloc(p, n ? n : 16, hipHostMallocMapped | hipHostMallocCoherent);
     if (e != hipSuccess) return ok(e);
     return ok(hipHostGetDevicePointer(dev, *p, 0));
+}
+int nnspk_stream_spin(void* stream) {
+    for (;;) {
+        const hipError_t r = hipStreamQuery((hipStream_t)stream);
+        if (r == hipSuccess) return 0;
+        if (r != hipErrorNotReady) return ok(r);
+    }
+}
+int nnspk_stream_done(void* stream) {
+    const hipError_t r = hipStreamQuery((hipStream_t)stream);
+    return r == hipSuccess ? 1 : (r == hipErrorNotReady ? 0 : -ok(r));
 }
 int nnspk_event_sync(void* e) { return ok(hipEventSynchronize((hipEvent_t)e)); }
 int nnspk_event_done(void* e) { return hipEventQuery((hipEvent_t)e) == hipSuccess; }
