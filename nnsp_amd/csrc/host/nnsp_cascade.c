@@ -221,12 +221,20 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_stream_create(&c->stream))) goto fail;
     for (int i = 0; i < 2; ++i)
         if ((e = nnspk_event_create(&c->ev[i])) || (e = nnspk_event_create(&c->ev_fe[i]))) goto fail;
-    if ((e = nnspk_event_create(&c->ev_fork))) goto fail;
+    /* the events that only order streams (and the host's wait on the counter
+     * copy) carry no timestamps: the waits behind them resolve sooner (gaps
+     * between rounds 20-24 -> 13-20 us in the stress case's kernel trace;
+     * cascade 1.2454 -> 1.2569 and 1.2196 -> 1.2358 G, 9 of 11 pairs,
+     * profiles/r05/dep_events/).  NNSP_DEP_EVENTS=0: timed events throughout */
+    const char *dv = getenv("NNSP_DEP_EVENTS");
+    const int dep = dv ? atoi(dv) : 1;
+#define DEP_EVENT(p) (dep ? nnspk_event_create_dep(p) : nnspk_event_create(p))
+    if ((e = DEP_EVENT(&c->ev_fork))) goto fail;
     for (int q = 0; q < 2; ++q)
         if ((e = nnspk_event_create(&c->ev_ahead[q][0])) || (e = nnspk_event_create(&c->ev_ahead[q][1]))) goto fail;
-    if ((e = nnspk_event_create(&c->ev_vad_proj))) goto fail;
+    if ((e = DEP_EVENT(&c->ev_vad_proj))) goto fail;
     for (int n = 0; n < 3; ++n)
-        if ((e = nnspk_event_create(&c->ev_r0proj[n])) || (e = nnspk_event_create(&c->ev_r1proj[n]))) goto fail;
+        if ((e = DEP_EVENT(&c->ev_r0proj[n])) || (e = DEP_EVENT(&c->ev_r1proj[n]))) goto fail;
     for (int n = 0; n < 3; ++n) {
         /* each net's rounds run on its batch's own stream: the cascade adds
          * one stream (c->stream) to the three, so on a device with four
@@ -241,8 +249,7 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
                 c->ns[n] = c->own_ns[n];
             }
         }
-        if ((e = nnspk_event_create(&c->ev_join[n])) || (e = nnspk_event_create(&c->ev_rnd[0][n])) ||
-            (e = nnspk_event_create(&c->ev_rnd[1][n])))
+        if ((e = DEP_EVENT(&c->ev_join[n])) || (e = DEP_EVENT(&c->ev_rnd[0][n])) || (e = DEP_EVENT(&c->ev_rnd[1][n])))
             goto fail;
         for (int r = 0; r < MAX_TIMED; ++r)
             for (int i = 0; i < 3; ++i)
@@ -253,7 +260,8 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
     if ((e = nnspk_malloc((void **)&c->d_zero, 2 * ZERO_STRIDE))) goto fail;
     if ((e = nnspk_memset(c->d_zero, 0, 2 * ZERO_STRIDE, c->stream))) goto fail;
     if ((e = nnspk_host_alloc(&c->h_book, ZERO_BYTES))) goto fail;
-    if ((e = nnspk_event_create(&c->ev_book))) goto fail;
+    if ((e = DEP_EVENT(&c->ev_book))) goto fail;
+#undef DEP_EVENT
     zero_bind(c, 0);
     if ((e = nnspk_malloc((void **)&c->d_seg_begin, S * 4))) goto fail;
     /* list lengths of 3 rounds in flight: 3 lists + 3 cold lists each */

@@ -318,6 +318,7 @@ int nnspk_stream_create(void **s);
 int nnspk_stream_create_prio(void **s, int high);
 int nnspk_stream_destroy(void *s);
 int nnspk_event_create(void **e);
+int nnspk_event_create_dep(void **e); /* no timestamps: ordering between streams and host waits only */
 int nnspk_event_destroy(void *e);
 int nnspk_event_record(void *e, void *stream);
 int nnspk_event_elapsed(float *ms, void *a, void *b);

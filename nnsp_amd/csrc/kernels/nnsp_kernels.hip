@@ -2154,6 +2154,7 @@ int nnspk_stream_create_prio(void** s, int high) {
 }
 int nnspk_stream_destroy(void* s) { return s ? ok(hipStreamDestroy((hipStream_t)s)) : 0; }
 int nnspk_event_create(void** e) { return ok(hipEventCreate((hipEvent_t*)e)); }
+int nnspk_event_create_dep(void** e) { return ok(hipEventCreateWithFlags((hipEvent_t*)e, hipEventDisableTiming)); }
 int nnspk_event_destroy(void* e) { return e ? ok(hipEventDestroy((hipEvent_t)e)) : 0; }
 int nnspk_event_record(void* e, void* stream) { return ok(hipEventRecord((hipEvent_t)e, (hipStream_t)stream)); }
 int nnspk_stream_wait(void* stream, void* event) {
