@@ -107,6 +107,10 @@ int nnsp_synth_pcm_mix(int16_t *dev_out, int S, int T, uint64_t seed, int s0, in
 int nnsp_device_count(int *n);
 int nnsp_set_device(int dev);
 int nnsp_device_info(int *compute_units, int *clock_khz, char *arch, int arch_len);
+/* error codes (negative: argument / validation; positive: HIP runtime) */
+#define NNSP_EINVAL (-1)
+#define NNSP_EUNSUPPORTED (-2)
+#define NNSP_ENOMEM (-3)
 const char *nnsp_strerror(int code);
 
 #ifdef __cplusplus

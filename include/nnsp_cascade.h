@@ -78,7 +78,11 @@ int nnsp_cascade_exec_device(nnsp_cascade *c, const int16_t *pcm, int T, int8_t 
  * that pointer and T; next_pcm must hold its final samples when passed and stay
  * unchanged until then (nnsp_cascade_reset drops the look-ahead).  Used when
  * the nets run concurrently (not in serial mode) and T, next_T >= the
- * look-back + 1; otherwise it is ignored.  Results are identical. */
+ * look-back + 1; otherwise it is ignored.  Results are identical.  next_pcm is
+ * read by the look-ahead front end until this call returns; with the
+ * development mode NNSP_EARLY_RETURN=1 (the call returns once the rounds are
+ * done) it is read until the next call on this cascade, nnsp_cascade_sync or
+ * nnsp_cascade_reset returns. */
 int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, const int16_t *next_pcm,
                                    int next_T, int8_t *net_ran, int16_t *detected, int16_t *outputs3);
 int nnsp_cascade_sync(nnsp_cascade *c);
@@ -166,8 +170,9 @@ int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
  *                                 1..5, LSTM h and c, post-processing state
  *
  * get waits for the cascade's work; set drops a look-ahead front end (the next
- * call recomputes its own).  Blobs carry H and a magic number; set refuses
- * blobs from a cascade with other look-backs (NNSP_EINVAL). */
+ * call recomputes its own).  Blobs carry H, their size and a signature of the
+ * three nets' state shapes (LSTM width and layers, outputs); set refuses blobs
+ * of a cascade with other look-backs or other nets (NNSP_EINVAL). */
 typedef struct {
     uint32_t magic;               /* NNSP_CASCADE_STATE_MAGIC */
     uint16_t hist_frames;         /* H */
@@ -177,9 +182,13 @@ typedef struct {
     uint16_t cnt_timeout_s2i;
     int16_t reserved0;
     int8_t frames_since_reset;    /* frames the current net ran since its reset (0, 1, 2 = 2 or more) */
-    int8_t reserved1[15];
+    int8_t reserved1[3];
+    uint32_t state_bytes;         /* nnsp_cascade_state_bytes() of the cascade that wrote it */
+    uint32_t nets_sig;            /* FNV-1a of each net's state shape (NNSP_ID order) */
+    uint32_t reserved2;
 } nnsp_cascade_stream_hdr;
 #define NNSP_CASCADE_STATE_MAGIC 0x3153434eu   /* "NCS1" */
+#define NNSP_CASCADE_STATE_VERSION 2
 size_t nnsp_cascade_state_bytes(const nnsp_cascade *c);
 int nnsp_cascade_get_state(nnsp_cascade *c, void *host, int first, int count);
 int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int count);

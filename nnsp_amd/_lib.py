@@ -85,6 +85,8 @@ class PostState(C.Structure):
 
 P = C.c_void_p
 I = C.c_int
+# error codes (include/nnsp_batch.h)
+NNSP_EINVAL, NNSP_EUNSUPPORTED, NNSP_ENOMEM = -1, -2, -3
 
 
 def _declare(L: C.CDLL) -> None:

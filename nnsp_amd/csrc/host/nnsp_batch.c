@@ -549,17 +549,34 @@ int nnsp_batch_state_segs(const nnsp_batch *b, StateSeg *seg, size_t off, size_t
     return 5;
 }
 
+/* through one device staging buffer of at most NNSP_STATE_STAGE bytes, in
+ * batches of streams: a whole large shard at once needed a transient
+ * allocation of hundreds of MB, whose failure left the caller unable to
+ * checkpoint */
+#define NNSP_STATE_STAGE ((size_t)16 << 20)
 int nnsp_state_xfer(StateCopy *sc, void *host, void *stream)
 {
     if (sc->count == 0) return 0;
+    const int first = sc->first, count = sc->count;
+    size_t per_batch = NNSP_STATE_STAGE / sc->per;
+    if (per_batch < 1) per_batch = 1;
+    const int nb = (int)((size_t)count < per_batch ? (size_t)count : per_batch);
     void *d = NULL;
-    const size_t n = (size_t)sc->count * sc->per;
-    int e = nnspk_malloc(&d, n);
+    int e = nnspk_malloc(&d, (size_t)nb * sc->per);
     if (e) return e;
-    if (!sc->to_blob) e = nnspk_h2d(d, host, n, stream);
-    if (!e) e = nnspk_launch_state_copy(sc, d, stream);
-    if (!e && sc->to_blob) e = nnspk_d2h(host, d, n, stream);
-    if (!e) e = nnspk_sync(stream);
+    for (int i = 0; i < count && !e; i += nb) {
+        const int k = count - i < nb ? count - i : nb;
+        char *hb = (char *)host + (size_t)i * sc->per;
+        const size_t n = (size_t)k * sc->per;
+        sc->first = first + i;
+        sc->count = k;
+        if (!sc->to_blob) e = nnspk_h2d(d, hb, n, stream);
+        if (!e) e = nnspk_launch_state_copy(sc, d, stream);
+        if (!e && sc->to_blob) e = nnspk_d2h(hb, d, n, stream);
+        if (!e) e = nnspk_sync(stream);
+    }
+    sc->first = first;
+    sc->count = count;
     nnspk_free(d);
     return e;
 }

@@ -818,7 +818,11 @@ int nnsp_cascade_exec_device_ahead(nnsp_cascade *c, const int16_t *pcm, int T, c
     if (ahead_done && c->early_prev) TRY(nnspk_stream_wait(bst, c->ev_ahead[k & 1][1]));
     TRY(nnspk_launch_casc_begin(&a, bst));
     DBG(bst, "casc_begin", -1, -1);
-    if (ahead_done) TRY(nnspk_event_record(c->ev[0], c->stream));   /* c->stream is idle: about now */
+    /* c->stream is idle: about now -- except after an early return, when the
+     * look-ahead front end may still run on it: ev[0] then goes on bst, behind
+     * the wait for that front end, so that it completes before ev[1] (on the
+     * book stream) and book_take's elapsed time is always ready */
+    if (ahead_done) TRY(nnspk_event_record(c->ev[0], c->early_prev ? bst : c->stream));
     if (c->fused) TRY(nnspk_event_record(c->ev_fork, bst));
     int ahead_launched = 0, behind_launched = 0;
     /* the look-ahead front end starts once the nets' first round (the bulk of
@@ -1095,6 +1099,21 @@ static void cascade_state_segs(const nnsp_cascade *c, StateCopy *sc)
     sc->per = off;
 }
 
+/* the nets' state shapes, as set_state must find them (a blob of other nets
+ * of the same size would otherwise be imported silently) */
+static uint32_t cascade_nets_sig(const nnsp_cascade *c)
+{
+    uint32_t h = 2166136261u;
+    for (int n = 0; n < 3; ++n) {
+        const nnsp_batch *b = c->net[n];
+        const uint32_t v[4] = {(uint32_t)b->hs, (uint32_t)b->im.img.n_lstm, (uint32_t)b->nout,
+                               (uint32_t)nnsp_batch_state_bytes(b)};
+        for (int i = 0; i < 4; ++i)
+            for (int k = 0; k < 4; ++k) h = (h ^ ((v[i] >> (8 * k)) & 0xffu)) * 16777619u;
+    }
+    return h;
+}
+
 static int cascade_quiesce(nnsp_cascade *c)
 {
     TRY(nnspk_sync(c->stream));
@@ -1121,7 +1140,9 @@ int nnsp_cascade_get_state(nnsp_cascade *c, void *host, int first, int count)
         nnsp_cascade_stream_hdr *h = (nnsp_cascade_stream_hdr *)((char *)host + (size_t)i * sc.per);
         h->magic = NNSP_CASCADE_STATE_MAGIC;
         h->hist_frames = (uint16_t)c->H;
-        h->version = 1;
+        h->version = NNSP_CASCADE_STATE_VERSION;
+        h->state_bytes = (uint32_t)sc.per;
+        h->nets_sig = cascade_nets_sig(c);
     }
     return 0;
 }
@@ -1132,11 +1153,18 @@ int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int cou
     StateCopy sc;
     memset(&sc, 0, sizeof sc);
     cascade_state_segs(c, &sc);
+    const uint32_t sig = cascade_nets_sig(c);
     for (int i = 0; i < count; ++i) {
         const nnsp_cascade_stream_hdr *h = (const nnsp_cascade_stream_hdr *)((const char *)host + (size_t)i * sc.per);
-        if (h->magic != NNSP_CASCADE_STATE_MAGIC || h->hist_frames != c->H || h->version != 1) {
-            nnsp_set_error("nnsp_cascade_set_state: blob %d is not a state of a cascade with %d history frames", i,
-                           c->H);
+        if (h->magic != NNSP_CASCADE_STATE_MAGIC || h->version != NNSP_CASCADE_STATE_VERSION) {
+            nnsp_set_error("nnsp_cascade_set_state: blob %d is not a cascade stream state (version %d)", i,
+                           NNSP_CASCADE_STATE_VERSION);
+            return NNSP_EINVAL;
+        }
+        if (h->hist_frames != c->H || h->state_bytes != (uint32_t)sc.per || h->nets_sig != sig) {
+            nnsp_set_error("nnsp_cascade_set_state: blob %d is the state of another cascade (%u history frames, "
+                           "%u bytes, nets %08x; this one: %d, %zu, %08x)", i, (unsigned)h->hist_frames,
+                           (unsigned)h->state_bytes, (unsigned)h->nets_sig, c->H, sc.per, (unsigned)sig);
             return NNSP_EINVAL;
         }
     }

@@ -8,10 +8,7 @@
 #include "../kernels/nnsp_kabi.h"
 #include "../../../include/nnsp_batch.h"
 
-/* error codes (negative: argument/validation; positive: HIP runtime) */
-#define NNSP_EINVAL (-1)
-#define NNSP_EUNSUPPORTED (-2)
-#define NNSP_ENOMEM (-3)
+/* error codes: NNSP_EINVAL / NNSP_EUNSUPPORTED / NNSP_ENOMEM (include/nnsp_batch.h) */
 
 /* One layer as the engine sees it (what a NeuralNetClass row describes). */
 typedef struct {

@@ -955,8 +955,12 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     const size_t o_pcm = 0, o_tail = 320, o_mean = o_tail + 640, o_std = o_mean + 160, o_p5 = o_std + 160;
     const size_t o_post = al16(o_p5 + 400), o_h = o_post + al16(sizeof(NnPost)), o_c = o_h + al16(rows * hs * 2);
     const size_t o_feat = o_c + al16(rows * hs * 4), o_log = o_feat + 80, o_trig = o_log + 160;
-    const size_t total = al16(o_trig + 2), o_done = total;
-    if (o_done + 16 > G.hpin_cap) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
+    /* the completion word sits at a fixed offset past every net's staging:
+     * at o_done = total it moved with the net's h/c size, and after a call to a
+     * larger net a smaller net's word held that call's state bytes, which could
+     * equal the new sequence number by chance (a stale read, no wait) */
+    const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16;
+    if (total > o_done) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
     uint8_t *hp = G.copy ? G.hpin : G.hmap;
     memcpy(hp + o_pcm, rawPCM, 320);
     memcpy(hp + o_tail, fe->state_stftModule.dataBuffer + 160, 640);
@@ -1021,6 +1025,8 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         if (G.wait == 2) {
             r.done = (uint32_t *)(G.hmap_dev + o_done);
             r.done_seq = (int32_t)++G.seq;
+            /* a value the kernel's store cannot be mistaken for, before the launch */
+            __atomic_store_n((uint32_t *)(G.hmap + o_done), ~(uint32_t)r.done_seq, __ATOMIC_RELEASE);
         }
     }
     if (G.copy) {

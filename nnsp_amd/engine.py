@@ -95,6 +95,9 @@ class NNSPBatch:
         return buf
 
     def set_state(self, buf: np.ndarray) -> None:
+        per = _lib.lib().nnsp_batch_state_bytes(self.h)
+        if buf.ndim != 2 or buf.shape != (self.S, per):
+            raise ValueError(f"set_state: blobs of shape {buf.shape}, this batch takes ({self.S}, {per})")
         buf = np.ascontiguousarray(buf, np.uint8)
         _lib.check(_lib.lib().nnsp_batch_set_state(self.h, _lib.ptr(buf), 0, self.S), "set_state")
 
@@ -227,6 +230,10 @@ class NNSPCascade:
         return buf
 
     def set_state(self, buf: np.ndarray, first: int = 0) -> None:
+        per = _lib.lib().nnsp_cascade_state_bytes(self.h)
+        if buf.ndim != 2 or buf.shape[1] != per or first < 0 or first + buf.shape[0] > self.S:
+            raise ValueError(f"set_state: blobs of shape {buf.shape} at stream {first}; this cascade takes "
+                             f"[<= {self.S - first}][{per}]")
         buf = np.ascontiguousarray(buf, np.uint8)
         _lib.check(_lib.lib().nnsp_cascade_set_state(self.h, _lib.ptr(buf), first, buf.shape[0]),
                    "nnsp_cascade_set_state")

@@ -125,9 +125,21 @@ def test_cascade_state_reshard():
     half = _gpu(h)
     half.set_state(full.get_state(first=h, count=h))
     _same(half.exec(pcm[h:, 190:275]), [w[h:] for w in want[2]], "chunk 2 after 1 -> 2 shards")
-    # a blob of a cascade with other look-backs (another history length) is refused
+    # a blob of a cascade with other look-backs (another history length) is
+    # refused: by the wrapper (its shape) and by the library itself (header)
     other = _gpu(h, lb_s2i=90)
-    with pytest.raises(RuntimeError):
-        other.set_state(full.get_state(first=0, count=h))
+    foreign = full.get_state(first=0, count=h)
+    with pytest.raises(ValueError):
+        other.set_state(foreign)
+    assert _lib.lib().nnsp_cascade_set_state(other.h, _lib.ptr(foreign), 0, 1) == _lib.NNSP_EINVAL
+    # a blob whose nets differ (header signature) or whose size field differs is
+    # refused even at the right size (foreign net state imported silently)
+    mine = half.get_state()
+    for off, what in ((24, "nets_sig"), (20, "state_bytes"), (6, "version")):
+        bad = mine.copy()
+        bad[0, off] ^= 0x5A
+        assert _lib.lib().nnsp_cascade_set_state(half.h, _lib.ptr(bad), 0, h) == _lib.NNSP_EINVAL, what
+    half.set_state(mine)
+    np.testing.assert_array_equal(half.get_state(), mine)
     for x in shards + [one, full, half, other]:
         x.close()

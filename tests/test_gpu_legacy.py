@@ -207,3 +207,35 @@ def test_nnsp_exec_per_frame(name):
         assert trig == o_trig[0, t], f"frame {t}"
         ctx5 = np.ctypeslib.as_array(feat.normFeatContext)[200:240]
         np.testing.assert_array_equal(ctx5, o_feat[0, t], err_msg=f"features frame {t}")
+
+
+def test_nnsp_exec_interleaved_nets():
+    """NNSPClass_exec on VAD, KWS and S2I instances in turn, frame by frame
+    (ADVICE r5): the three nets' staging layouts differ in size, and the
+    drop-in completion word must not be satisfied by another net's bytes left
+    from the call before.  Every call is compared with that net's oracle."""
+    nets = []
+    for k, name in enumerate(("s2i", "vad", "kws")):
+        data = synth_net(name, 30 + k)
+        orc = OracleNet(data, thresh_prob=3000, th_count=1)
+        h = _lib.NetHandle(data)
+        feat = _lib.FeatureClass()
+        inst = _lib.NNSPClass()
+        thr = np.array([3000], np.int16)
+        cnt = np.array([1], np.int16)
+        _KEEP.extend([h, feat, inst, thr, cnt])
+        assert L().NNSPClass_init(C.byref(inst), C.c_void_p(h.addr), C.byref(feat), bytes([k]), vp(h.mean),
+                                  vp(h.stdR), vp(thr), vp(cnt)) == 0
+        L().NNSPClass_reset(C.byref(inst))
+        nets.append((name, orc, inst, feat))
+    T = 12
+    pcm = synthetic_pcm(3, T, seed=91)
+    ref = [orc.run(pcm[k:k + 1]) for k, (_, orc, _, _) in enumerate(nets)]
+    for t in range(T):
+        for k in (2, 0, 1) if t % 2 else (1, 2, 0):   # large and small staging layouts alternate
+            name, _, inst, feat = nets[k]
+            frame = np.ascontiguousarray(pcm[k, t])
+            trig = L().NNSPClass_exec(C.byref(inst), vp(frame))
+            assert trig == ref[k][0][0, t], f"{name} frame {t}"
+            ctx5 = np.ctypeslib.as_array(feat.normFeatContext)[200:240]
+            np.testing.assert_array_equal(ctx5, ref[k][2][0, t], err_msg=f"{name} features frame {t}")
