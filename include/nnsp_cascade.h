@@ -159,11 +159,12 @@ int nnsp_cascade_positions(nnsp_cascade *c, int8_t *pos);
  *   nnsp_cascade_stream_hdr                       32 B (below)
  *   PCM history  int16 [H][160]   the stream's last H frames, oldest first
  *                                 (PcmBufClass's voice buffer as far back as
- *                                 the look-backs reach: H = max(frs_vbufBk) + 1)
+ *                                 the look-backs reach, and the STFT buffer of
+ *                                 a net at the largest one: H = max(frs_vbufBk) + 2)
  *   STFT tail    int16 [320]      the last two frames (the shared front end's
  *                                 stftModule.dataBuffer before the next frame)
- *   look-back features int16 [3][H - 1][40]   per NNSP_ID, the normalised
- *                                 log-Mel of frames -(H-1) .. -1, which KWS and
+ *   look-back features int16 [3][H - 2][40]   per NNSP_ID, the normalised
+ *                                 log-Mel of frames -(H-2) .. -1, which KWS and
  *                                 S2I read frs_vbufBk frames back
  *   3 x nnsp_batch blob           per NNSP_ID, nnsp_batch_get_state's layout:
  *                                 that net's STFT tail, normFeatContext slots
@@ -192,6 +193,74 @@ typedef struct {
 size_t nnsp_cascade_state_bytes(const nnsp_cascade *c);
 int nnsp_cascade_get_state(nnsp_cascade *c, void *host, int first, int count);
 int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int count);
+
+/* Stream state in the reference's own per-stream objects: moving a live
+ * single-stream session of the reference (one nnCntrlClass, its PcmBufClass
+ * and three NNSPClass) onto the batched cascade and back.
+ *
+ * The EVB controller's structs are not part of ns-nnsp's API; these are
+ * ABI-identical mirrors (evb/src/nnCntrlClass.h:11-45, PcmBufClass.h:9-16):
+ * an application passes pointers to its own nnCntrlClass / PcmBufClass cast
+ * to them. */
+typedef struct {
+    int16_t thresh_prob_vad, thresh_cnts_vad;
+    int16_t frs_vbufBk_s2i, thresh_timeout_s2i, thresh_prob_s2i, thresh_cnts_s2i;
+    int16_t frs_vbufBk_kws, thresh_timeout_kws, thresh_prob_kws, thresh_cnts_kws;
+} nnsp_ref_params;                /* ParamCntrlClass */
+typedef struct {
+    void *pt_seq_cntrl;
+    int8_t len_seq_cntrl;
+    int8_t current_pos_seq;
+    void *pt_nnsp_arry;
+    nnsp_ref_params Params;
+    uint16_t cnt_timeout_kws;
+    uint16_t cnt_timeout_s2i;
+    uint16_t cnt_voice_frames_detected;
+    uint16_t cnt_voice_frames_not_detected;
+} nnsp_ref_cntrl;                 /* nnCntrlClass */
+typedef struct {
+    int16_t *pcm_buffer;          /* [num_frs][smpls_fr] */
+    int16_t idx_set;
+    int16_t idx_data_latest;
+    int16_t num_frs;
+    int16_t smpls_fr;
+} nnsp_ref_pcmbuf;                /* PcmBufClass */
+
+/* One stream: its controller, voice buffer and the three NNSPClass by
+ * NNSP_ID (nnsp[i]->pt_feat: its FeatureClass; nnsp[i]->pt_net: its
+ * NeuralNetClass, whose LSTM layers' pt_hstate / pt_cstate hold the state). */
+typedef struct {
+    nnsp_ref_cntrl *cntrl;
+    nnsp_ref_pcmbuf *pcmbuf;
+    NNSPClass *nnsp[3];
+} nnsp_ref_stream;
+
+/* set_state_ref: streams first .. first + count - 1 take the state the
+ * reference objects refs[i] hold between two nnCntrlClass_exec calls.  Read:
+ * current_pos_seq and the two timeout counters; the voice buffer's frames as
+ * far back as the look-backs reach (from idx_data_latest; smpls_fr 160,
+ * num_frs >= max(frs_vbufBk) + 1); per net its post-processing state
+ * (slides, trigger, counts_category, outputs, argmax_last), normFeatContext
+ * slots 1..5, the LSTM h / c, and for the net at the current position its STFT
+ * buffer, from which the frames its next window re-reads follow (the other
+ * two nets are reset when the controller leaves them: their STFT buffers must
+ * be zero).  The look-back features are recomputed on the device from the
+ * voice buffer (the shared front end over the history).  NNSP_EINVAL when the
+ * objects do not fit the cascade: another sequence length, a position past it,
+ * an NNSPClass of another NNSP_ID, an LSTM of another width, or an STFT
+ * buffer that is not the voice buffer's frames at that net's look-back.
+ *
+ * get_state_ref: the reverse, into the objects refs[i] point to (the pointers
+ * and parameters are not changed): the controller's position and counters,
+ * the voice buffer (idx_data_latest = num_frs - 1, idx_set = 0; frames older
+ * than the look-backs reach, which the reference never reads again, are
+ * zero), and per net the same fields; the current net's STFT buffer
+ * (dataBuffer[160..479]) holds the frames its next window re-reads.  Fields
+ * the reference overwrites before reading them (dataBuffer[0..159],
+ * normFeatContext slot 0, FeatureClass.feature) are zero or untouched.
+ * Running nnCntrlClass_exec on the result continues the stream bit-exactly. */
+int nnsp_cascade_set_state_ref(nnsp_cascade *c, int first, int count, const nnsp_ref_stream *refs);
+int nnsp_cascade_get_state_ref(nnsp_cascade *c, int first, int count, const nnsp_ref_stream *refs);
 
 #ifdef __cplusplus
 }

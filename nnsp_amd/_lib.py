@@ -77,6 +77,32 @@ class CascadeParams(C.Structure):
                 ("frs_vbufBk_kws", C.c_int16), ("thresh_timeout_kws", C.c_int16)]
 
 
+class RefParams(C.Structure):
+    """nnsp_ref_params: ABI mirror of ParamCntrlClass (evb/src/nnCntrlClass.h:11-31)."""
+    _fields_ = [(n, C.c_int16) for n in (
+        "thresh_prob_vad", "thresh_cnts_vad", "frs_vbufBk_s2i", "thresh_timeout_s2i", "thresh_prob_s2i",
+        "thresh_cnts_s2i", "frs_vbufBk_kws", "thresh_timeout_kws", "thresh_prob_kws", "thresh_cnts_kws")]
+
+
+class RefCntrl(C.Structure):
+    """nnsp_ref_cntrl: ABI mirror of nnCntrlClass (evb/src/nnCntrlClass.h:35-45)."""
+    _fields_ = [("pt_seq_cntrl", C.c_void_p), ("len_seq_cntrl", C.c_int8), ("current_pos_seq", C.c_int8),
+                ("pt_nnsp_arry", C.c_void_p), ("Params", RefParams), ("cnt_timeout_kws", C.c_uint16),
+                ("cnt_timeout_s2i", C.c_uint16), ("cnt_voice_frames_detected", C.c_uint16),
+                ("cnt_voice_frames_not_detected", C.c_uint16)]
+
+
+class RefPcmBuf(C.Structure):
+    """nnsp_ref_pcmbuf: ABI mirror of PcmBufClass (evb/src/PcmBufClass.h:9-16)."""
+    _fields_ = [("pcm_buffer", C.c_void_p), ("idx_set", C.c_int16), ("idx_data_latest", C.c_int16),
+                ("num_frs", C.c_int16), ("smpls_fr", C.c_int16)]
+
+
+class RefStreamC(C.Structure):
+    """nnsp_ref_stream (include/nnsp_cascade.h)."""
+    _fields_ = [("cntrl", C.c_void_p), ("pcmbuf", C.c_void_p), ("nnsp", C.c_void_p * 3)]
+
+
 class PostState(C.Structure):
     _fields_ = [("slides", C.c_int16), ("trigger", C.c_int16), ("argmax_last", C.c_int16),
                 ("pad0", C.c_int16), ("counts_category", C.c_int16 * 8),
@@ -126,6 +152,8 @@ def _declare(L: C.CDLL) -> None:
         "nnsp_cascade_totals_reset": (I, [P]),
         "nnsp_cascade_get_state": (I, [P, P, I, I]),
         "nnsp_cascade_set_state": (I, [P, P, I, I]),
+        "nnsp_cascade_set_state_ref": (I, [P, I, I, P]),
+        "nnsp_cascade_get_state_ref": (I, [P, I, I, P]),
         "nnsp_cascade_last_rounds": (I, [P, I, P, P, P]),
         "nnsp_cascade_last_fe_stats": (I, [P, C.POINTER(C.c_float)]),
         "nnsp_cascade_last_net_stats": (I, [P, I, C.POINTER(C.c_longlong), C.POINTER(C.c_float),

@@ -100,6 +100,8 @@ struct nnsp_cascade {
     void *ev_r1proj[3];             /* round-1 prefix FC layers done, per net (ahead_mode 1) */
     int ahead_mode;                 /* when the look-ahead front end starts (NNSP_AHEAD_MODE, see exec) */
     int r0_order;                   /* round 0's launch order (NNSP_R0_ORDER, see launch_round) */
+    int8_t seq[8];                  /* pt_seq_cntrl: NNSP_ID per sequence position */
+    int len_seq;
     void *ev_rnd[2][3];             /* fused control: per round parity and net, end of the net's round */
     void *ev_t[MAX_TIMED][3][3];    /* per round and net: before features, before NN, after NN */
     int last_rounds, launched;
@@ -201,12 +203,18 @@ int nnsp_cascade_create(nnsp_cascade **out, nnsp_batch *const nets[3], const int
         c->net[i] = nets[i];
         if (nets[i]->Tmax < c->Tmax) c->Tmax = nets[i]->Tmax;
     }
+    memcpy(c->seq, seq, (size_t)len_seq);
+    c->len_seq = len_seq;
     c->lookback[0] = p->frs_vbufBk_s2i;
     c->lookback[1] = 0; /* VAD reads the current frame (nnCntrlClass.c:243-247) */
     c->lookback[2] = p->frs_vbufBk_kws;
     /* PCM history: the look-back frame and, for the second frame after a
-     * net's reset, the one before it (FE_MODE_COLD re-reads it) */
-    c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 1;
+     * net's reset, the one before it (FE_MODE_COLD re-reads it); and one
+     * more, the oldest frame in the STFT buffer of a net that runs at the
+     * largest look-back (stftModule.dataBuffer[160..319]): the stream state
+     * then maps onto the reference's own structs and back exactly
+     * (nnsp_cascade_get_state_ref / set_state_ref) */
+    c->H = (c->lookback[0] > c->lookback[2] ? c->lookback[0] : c->lookback[2]) + 2;
     c->ring = c->H + 2 * c->Tmax;   /* look-back + this chunk + the look-ahead chunk */
     /* ring rows s * ring + slot are 32-bit in the kernels (fe_kernel's shared
      * store, the proj union loads); element offsets beyond are 64-bit */
@@ -1063,7 +1071,7 @@ _Static_assert(sizeof(CascState) == 8, "CascState: the header's 8 bytes at offse
 size_t nnsp_cascade_state_bytes(const nnsp_cascade *c)
 {
     if (!c) return 0;
-    size_t n = sizeof(nnsp_cascade_stream_hdr) + (size_t)c->H * 320 + 640 + 3 * (size_t)(c->H - 1) * 80;
+    size_t n = sizeof(nnsp_cascade_stream_hdr) + (size_t)c->H * 320 + 640 + 3 * (size_t)(c->H - 2) * 80;
     for (int i = 0; i < 3; ++i) n += nnsp_batch_state_bytes(c->net[i]);
     return n;
 }
@@ -1086,13 +1094,14 @@ static void cascade_state_segs(const nnsp_cascade *c, StateCopy *sc)
     off += H * 320;
     g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_stail, 640, 0, 1, 640, 0, 1, (uint32_t)off, 0};
     off += 640;
-    /* ring slots abs0 - (H - 1) .. abs0 - 1, oldest first */
+    /* ring slots abs0 - (H - 2) .. abs0 - 1 (the look-back frames: a net at
+     * look-back L reads frames -L .. -1 of them), oldest first */
     for (int n = 0; n < 3; ++n) {
-        if (H > 1)
+        if (H > 2)
             g[k++] = (StateSeg){(unsigned long long)(uintptr_t)c->d_nring[n], (unsigned long long)c->ring * 80, 80,
-                                (uint32_t)(H - 1), 80, (uint32_t)((c->abs0 - (int)(H - 1) + c->ring) % c->ring),
+                                (uint32_t)(H - 2), 80, (uint32_t)((c->abs0 - (int)(H - 2) + c->ring) % c->ring),
                                 (uint32_t)c->ring, (uint32_t)off, 0};
-        off += (H - 1) * 80;
+        off += (H - 2) * 80;
     }
     for (int n = 0; n < 3; ++n) k += nnsp_batch_state_segs(c->net[n], g + k, off, &off);
     sc->nseg = k;
@@ -1176,6 +1185,300 @@ int nnsp_cascade_set_state(nnsp_cascade *c, const void *host, int first, int cou
     TRY(nnsp_state_xfer(&sc, (void *)host, c->stream));
     c->pre_pcm = NULL; /* a look-ahead front end ran on the old state: the next call recomputes */
     return 0;
+}
+
+/* ---- the reference's per-stream objects (include/nnsp_cascade.h) ----
+ * A blob (nnsp_cascade_get_state's layout) is built from / taken apart into
+ * the objects the reference keeps per stream: nnCntrlClass
+ * (evb/src/nnCntrlClass.h:35-45), PcmBufClass (PcmBufClass.c:10-85), and per
+ * net NNSPClass (nn_speech.h:12-25), FeatureClass (feature_module.h:7-18) and
+ * the LSTM state of its NeuralNetClass.  Only the layout moves here; the
+ * look-back features, which the reference does not keep, are recomputed on
+ * the device by the shared front end. */
+typedef struct {
+    size_t hist, stail, look, net[3];
+} blob_offs;
+
+static blob_offs blob_layout(const nnsp_cascade *c)
+{
+    blob_offs o;
+    o.hist = sizeof(nnsp_cascade_stream_hdr);
+    o.stail = o.hist + (size_t)c->H * 320;
+    o.look = o.stail + 640;
+    o.net[0] = o.look + 3 * (size_t)(c->H - 2) * 80;
+    o.net[1] = o.net[0] + nnsp_batch_state_bytes(c->net[0]);
+    o.net[2] = o.net[1] + nnsp_batch_state_bytes(c->net[1]);
+    return o;
+}
+
+/* frame -j (j >= 1, 1 = the newest) of the voice buffer (PcmBufClass_getData
+ * with lookbk_frs = j - 1), NULL past the frames it holds */
+static const int16_t *vbuf_frame(const nnsp_ref_pcmbuf *pb, int j)
+{
+    if (j < 1 || j > pb->num_frs) return NULL;
+    int slot = (pb->idx_data_latest - (j - 1)) % pb->num_frs;
+    if (slot < 0) slot += pb->num_frs;
+    return pb->pcm_buffer + (size_t)slot * 160;
+}
+
+static int all_zero(const int16_t *x, int n)
+{
+    for (int i = 0; i < n; ++i)
+        if (x[i]) return 0;
+    return 1;
+}
+
+/* the LSTM layers of a reference NeuralNetClass, checked against net n of the
+ * cascade (one state row per LSTM layer, hs elements apart in the blob) */
+static int ref_lstm_layers(const nnsp_cascade *c, int n, const NeuralNetClass *net, int *layer)
+{
+    const nnsp_batch *b = c->net[n];
+    int k = 0;
+    for (int i = 0; i < net->numlayers && i < NN_MAX_LAYERS; ++i)
+        if (net->net_layer_type[i] == lstm) {
+            if (k >= b->im.img.n_lstm || net->size_layer[i + 1] != b->im.img.lstm_n[k] || !net->pt_hstate[i] ||
+                !net->pt_cstate[i])
+                return -1;
+            layer[k++] = i;
+        }
+    return k == b->im.img.n_lstm ? k : -1;
+}
+
+static void ref_post_pack(const NNSPClass *p, NnPost *q)
+{
+    memset(q, 0, sizeof *q);
+    q->slides = p->slides;
+    q->trigger = p->trigger;
+    q->argmax_last = p->argmax_last;
+    memcpy(q->counts, p->counts_category, sizeof q->counts);
+    memcpy(q->outputs, p->outputs, sizeof q->outputs);
+}
+
+static void ref_post_unpack(NNSPClass *p, const NnPost *q)
+{
+    p->slides = (int8_t)q->slides;
+    p->trigger = q->trigger;
+    p->argmax_last = q->argmax_last;
+    memcpy(p->counts_category, q->counts, sizeof q->counts);
+    memcpy(p->outputs, q->outputs, sizeof q->outputs);
+}
+
+static int ref_check(const nnsp_cascade *c, const nnsp_ref_stream *R, int i, int need_frames)
+{
+    if (!R->cntrl || !R->pcmbuf || !R->pcmbuf->pcm_buffer) {
+        nnsp_set_error("nnsp_cascade state_ref: stream %d: NULL controller or voice buffer", i);
+        return NNSP_EINVAL;
+    }
+    const nnsp_ref_pcmbuf *pb = R->pcmbuf;
+    if (pb->smpls_fr != 160 || pb->num_frs < need_frames || pb->idx_data_latest < 0 ||
+        pb->idx_data_latest >= pb->num_frs) {
+        nnsp_set_error("nnsp_cascade state_ref: stream %d: voice buffer of %d x %d samples (latest %d); 160-sample "
+                       "frames, at least %d of them, are needed", i, pb->num_frs, pb->smpls_fr, pb->idx_data_latest,
+                       need_frames);
+        return NNSP_EINVAL;
+    }
+    if (R->cntrl->len_seq_cntrl != c->len_seq || R->cntrl->current_pos_seq < 0 ||
+        R->cntrl->current_pos_seq >= c->len_seq) {
+        nnsp_set_error("nnsp_cascade state_ref: stream %d: position %d of a sequence of %d (the cascade's: %d)", i,
+                       R->cntrl->current_pos_seq, R->cntrl->len_seq_cntrl, c->len_seq);
+        return NNSP_EINVAL;
+    }
+    for (int n = 0; n < 3; ++n) {
+        const NNSPClass *q = R->nnsp[n];
+        int layer[NN_MAX_LSTM];
+        if (!q || (int)q->nn_id != n || !q->pt_feat || !q->pt_net ||
+            ref_lstm_layers(c, n, (const NeuralNetClass *)q->pt_net, layer) < 0) {
+            nnsp_set_error("nnsp_cascade state_ref: stream %d: nnsp[%d] is not an NNSPClass of NNSP_ID %d whose net's "
+                           "LSTM layers are the cascade's", i, n, n);
+            return NNSP_EINVAL;
+        }
+    }
+    return 0;
+}
+
+int nnsp_cascade_set_state_ref(nnsp_cascade *c, int first, int count, const nnsp_ref_stream *refs)
+{
+    if (!c || !refs || first < 0 || count < 0 || first + count > c->S) return NNSP_EINVAL;
+    if (count == 0) return 0;
+    const size_t per = nnsp_cascade_state_bytes(c);
+    const blob_offs o = blob_layout(c);
+    const int H = c->H;
+    const uint32_t sig = cascade_nets_sig(c);
+    uint8_t *blob = (uint8_t *)calloc((size_t)count, per);
+    if (!blob) return NNSP_ENOMEM;
+    int e = 0;
+    for (int i = 0; i < count && !e; ++i) {
+        const nnsp_ref_stream *R = &refs[i];
+        /* frames -(H-1) .. -1: the look-back frame of every net and the one
+         * before it; frame -H only as the STFT buffer's oldest frame */
+        if ((e = ref_check(c, R, i, H - 1))) break;
+        uint8_t *b = blob + (size_t)i * per;
+        nnsp_cascade_stream_hdr *h = (nnsp_cascade_stream_hdr *)b;
+        h->magic = NNSP_CASCADE_STATE_MAGIC;
+        h->hist_frames = (uint16_t)H;
+        h->version = NNSP_CASCADE_STATE_VERSION;
+        h->state_bytes = (uint32_t)per;
+        h->nets_sig = sig;
+        h->current_pos_seq = R->cntrl->current_pos_seq;
+        h->cnt_timeout_kws = R->cntrl->cnt_timeout_kws;
+        h->cnt_timeout_s2i = R->cntrl->cnt_timeout_s2i;
+        const nnsp_ref_pcmbuf *pb = R->pcmbuf;
+        int16_t *hist = (int16_t *)(b + o.hist);   /* [H][160], frame -H first */
+        for (int j = 1; j <= H; ++j) {
+            const int16_t *f = vbuf_frame(pb, j);
+            if (f) memcpy(hist + (size_t)(H - j) * 160, f, 320);
+        }
+        memcpy(b + o.stail, hist + (size_t)(H - 2) * 160, 640);
+        /* the net at the current position: frames since its reset, from its
+         * STFT buffer (dataBuffer[160..479] = the two frames before its next
+         * one; zero before a reset, stftModule_setDefault); the other two are
+         * reset when the controller leaves them */
+        const int cur = c->seq[R->cntrl->current_pos_seq], L = c->lookback[cur];
+        int fresh = -1;
+        for (int n = 0; n < 3 && !e; ++n) {
+            const FeatureClass *fe = (const FeatureClass *)R->nnsp[n]->pt_feat;
+            const int16_t *A = fe->state_stftModule.dataBuffer + 160, *B = A + 160;
+            if (n != cur) {
+                if (!all_zero(A, 320)) {
+                    nnsp_set_error("nnsp_cascade_set_state_ref: stream %d: net %d is not at the current position "
+                                   "and its STFT buffer is not reset", i, n);
+                    e = NNSP_EINVAL;
+                }
+                continue;
+            }
+            const int16_t *F1 = vbuf_frame(pb, L + 1), *F2 = vbuf_frame(pb, L + 2);
+            /* (where two readings fit -- zero frames in the voice buffer --
+             * both give the same outputs) */
+            if (!memcmp(B, F1, 320) && F2 && !memcmp(A, F2, 320)) {
+                fresh = 2;
+            } else if (all_zero(A, 160) && !memcmp(B, F1, 320)) {
+                fresh = 1;
+            } else if (!F2 && !memcmp(B, F1, 320)) {
+                fresh = 2;
+                memcpy(hist, A, 320);   /* frame -(L + 2) = -H: past the voice buffer */
+            } else if (all_zero(A, 320)) {
+                fresh = 0;
+            } else {
+                nnsp_set_error("nnsp_cascade_set_state_ref: stream %d: the STFT buffer of net %d does not hold the "
+                               "voice buffer's frames at look-back %d", i, n, L);
+                e = NNSP_EINVAL;
+            }
+        }
+        if (e) break;
+        h->frames_since_reset = (int8_t)fresh;
+        for (int n = 0; n < 3; ++n) {
+            const nnsp_batch *nb = c->net[n];
+            const NNSPClass *q = R->nnsp[n];
+            const FeatureClass *fe = (const FeatureClass *)q->pt_feat;
+            const NeuralNetClass *net = (const NeuralNetClass *)q->pt_net;
+            uint8_t *nbp = b + o.net[n];   /* [STFT tail 640, unused by the cascade: 0][prev5 400][h][c][post] */
+            memcpy(nbp + 640, fe->normFeatContext + 40, 400);
+            int layer[NN_MAX_LSTM];
+            const int nl = ref_lstm_layers(c, n, net, layer);
+            const size_t hb = (size_t)(nl ? nl : 1) * nb->hs * 2;
+            for (int l = 0; l < nl; ++l) {
+                const int N = net->size_layer[layer[l] + 1];
+                memcpy(nbp + 1040 + (size_t)l * nb->hs * 2, net->pt_hstate[layer[l]], (size_t)N * 2);
+                memcpy(nbp + 1040 + hb + (size_t)l * nb->hs * 4, net->pt_cstate[layer[l]], (size_t)N * 4);
+            }
+            NnPost ps;
+            ref_post_pack(q, &ps);
+            memcpy(nbp + 1040 + hb + hb * 2, &ps, sizeof ps);
+        }
+    }
+    if (!e) e = nnsp_cascade_set_state(c, blob, first, count);
+    free(blob);
+    if (e) return e;
+    /* the look-back features: the shared front end over the imported history
+     * (frames -H .. -1 of these streams as a chunk of H frames, written to ring
+     * slots abs0 - H .. abs0 - 1).  Frames -H and -(H-1) see a zero STFT tail;
+     * no net reads them (a net at look-back L reads frames -L .. -1 of the
+     * ring, and L <= H - 2) */
+    void *ztail = NULL;
+    TRY(nnspk_malloc(&ztail, (size_t)count * 640));
+    FeArgs fa;
+    memset(&fa, 0, sizeof fa);
+    fa.tb_img = c->d_fetab;
+    fa.sched = c->fe_sched;
+    fa.pcm = c->d_hist[c->chunk % 3] + (size_t)first * H * 160;
+    fa.tail = (const int16_t *)ztail;
+    fa.S = count;
+    fa.T = H;
+    fa.mean = c->net[0]->d_mean;
+    fa.stdR = c->net[0]->d_stdR;
+    fa.mode = FE_MODE_SHARED;
+    fa.port = c->net[0]->port;
+    fa.norm32 = c->net[0]->norm32 && c->net[1]->norm32 && c->net[2]->norm32;
+    fa.ring = c->ring;
+    fa.abs0 = (c->abs0 - H + c->ring) % c->ring;
+    for (int n = 0; n < 3; ++n) {
+        fa.nring[n] = c->d_nring[n] + (size_t)first * c->ring * 40;
+        fa.nmean[n] = c->net[n]->d_mean;
+        fa.nstdR[n] = c->net[n]->d_stdR;
+        fa.nshift[n] = c->net[n]->norm_shift;
+    }
+    e = nnspk_memset(ztail, 0, (size_t)count * 640, c->stream);
+    if (!e) e = nnspk_launch_fe(&fa, c->stream);
+    if (!e) e = nnspk_sync(c->stream);
+    nnspk_free(ztail);
+    return e;
+}
+
+int nnsp_cascade_get_state_ref(nnsp_cascade *c, int first, int count, const nnsp_ref_stream *refs)
+{
+    if (!c || !refs || first < 0 || count < 0 || first + count > c->S) return NNSP_EINVAL;
+    if (count == 0) return 0;
+    const int H = c->H;
+    for (int i = 0; i < count; ++i) TRY(ref_check(c, &refs[i], i, H - 1));
+    const size_t per = nnsp_cascade_state_bytes(c);
+    const blob_offs o = blob_layout(c);
+    uint8_t *blob = (uint8_t *)malloc((size_t)count * per);
+    if (!blob) return NNSP_ENOMEM;
+    int e = nnsp_cascade_get_state(c, blob, first, count);
+    for (int i = 0; i < count && !e; ++i) {
+        const nnsp_ref_stream *R = &refs[i];
+        const uint8_t *b = blob + (size_t)i * per;
+        const nnsp_cascade_stream_hdr *h = (const nnsp_cascade_stream_hdr *)b;
+        R->cntrl->current_pos_seq = (int8_t)h->current_pos_seq;
+        R->cntrl->cnt_timeout_kws = h->cnt_timeout_kws;
+        R->cntrl->cnt_timeout_s2i = h->cnt_timeout_s2i;
+        nnsp_ref_pcmbuf *pb = R->pcmbuf;
+        const int16_t *hist = (const int16_t *)(b + o.hist);   /* frame -H first */
+        memset(pb->pcm_buffer, 0, (size_t)pb->num_frs * 320);
+        pb->idx_data_latest = (int16_t)(pb->num_frs - 1);
+        pb->idx_set = 0;
+        for (int j = 1; j <= H && j <= pb->num_frs; ++j)
+            memcpy(pb->pcm_buffer + (size_t)(pb->num_frs - j) * 160, hist + (size_t)(H - j) * 160, 320);
+        const int cur = c->seq[h->current_pos_seq], L = c->lookback[cur], fresh = h->frames_since_reset;
+        for (int n = 0; n < 3; ++n) {
+            const nnsp_batch *nb = c->net[n];
+            NNSPClass *q = R->nnsp[n];
+            FeatureClass *fe = (FeatureClass *)q->pt_feat;
+            NeuralNetClass *net = (NeuralNetClass *)q->pt_net;
+            const uint8_t *nbp = b + o.net[n];
+            int16_t *db = fe->state_stftModule.dataBuffer;
+            memset(db, 0, 480 * 2);
+            if (n == cur && fresh >= 1) {   /* [160..319] frame -(L+2), [320..479] frame -(L+1) */
+                memcpy(db + 320, hist + (size_t)(H - (L + 1)) * 160, 320);
+                if (fresh >= 2) memcpy(db + 160, hist + (size_t)(H - (L + 2)) * 160, 320);
+            }
+            memset(fe->normFeatContext, 0, 80);
+            memcpy(fe->normFeatContext + 40, nbp + 640, 400);
+            int layer[NN_MAX_LSTM];
+            const int nl = ref_lstm_layers(c, n, net, layer);
+            const size_t hb = (size_t)(nl ? nl : 1) * nb->hs * 2;
+            for (int l = 0; l < nl; ++l) {
+                const int N = net->size_layer[layer[l] + 1];
+                memcpy(net->pt_hstate[layer[l]], nbp + 1040 + (size_t)l * nb->hs * 2, (size_t)N * 2);
+                memcpy(net->pt_cstate[layer[l]], nbp + 1040 + hb + (size_t)l * nb->hs * 4, (size_t)N * 4);
+            }
+            NnPost ps;
+            memcpy(&ps, nbp + 1040 + hb + hb * 2, sizeof ps);
+            ref_post_unpack(q, &ps);
+        }
+    }
+    free(blob);
+    return e;
 }
 
 int nnsp_cascade_totals(nnsp_cascade *c, long long *chunks, long long *rounds, long long *frames_run, double *fe_ms,

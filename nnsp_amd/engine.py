@@ -238,6 +238,20 @@ class NNSPCascade:
         _lib.check(_lib.lib().nnsp_cascade_set_state(self.h, _lib.ptr(buf), first, buf.shape[0]),
                    "nnsp_cascade_set_state")
 
+    def set_state_ref(self, refs: list, first: int = 0) -> None:
+        """Streams first.. take the state held by the reference objects of
+        each RefStream (nnsp_cascade_set_state_ref)."""
+        arr = (_lib.RefStreamC * len(refs))(*[r.c_struct() for r in refs])
+        _lib.check(_lib.lib().nnsp_cascade_set_state_ref(self.h, first, len(refs), C.addressof(arr)),
+                   "nnsp_cascade_set_state_ref")
+
+    def get_state_ref(self, refs: list, first: int = 0) -> None:
+        """The state of streams first.. into each RefStream's reference objects
+        (nnsp_cascade_get_state_ref)."""
+        arr = (_lib.RefStreamC * len(refs))(*[r.c_struct() for r in refs])
+        _lib.check(_lib.lib().nnsp_cascade_get_state_ref(self.h, first, len(refs), C.addressof(arr)),
+                   "nnsp_cascade_get_state_ref")
+
     def positions(self) -> np.ndarray:
         pos = np.zeros(self.S, np.int8)
         _lib.check(_lib.lib().nnsp_cascade_positions(self.h, _lib.ptr(pos)), "positions")
@@ -249,3 +263,46 @@ def device_info() -> dict:
     arch = C.create_string_buffer(64)
     _lib.check(_lib.lib().nnsp_device_info(C.byref(cu), C.byref(clk), arch, 64), "device_info")
     return {"compute_units": cu.value, "clock_khz": clk.value, "arch": arch.value.decode()}
+
+
+class RefStream:
+    """One stream's state in the reference's own per-stream objects, as a
+    single-stream reference application holds them: an nnCntrlClass, its
+    PcmBufClass (num_frs x 160 voice buffer) and, by NNSP_ID, an NNSPClass
+    with its FeatureClass and NeuralNetClass (the LSTM state in this stream's
+    own h / c arrays).  ``handles``: _lib.NetHandle per NNSP_ID (s2i, vad,
+    kws), whose layer tables the NeuralNetClass copies share."""
+
+    def __init__(self, handles: list, seq=(1, 2, 0), num_frs: int = 100):
+        self.seq = np.ascontiguousarray(seq, np.int8)
+        self.cntrl = _lib.RefCntrl()
+        self.cntrl.pt_seq_cntrl = self.seq.ctypes.data
+        self.cntrl.len_seq_cntrl = len(seq)
+        self.pcm = np.zeros((num_frs, 160), np.int16)
+        self.pcmbuf = _lib.RefPcmBuf(self.pcm.ctypes.data, 0, num_frs - 1, num_frs, 160)
+        self.feat = [_lib.FeatureClass() for _ in range(3)]
+        self.net, self.h, self.c, self.nnsp = [], [], [], []
+        for n, hd in enumerate(handles):
+            net = _lib.NeuralNetClass.from_buffer_copy(hd.net)
+            hs, cs = {}, {}
+            for i in range(net.numlayers):
+                if net.net_layer_type[i] == 1:   # lstm
+                    N = net.size_layer[i + 1]
+                    hs[i], cs[i] = np.zeros(N, np.int16), np.zeros(N, np.int32)
+                    net.pt_hstate[i], net.pt_cstate[i] = hs[i].ctypes.data, cs[i].ctypes.data
+            q = _lib.NNSPClass()
+            q.nn_id = bytes([n])
+            q.pt_net = C.addressof(net)
+            q.pt_feat = C.addressof(self.feat[n])
+            self.net.append(net)
+            self.h.append(hs)
+            self.c.append(cs)
+            self.nnsp.append(q)
+
+    def c_struct(self) -> "_lib.RefStreamC":
+        r = _lib.RefStreamC()
+        r.cntrl = C.addressof(self.cntrl)
+        r.pcmbuf = C.addressof(self.pcmbuf)
+        for n in range(3):
+            r.nnsp[n] = C.addressof(self.nnsp[n])
+        return r

@@ -12,7 +12,7 @@ from nnsp_amd import _lib
 
 def _declared_functions():
     names = set()
-    for h in ("nnsp_api.h", "nnsp_batch.h"):
+    for h in ("nnsp_api.h", "nnsp_batch.h", "nnsp_cascade.h"):
         text = open(os.path.join(ROOT, "include", h)).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
         text = re.sub(r"typedef[^;]*;", "", text, flags=re.S)
@@ -95,6 +95,70 @@ def test_struct_abi_matches_headers():
 @pytest.mark.skipif(not os.path.isdir("/root/reference/ns-nnsp"), reason="reference absent")
 def test_struct_abi_matches_reference_headers():
     assert _layout(os.path.join(ROOT, "include")) == _layout("/root/reference/ns-nnsp/includes-api")
+
+
+CNTRL_PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include <stdint.h>
+#ifdef MINE
+#include "nnsp_cascade.h"
+#define CNTRL nnsp_ref_cntrl
+#define PCMBUF nnsp_ref_pcmbuf
+#define PARAMS nnsp_ref_params
+#else
+#include "nnCntrlClass.h"
+#include "PcmBufClass.h"
+#define CNTRL nnCntrlClass
+#define PCMBUF PcmBufClass
+#define PARAMS ParamCntrlClass
+#endif
+#define O(T, f) printf("%s.%s %zu\n", #T, #f, offsetof(T, f))
+int main(void) {
+    printf("cntrl %zu\npcmbuf %zu\nparams %zu\n", sizeof(CNTRL), sizeof(PCMBUF), sizeof(PARAMS));
+    O(CNTRL, pt_seq_cntrl); O(CNTRL, len_seq_cntrl); O(CNTRL, current_pos_seq); O(CNTRL, pt_nnsp_arry);
+    O(CNTRL, Params); O(CNTRL, cnt_timeout_kws); O(CNTRL, cnt_timeout_s2i); O(CNTRL, cnt_voice_frames_detected);
+    O(CNTRL, cnt_voice_frames_not_detected);
+    O(PARAMS, thresh_prob_vad); O(PARAMS, frs_vbufBk_s2i); O(PARAMS, thresh_timeout_s2i); O(PARAMS, frs_vbufBk_kws);
+    O(PARAMS, thresh_timeout_kws); O(PARAMS, thresh_cnts_kws);
+    O(PCMBUF, pcm_buffer); O(PCMBUF, idx_set); O(PCMBUF, idx_data_latest); O(PCMBUF, num_frs); O(PCMBUF, smpls_fr);
+    return 0;
+}
+"""
+
+
+def _cntrl_layout(mine: bool):
+    import subprocess
+    import tempfile
+    inc = os.path.join(ROOT, "include") if mine else "/root/reference/evb/src"
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "p.c")
+        open(src, "w").write(CNTRL_PROBE)
+        exe = os.path.join(d, "p")
+        subprocess.check_call(["gcc"] + (["-DMINE"] if mine else []) + ["-I", inc, src, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split("\n")
+    return dict(l.rsplit(" ", 1) for l in out if l)
+
+
+def test_ref_stream_mirrors_match_ctypes():
+    """nnsp_ref_cntrl / nnsp_ref_pcmbuf / nnsp_ref_params (include/nnsp_cascade.h)
+    against the ctypes mirrors the Python bindings pass."""
+    mine = _cntrl_layout(True)
+    assert mine["cntrl"] == str(C.sizeof(_lib.RefCntrl)) and mine["pcmbuf"] == str(C.sizeof(_lib.RefPcmBuf))
+    assert mine["params"] == str(C.sizeof(_lib.RefParams))
+    for k, v in mine.items():
+        if "." in k:
+            T, f = k.split(".")
+            cls = {"CNTRL": _lib.RefCntrl, "PCMBUF": _lib.RefPcmBuf, "PARAMS": _lib.RefParams}[T]
+            assert str(getattr(cls, f).offset) == v, (k, v)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/evb/src"), reason="reference absent")
+def test_ref_stream_mirrors_match_reference_headers():
+    """The mirrors are ABI-identical to the reference's own nnCntrlClass,
+    ParamCntrlClass and PcmBufClass (evb/src/nnCntrlClass.h:11-45,
+    PcmBufClass.h:9-16), so an application passes pointers to its objects."""
+    assert _cntrl_layout(True) == _cntrl_layout(False)
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/evb/src"), reason="reference absent")
