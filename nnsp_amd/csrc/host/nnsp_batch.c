@@ -235,6 +235,19 @@ int nnsp_batch_create_ex(nnsp_batch **out, const NeuralNetClass *net, int nn_id,
     if ((e = nnspk_malloc((void **)&b->d_mask, S))) goto fail;
     plan_fast(b);
     b->ep32 = !b->im.img.acc32 && !b->im.img.mixed_acc && !getenv("NNSP_NO_EP32") && fits_int32(b, L, nl);
+    {   /* the fused prefix (VAD): recur also runs the layer before the LSTM,
+         * one pipeline stage ahead, for segments of whole chunks on the
+         * cascade's ring (nnsp_batch_run_nn) */
+        const char *fe = getenv("NNSP_FUSE_PREFIX");
+        b->fuse = b->fast && (fe ? atoi(fe) != 0 : 0) &&
+                  nnspk_fast_fuse_ok(b->shape, (int)b->im.a_bytes, b->im.rows_total, b->im.img.acc32 || b->ep32);
+        /* 2 (tests): a VAD net that cannot fuse is an error rather than a silent fallback */
+        if (fe && atoi(fe) == 2 && b->fast && b->shape == NN_SHAPE_VAD && !b->fuse) {
+            nnsp_set_error("nnsp_batch_create: NNSP_FUSE_PREFIX=2 and the net cannot run the fused prefix");
+            e = NNSP_EUNSUPPORTED;
+            goto fail;
+        }
+    }
     if (b->fast) {
         if ((e = nnspk_set_lds_limit())) goto fail;
         if (b->shape != NN_SHAPE_GENERIC) { /* x rows: int16, 16 * ceil(N / 16) per (stream, step) */
@@ -431,15 +444,18 @@ int nnsp_batch_run_nn(nnsp_batch *b, int T, int16_t *trig, int32_t *logits, cons
             const long long need = (pt + b->proj_waves - 1) / b->proj_waves;
             if (need < blocks) blocks = (int)need;
         }
-        TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
+        f.tseq = recur_tseq(seg, T, b->shape);
+        /* the fused prefix: one tile per workgroup, features from the ring */
+        const int fuse = b->fuse && f.tseq == 1 && seg->fs.nring != NULL;
+        if (!fuse) TRY(nnspk_launch_proj(&b->im.img, &f, blocks, b->proj_waves, stream));
         if (seg->proj_done) TRY(nnspk_event_record(seg->proj_done, stream));
         for (int k = 0; k < 2; ++k)
             if (seg->recur_wait[k]) TRY(nnspk_stream_wait(stream, seg->recur_wait[k]));
-        f.a_off = b->rec_a_off;
-        f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)b->rec_a_off);
-        f.ep_lo = b->ep_rec_lo;
-        f.ep_n = b->ep_rec_n;
-        f.tseq = recur_tseq(seg, T, b->shape);
+        f.fuse = fuse;
+        f.a_off = fuse ? 0 : b->rec_a_off;
+        f.a_lds_bytes = (int)(b->im.a_bytes - (size_t)f.a_off);
+        f.ep_lo = fuse ? 0 : b->ep_rec_lo;
+        f.ep_n = fuse ? b->im.rows_total : b->ep_rec_n;
         TRY(nnspk_launch_recur(&b->im.img, &f, b->rec_waves, seg->ctl, stream));
     } else {
         NnRun r;

@@ -62,6 +62,8 @@ struct nnsp_batch {
     int last_T;
     /* split NN path (one LSTM layer) */
     int fast, li, nstep_max, rec_waves, proj_blocks, proj_waves;
+    int fuse;                         /* the cascade's whole-segment VAD rounds run the prefix layer inside recur
+                                         (FastRun.fuse; NNSP_FUSE_PREFIX) */
     int ep_proj, ep_rec_lo, ep_rec_n; /* epilogue rows staged into LDS by proj / recur */
     int shape;                        /* NN_SHAPE_* compiled split-path shape */
     int ep32;                         /* acc64 net that provably fits int32 accumulators */

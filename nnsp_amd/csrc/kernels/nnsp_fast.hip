@@ -350,6 +350,14 @@ __device__ __forceinline__ void lds_dma(const void* g, void* lds) {
                      : "=&s"(saved) : "v"(g), "s"(l) : "memory");
 }
 
+// 16 bytes through a global (not flat) load: flat loads also count in lgkmcnt
+// and complete out of order, so the compiler waits for them (and everything
+// else) at once
+__device__ __forceinline__ int4 gload16(uintptr_t a) {
+    const v4i v = *reinterpret_cast<const __attribute__((address_space(1))) v4i*>(a);
+    return make_int4(v.x, v.y, v.z, v.w);
+}
+
 // 16 zero bytes: the source of union elements outside a segment (proj_kernel)
 __device__ __attribute__((aligned(16))) int4 nnsp_proj_zero16;
 // where proj's x-row stores of rows without an NN step go (>= XS + 8 bytes)
@@ -1113,7 +1121,7 @@ __global__ __launch_bounds__(64 * RW * 2) void recur_kernel(NnImage img, FastRun
 // what stage k-1 wrote one iteration earlier, and that buffer is rewritten
 // only after the next barrier).
 // ---------------------------------------------------------------------------
-template <class SH>
+template <class SH, bool FP = false>
 struct PipeCfg {
     // LSTM waves: <= 2 row tiles each (4 tiles each on 4 waves would let KWS's
     // workgroups fit two per CU, but spills ~250 B per lane at 128 VGPRs)
@@ -1134,7 +1142,9 @@ struct PipeCfg {
     // frame outputs are stored by the two FC waves (frame t / t + 1) instead of
     // the FC-linear wave
     static constexpr bool STORE_FC12 = SH::NOUT > 2;
-    static constexpr int NWV = LW + 3 + SPLIT;               // waves per tile
+    // FP: two more waves, the fused prefix FC stage (the layer before the
+    // LSTM, two steps ahead of it, one row tile per wave; no proj launch)
+    static constexpr int NWV = LW + 3 + SPLIT + (FP ? 2 : 0); // waves per tile
     // tiles per workgroup (the kernel supports several, sharing the staged
     // weights): one.  Two VAD tiles per workgroup (16 waves, so that every
     // net's recur workgroup fills one CU in a cascade round) measured slower:
@@ -1154,7 +1164,18 @@ struct PipeCfg {
 // tiles one workgroup can run back to back through its pipeline (FastRun.tseq)
 #define PIPE_KT 4
 
+// the fused prefix stage's LDS (FP): the LSTM input x of a step, per stream
+// row the high bytes then the low bytes ^ 0x80 (the B operand's split form),
+// rows 16 B longer than the two planes so that the 16 rows of a ds_read_b128
+// lane group fall on distinct banks
 template <class SH>
+struct PipeX {
+    static constexpr int XSR = 2 * SH::XS + 16;
+};
+
+// KT: tiles the workgroup can hold (PIPE_KT for the multi-tile instantiation,
+// else 1); FP: the fused prefix stage's buffers
+template <class SH, int KT = PIPE_KT, bool FP = false>
 struct alignas(16) PipeTile {
     static constexpr int RS = 64 * SH::NKR + 8;
     static constexpr int CW = cstride(SH::NW);
@@ -1162,16 +1183,24 @@ struct alignas(16) PipeTile {
     int16_t a2[2][16][RS];
     int16_t a3[2][16][RS];
     int16_t a4[2][16][RS];    // stage 3 -> 4: int32 logits
-    int16_t hs[16][RS];       // h at the start of a tile (its LSTM step 0 reads it)
+    int16_t hs[KT > 1 ? 16 : 1][RS];   // h at the start of a tile (its LSTM step 0 reads it; several tiles only)
     int32_t c[16][CW];
     // the workgroup's tiles, in pipeline order
-    int4 ti[PIPE_KT][16];     // per stream: {stream, segment begin, end (exclusive), phase | valid << 1}
-    int4 ps[PIPE_KT][16][2];  // PostState (32 bytes) as two 16-byte words
-    CascState cst[PIPE_KT][16];
-    int32_t fresh[PIPE_KT][16];
-    int32_t cut[PIPE_KT][16]; // fused control: frame that reset the net (-1: none)
-    int32_t pbt[PIPE_KT][16]; // frame b of a stream starting at NN phase 1 (no NN, trigger carried), -1: none
-    int2 pb[PIPE_KT][16];     // its outputs: trigger | outputs[0] << 16, outputs[1] | outputs[2] << 16
+    int4 ti[KT][16];          // per stream: {stream, segment begin, end (exclusive), phase | valid << 1}
+    int4 ps[KT][16][2];       // PostState (32 bytes) as two 16-byte words
+    CascState cst[KT][16];
+    int32_t fresh[KT][16];
+    int32_t cut[KT][16];      // fused control: frame that reset the net (-1: none)
+    int32_t pbt[KT][16];      // frame b of a stream starting at NN phase 1 (no NN, trigger carried), -1: none
+    int2 pb[KT][16];          // its outputs: trigger | outputs[0] << 16, outputs[1] | outputs[2] << 16
+    // FP: per stream a ring of its last 8 context frames (V index v at slot
+    // v & 7), rows 656 B apart: the 16 rows of a B-fragment read fall on
+    // distinct banks; and per stream its ring row and the ring slot of V
+    // index phase + 4 (pf_load)
+    int16_t pfr[FP ? 16 : 1][FP ? 328 : 8];
+    int4 pdesc[FP ? 16 : 1];
+    // FP: the LSTM input x of three steps (step s in xs[s % 3])
+    uint8_t xs[FP ? 3 : 1][FP ? 16 : 1][FP ? PipeX<SH>::XSR : 16];
     int32_t off[8];           // first pipeline step of tiles 1..3 (0x7fffffff past the last), [4]: steps in all
     // the post wave's frame outputs of one step, stored to HBM by another wave
     // one iteration later (double-buffered by iteration parity): frame t,
@@ -1182,6 +1211,7 @@ struct alignas(16) PipeTile {
     int16_t po[2][16][4];
 };
 static_assert(PIPE_KT == 4, "the post wave describes one tile per 16 lanes");
+static_assert(sizeof(PipeTile<ShapeVad, 1, true>::xs[0]) == 16 * 80, "FP x rows: 80 B");
 static_assert(cstride(28) == 30 && cstride(64) == 66 && cstride(72) == 74 && cstride(128) == 130, "cstride");
 
 //
@@ -1216,12 +1246,15 @@ static_assert(cstride(28) == 30 && cstride(64) == 66 && cstride(72) == 74 && cst
 // instantiation compiles the hand-overs and tile switches away: with them the
 // post and LSTM waves' loops carried the switch code (if-converted into
 // selects every step), and the FC waves on their SIMDs lost issue slots to it.
-template <class SH, bool ACC32, bool MT>
-__global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recur_pipe_kernel(NnImage img, FastRun r,
-                                                                                            CascArgs ca) {
+template <class SH, bool ACC32, bool MT, bool FP = false>
+__global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW)) void recur_pipe_kernel(NnImage img,
+                                                                                                    FastRun r,
+                                                                                                    CascArgs ca) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    using CF = PipeCfg<SH>;
-    using PT = PipeTile<SH>;
+    using CF = PipeCfg<SH, FP>;
+    using PT = PipeTile<SH, MT ? PIPE_KT : 1, FP>;
+    constexpr int KT = MT ? PIPE_KT : 1;
+    static_assert(!(FP && MT), "recur_pipe_kernel: the fused prefix stage runs one tile per workgroup");
     constexpr int RGP = CF::LW, RPW = CF::RPW, RS = PT::RS;
     constexpr int N = SH::NW, nrt = SH::NRT, nkt_r = SH::NKR;
     static_assert(CF::TPW == 1, "recur_pipe_kernel: one pipeline per workgroup");
@@ -1233,6 +1266,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // does; nothing reads or appends to it during this round)
     if (ctl && blockIdx.x == 0 && threadIdx.x < 6) ca.counts_clear[threadIdx.x] = 0;
     const int nrow = r.n_list_dev ? *r.n_list_dev : (r.list ? r.n_list : r.S);
+    // (FP: no proj launch records the list length the round ran with)
+    if (FP && r.n_list_rec && blockIdx.x == 0 && threadIdx.x == 0) *r.n_list_rec = nrow;
     const int tseq = MT ? r.tseq : 1;   // 1..PIPE_KT (host)
     const int row0 = (int)blockIdx.x * tseq * 16;   // the workgroup's first list entry
     if (row0 >= nrow) return;
@@ -1290,19 +1325,21 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         }
         const int ph = ok ? 1 - (int)(int16_t)(p0.x & 0xffff) : 0;   // 1 - slides
         int m = ok && e - b - ph > 0 ? (e - b - ph + 1) / 2 : 0;
-        R.ti[k][sc] = make_int4(s, b, e, ph | (ok ? 2 : 0));
-        R.ps[k][sc][0] = p0;
-        R.ps[k][sc][1] = p1;
         if (lane < 16) R.pw[0][lane] = R.pw[1][lane] = 0;   // no frame outputs before the first post step
-        R.pbt[k][sc] = -1;
-        // fresh[] (frames since the net's reset: the cold front end's frames)
-        // as at the kernel start -- the feature-context roll reads through it
-        // after the bookkeeping has overwritten it for the next net
-        R.fresh[k][sc] = ok && r.fs.nring ? (int)r.fs.fresh[s] : 2;
-        if (ctl) {
-            CascState cs = {};
-            if (ok) cs = ca.st[s];
-            R.cst[k][sc] = cs;
+        if (k < KT) {
+            R.ti[k][sc] = make_int4(s, b, e, ph | (ok ? 2 : 0));
+            R.ps[k][sc][0] = p0;
+            R.ps[k][sc][1] = p1;
+            R.pbt[k][sc] = -1;
+            // fresh[] (frames since the net's reset: the cold front end's frames)
+            // as at the kernel start -- the feature-context roll reads through it
+            // after the bookkeeping has overwritten it for the next net
+            R.fresh[k][sc] = ok && r.fs.nring ? (int)r.fs.fresh[s] : 2;
+            if (ctl) {
+                CascState cs = {};
+                if (ok) cs = ca.st[s];
+                R.cst[k][sc] = cs;
+            }
         }
 #pragma unroll
         for (int o = 8; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
@@ -1366,9 +1403,10 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     auto tile_of = [&](int j) { return MT ? (j >= off1 ? 1 : 0) + (j >= off2 ? 1 : 0) + (j >= off3 ? 1 : 0) : 0; };
     auto off_of = [&](int k) { return MT ? (k == 0 ? 0 : (k == 1 ? off1 : (k == 2 ? off2 : off3))) : 0; };
     auto end_of = [&](int k) { return MT && k + 1 < nk ? off_of(k + 1) : total; };
-    // staged region: the LSTM's input fragments, then its recurrent ones, then the FC tail
-    const uint8_t* Ax = W;
-    const uint8_t* Ar = W + (LL.ar_off - LL.a_off);
+    // staged region: (FP: the layers before the LSTM,) the LSTM's input
+    // fragments, then its recurrent ones, then the FC tail
+    const uint8_t* Ax = W + (LL.a_off - r.a_off);
+    const uint8_t* Ar = W + (LL.ar_off - r.a_off);
     const EpRow* epl = ep + (LL.ep_off - r.ep_lo) + 4 * q;
     // the input half Wx.x of the NEXT step is computed at the end of each
     // step (off the recurrence's critical path) into the accumulators the
@@ -1395,6 +1433,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     TileLane xl = {0, 0, 0, false};   // load_x's tile (xk)
     int xk = -1;
     auto load_x = [&](int jj) {   // split x of pipeline step jj for the lane's stream (B fragments: high, low bytes)
+        if constexpr (FP) return;   // (FP: the prefix stage leaves x in R.xs)
         const int kx = tile_of(jj);
         if (MT && kx != xk) {
             xl = tile_lane(kx);
@@ -1417,15 +1456,23 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // nothing but the high plane (mod 2^32 the same sum, affine_acc32b.c's
     // wrap and the proven-int32 acc64 nets alike); the step then loads no cst
     constexpr bool CST_IN_ACC = ACC32;
-    auto x_half = [&]() {   // axh/axl := Wx . x (hi / lo planes) from xr
+    // xb (FP): the R.xs slot of the step (step % 3)
+    auto x_half = [&](int xb) {   // axh/axl := Wx . x (hi / lo planes) from xr (FP: from R.xs[xb])
         v4i bxh[nkt_r], bxl[nkt_r];
 #pragma unroll
         for (int kt = 0; kt < nkt_r; ++kt) {
             // lanes whose k range lies past xs loaded column 0 of the row:
             // used as is, since the A fragments' columns past the LSTM's input
             // width are zero (a select here cost 16 VALU moves per step)
-            bxh[kt] = v4i{xr[kt][0].x, xr[kt][0].y, xr[kt][0].z, xr[kt][0].w};
-            bxl[kt] = v4i{xr[kt][1].x, xr[kt][1].y, xr[kt][1].z, xr[kt][1].w};
+            if constexpr (FP) {
+                const int k0 = 64 * kt + 16 * q;
+                const uint8_t* xp = &R.xs[xb][sc][k0 < XS ? k0 : 0];
+                bxh[kt] = *reinterpret_cast<const v4i*>(xp);
+                bxl[kt] = *reinterpret_cast<const v4i*>(xp + XS);
+            } else {
+                bxh[kt] = v4i{xr[kt][0].x, xr[kt][0].y, xr[kt][0].z, xr[kt][0].w};
+                bxl[kt] = v4i{xr[kt][1].x, xr[kt][1].y, xr[kt][1].z, xr[kt][1].w};
+            }
         }
 #pragma unroll
         for (int k = 0; k < RPW; ++k) {   // one row tile's fragments at a time (no LDS stores here)
@@ -1444,11 +1491,202 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 }
         }
     };
+    // ---- FP: the prefix stage, on waves PFW and PFW + 1 (row tiles p, p + 2,
+    //      ... of the layer before the LSTM: compiled shapes, one FC layer,
+    //      K = 240, tanh) for step st of the tile's 16 streams, two steps
+    //      ahead of the LSTM step that reads its output.  Stream k's rows read
+    //      the context V[2 st + phase .. + 5] with V = prev5 ++ the segment's
+    //      features (as proj_kernel's union, one NN step per MFMA row).  The
+    //      frames sit in a per-stream ring of 8 in LDS (R.pfr; V index v at
+    //      slot v & 7): a step brings 2 new frames per stream, 160 16-byte
+    //      chunks (80 per prefix wave), loaded into registers while the wave
+    //      computes the current step and written to the ring behind it, one
+    //      barrier before the next step reads them.  The output goes to
+    //      R.xs[st % 3] in the LSTM's B-operand form.  No proj launch, and the
+    //      x rows do not go through HBM.  (Measured, not kept: the whole 6-frame
+    //      window by LDS-DMA per step -- ~380 cycles per global_load_lds issue,
+    //      the stage 4 100 cycles against the LSTM's 2 300; one prefix wave for
+    //      both row tiles -- its chain of k tiles, 5 500 cycles.)
+    constexpr int PFW = RGP + 3 + CF::SPLIT;   // the first prefix wave (FP)
+    const int pfp = g - PFW;                   // (FP: 0, 1 on the prefix waves)
+    const unsigned prg = (unsigned)r.fs.ring;
+    const FeatSrc pfs = r.fs;   // (a copy: a reference into the kernel arguments put them in scratch)
+    // the address of V index v of the tile's stream k (the general form:
+    // prev5, the ring, the cold frames after a reset; zero row outside a
+    // valid stream or past its segment)
+    auto pf_src = [&](int k, int v, int part) -> uintptr_t {
+        const int4 d = R.ti[0][k];
+        const int s_ = d.x, b_ = d.y, e_ = d.z;
+        uintptr_t src = reinterpret_cast<uintptr_t>(&nnsp_proj_zero16);
+        if (d.w & 2) {
+            if (v < 5)
+                src = reinterpret_cast<uintptr_t>(r.prev5 + ((size_t)s_ * 5 + v) * 40 + 8 * part);
+            else if (b_ + v - 5 < e_)
+                src = reinterpret_cast<uintptr_t>(feat8_ptr<true>(pfs, r.feats, s_, T, b_, b_ + v - 5, part,
+                                                                  min(max(R.fresh[0][k], 0), 2)));
+        }
+        return src;
+    };
+    // this lane's chunk slots of a step's 160 (2 new frames x 16 streams):
+    // prefix wave p takes chunks 80 p + lane and 80 p + 64 + lane (lane < 16);
+    // chunk c -> stream c / 10, frame (c % 10) / 5 of the two, 8 features
+    // c % 5.  (ln: the lane, opaque per use -- hoisted out of the step loop,
+    // the per-lane constants pinned ~30 VGPRs and spilled)
+    auto pf_chunk = [&](int i, int ln, int& k, int& fw, int& part) {
+        const int c = 80 * pfp + ln + 64 * i;
+        k = (c * 205) >> 11;   // c / 10 (c < 160)
+        const int w = c - 10 * k;
+        fw = w >= 5 ? 1 : 0;
+        part = w - 5 * fw;
+    };
+    int4 pf_x[2];   // the staged chunks of the next step's new frames
+    // FAST (steps >= 2): the new frames V[2 st + phase + 4, + 5] are past prev5
+    // and past the segment's first two (possibly cold) frames -- ring slots
+    // (abs0 + b + v - 5 - lookback) mod ring; past the segment they read an
+    // in-bounds slot whose rows are not used
+    auto pf_load = [&](int st) __attribute__((always_inline)) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i < 1 || ln < 16) {
+                int k, fw, part;
+                pf_chunk(i, ln, k, fw, part);
+                const int4 pd = R.pdesc[k];   // {row lo, row hi, slot of V index phase + 4, valid}
+                unsigned slot = (unsigned)pd.z + (unsigned)(2 * st + fw);
+                slot = slot >= prg ? slot - prg : slot;
+                const uintptr_t row = (uintptr_t)(uint32_t)pd.x | ((uintptr_t)(uint32_t)pd.y << 32);
+                uintptr_t src = pd.w ? row + (uintptr_t)(slot * 80u + 16u * (unsigned)part)
+                                     : reinterpret_cast<uintptr_t>(&nnsp_proj_zero16);
+                asm volatile("" : "+v"(src));
+                pf_x[i] = gload16(src);
+            }
+        }
+    };
+    auto pf_store = [&](int st) __attribute__((always_inline)) {   // the staged chunks -> the ring
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            if (i < 1 || ln < 16) {
+                int k, fw, part;
+                pf_chunk(i, ln, k, fw, part);
+                const int v = 2 * st + (R.ti[0][k].w & 1) + 4 + fw;
+                *reinterpret_cast<int4*>(&R.pfr[k][(v & 7) * 40 + 8 * part]) = pf_x[i];
+            }
+        }
+    };
+    const NnLayer& L0 = img.L[0];
+    auto pf_compute = [&](int st, int xb, long long* pp = nullptr) __attribute__((always_inline)) {   // pp: probes
+        // B fragments: lane (sc, q), k tile kt = columns 64 kt + 16 q .. + 15 =
+        // chunks cc = 8 kt + 2 q and cc + 1 of the 6 x 40 window (chunks 30, 31
+        // meet zero A columns: any ring row will do); chunk cc is frame cc / 5,
+        // features 8 (cc % 5) .., at V index 2 st + phase + cc / 5
+        int qq = q;   // (opaque per step, as in pf_load)
+        asm volatile("" : "+v"(qq));
+        const int v0 = 2 * st + (R.ti[0][sc].w & 1);
+        const int16_t* ring = &R.pfr[sc][0];
+        v4i bh[4], bl[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            int4 h2[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int cc = 8 * kt + 2 * qq + e;
+                const int f = (cc * 13) >> 6, part = cc - 5 * f;   // cc / 5, cc % 5 (cc < 32)
+                h2[e] = *reinterpret_cast<const int4*>(ring + ((v0 + f) & 7) * 40 + 8 * part);
+            }
+            split_hilo_r(h2[0], h2[1], bh[kt], bl[kt]);
+        }
+        const uint8_t* A0 = W + (L0.a_off - r.a_off);
+        const EpRow* e0 = ep + (L0.ep_off - r.ep_lo) + 4 * q;
+        const int rsh0 = L0.out_sh < 0 ? -L0.out_sh : 0, lsh0 = L0.out_sh > 0 ? L0.out_sh : 0;
+#pragma unroll
+        for (int rt = 0; rt < SH::R0; ++rt) {
+            if (rt % 2 != pfp) continue;   // this wave's row tiles
+            v4i w[4];
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) w[kt] = *reinterpret_cast<const v4i*>(A0 + (size_t)(rt * 4 + kt) * 1024 + 16 * lane);
+            v4i ah = {0, 0, 0, 0};
+            // ACC32: the row's constant starts the low-plane accumulator (fc_layer)
+            v4i al = ACC32 ? v4i{ep_cst<true>(e0[16 * rt]), ep_cst<true>(e0[16 * rt + 1]), ep_cst<true>(e0[16 * rt + 2]),
+                                 ep_cst<true>(e0[16 * rt + 3])}
+                           : v4i{0, 0, 0, 0};
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                ah = mfma8(w[kt], bh[kt], ah);
+                al = mfma8(w[kt], bl[kt], al);
+            }
+            if (NNSP_PROBES && pp) pp[0] = (long long)__builtin_amdgcn_s_memtime();
+            int32_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int32_t acc = (ah[i] << 8) + al[i];
+                const int32_t v = ep_out<ACC32>(acc, ACC32 ? 0 : ep_cst<ACC32>(e0[16 * rt + i]), rsh0, lsh0);
+                // columns past N: zero (as proj_kernel's x rows; the LSTM's
+                // A columns there are zero anyway)
+                o[i] = 16 * rt + 4 * q + i < SH::NW ? (int32_t)act16s(ACT_TANH, v, tt) : 0;
+            }
+            const uint32_t d0 = (uint32_t)(uint16_t)o[0] | ((uint32_t)o[1] << 16);
+            const uint32_t d1 = (uint32_t)(uint16_t)o[2] | ((uint32_t)o[3] << 16);
+            uint8_t* xp = &R.xs[xb][sc][16 * rt + 4 * q];
+            *reinterpret_cast<uint32_t*>(xp) = __builtin_amdgcn_perm(d1, d0, 0x07050301u);
+            *reinterpret_cast<uint32_t*>(xp + XS) = __builtin_amdgcn_perm(d1, d0, 0x06040200u) ^ 0x80808080u;
+        }
+        if (NNSP_PROBES && pp) pp[1] = (long long)__builtin_amdgcn_s_memtime();
+    };
+    if constexpr (FP) {
+        const bool pfw = g == PFW || g == PFW + 1;
+        if (pfw) {
+            if (pfp == 0 && lane < 16) {   // per stream: its ring row and the slot of V index phase + 4
+                const int4 d = R.ti[0][lane];
+                const int ph = d.w & 1;
+                const int v0 = (pfs.abs0 + d.y + ph + 4 - 5 - pfs.lookback) % (int)prg;
+                const uintptr_t row = reinterpret_cast<uintptr_t>(pfs.nring) + (uintptr_t)d.x * prg * 80u;
+                R.pdesc[lane] = make_int4((int)(uint32_t)row, (int)(uint32_t)(row >> 32),
+                                          v0 < 0 ? v0 + (int)prg : v0, (d.w & 2) ? 1 : 0);
+            }
+            // V indices phase .. phase + 7 of every stream (the windows of
+            // steps 0 and 1) through the general form: 640 chunks, 5 per lane
+            // of each prefix wave
+            int4 x[5];
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const int c = 320 * pfp + lane + 64 * i;   // stream c / 40, frame (c % 40) / 5
+                const int k = c / 40, w = c - 40 * k, f = w / 5, part = w - 5 * f;
+                uintptr_t src = pf_src(k, f + (R.ti[0][k].w & 1), part);
+                asm volatile("" : "+v"(src));
+                x[i] = gload16(src);
+            }
+#pragma unroll
+            for (int i = 0; i < 5; ++i) {
+                const int c = 320 * pfp + lane + 64 * i;
+                const int k = c / 40, w = c - 40 * k, f = w / 5, part = w - 5 * f;
+                const int v = f + (R.ti[0][k].w & 1);
+                *reinterpret_cast<int4*>(&R.pfr[k][(v & 7) * 40 + 8 * part]) = x[i];
+            }
+        }
+        __syncthreads();   // (the ring holds both prefix waves' chunks)
+        if (pfw) {
+            // steps 0 and 1 before the loop (the LSTM's step 0 reads step 0's
+            // x, iteration 0 computes step 1's input half)
+            if (total > 2) pf_load(2);
+            pf_compute(0, 0);
+            asm volatile("" ::: "memory");   // (the two steps one after the other: overlapped, they spilled)
+            if (total > 1) pf_compute(1, 1);
+        }
+        __syncthreads();   // (step 0's window read by both before step 2's frames replace it)
+        if (pfw && total > 2) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            pf_store(2);
+        }
+        __syncthreads();
+    }
     if (g < RGP) {   // (past a segment: row 0 of xg, unused)
         ll = xl = tile_lane(0);
         xk = 0;
         load_x(0);
-        x_half();
+        x_half(0);
         load_x(1);
     }
     // store the frame outputs the post wave left in slot p (lanes 0..15: the
@@ -1521,8 +1759,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
 #define RECUR_CLK_WAVE 0
 #endif
     constexpr int CLKW = RECUR_CLK_WAVE < RGP ? RECUR_CLK_WAVE : 0;
-    long long* clk = (NNSP_PROBES && r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 && (g == CLKW || g >= RGP))
-                         ? r.dbg_clk + 2 * (g == CLKW ? 0 : g - RGP + 1)
+    long long* clk = (NNSP_PROBES && r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 &&
+                      (g == CLKW || (g >= RGP && g < RGP + 3 + SPL) || (FP && g == RGP + 3 + SPL)))
+                         ? r.dbg_clk + (FP && g == RGP + 3 + SPL ? 14 : 2 * (g == CLKW ? 0 : g - RGP + 1))
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the
     // loop runs two iterations per trip), so every LDS access of the stages
@@ -1530,7 +1769,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     // parity cost the S2I post wave ~1100 of its ~6000 cycles per step
     // LSTM wave 0's sub-phases (dbg_clk[1536 + 8 j + k]): loads + MFMA, gates, stores, x_half, load_x
     // (in time order 0, 3, 4, 1, 2)
-    long long* lclk = (clk && g == CLKW) ? r.dbg_clk + 1536 : nullptr;
+    // (FP: the prefix wave's sub-phases instead: MFMAs done, x stored, DMAs issued)
+    long long* lclk = (clk && (FP ? g == RGP + 3 + SPL : g == CLKW)) ? r.dbg_clk + 1536 : nullptr;
 #define LCLK(k) \
     if (lclk && j < 64) lclk[8 * j + (k)] = (long long)__builtin_amdgcn_s_memtime()
     auto iteration = [&](const int j, auto CUR, auto RL) {
@@ -1593,7 +1833,7 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                 // the loads have the gates and stores to land in -- issued at
                 // the end of the step, the copy into the loop-carried xr at the
                 // loop latch waited out their latency every step
-                x_half();
+                x_half(FP ? (j + 1) % 3 : 0);
                 LCLK(3);
                 load_x(j + 2);
                 // the next tile's h and c: fetched now, h into R.hs at step 1
@@ -1684,6 +1924,21 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
                         L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                         &R.a4[cur][0][0], RS, tt, lane);
                 if (!SFC) flush(cur ^ 1);   // the post wave's outputs of the previous iteration
+            }
+        } else if constexpr (role == 5) {   // FP prefix: step j + 2 (its new frames stored in iteration j - 1)
+            if (j + 2 < total) {
+                const int st = j + 2;
+                if (clk && j < 64) clk[j * 16 - 1] = (long long)__builtin_amdgcn_s_memtime();   // (slot 13)
+                if (st + 1 < total) pf_load(st + 1);   // in flight during the compute
+                pf_compute(st, st % 3, lclk && j < 64 ? lclk + 8 * j : nullptr);
+                if (st + 1 < total) {
+                    // (the prefix waves' only vector-memory loads)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    // V[2 st + phase + 6, + 7]: slots outside step st's window
+                    // (the other prefix wave may still read it)
+                    pf_store(st + 1);
+                }
+                LCLK(2);
             }
         } else {   // post: step jp = j-3-SPL
           int wfl = 0;   // frames of this step to store (bits: t, t + 1)
@@ -1787,6 +2042,8 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
         run(std::integral_constant<int, 2>{});
     else if (SPL && g == RGP + 2)
         run(std::integral_constant<int, 3>{});
+    else if (FP && g >= RGP + 3 + SPL)
+        run(std::integral_constant<int, 5>{});
     else
         run(std::integral_constant<int, 4>{});
 #undef LCLK
@@ -1894,9 +2151,9 @@ __global__ __launch_bounds__(64 * PipeCfg<SH>::WPG, PipeCfg<SH>::MINW) void recu
     //      the net the stream runs next, position, next segment start, next
     //      round's lists.  Post wave, lane = 16 x tile + stream.
     if (post_w) {
-        const int k = lane >> 4;
+        const int k = lane >> 4 < KT ? lane >> 4 : 0;   // (lanes of tiles past KT: not ok below)
         const int4 d = R.ti[k][sc];
-        const bool ok = k < nk && (d.w & 2);
+        const bool ok = lane >> 4 < nk && (d.w & 2);
         const int sb = d.x, bb = d.y, ee = d.z, ct = R.cut[k][sc];
         if (ok && bb < ee) {
             PostState pz;
@@ -1973,23 +2230,38 @@ template <class SH>
 const void* pipe_fn_mt(bool acc32) {
     return acc32 ? (const void*)recur_pipe_kernel<SH, true, true> : (const void*)recur_pipe_kernel<SH, false, true>;
 }
+// (int32 accumulators only: the acc64 build spills ~30 VGPRs at the fused
+// workgroup's 96-register budget)
+template <class SH>
+const void* pipe_fn_fp(bool acc32) {
+    return acc32 ? (const void*)recur_pipe_kernel<SH, true, false, true> : nullptr;
+}
+
+// the shapes with a fused-prefix instantiation (FastRun.fuse): VAD
+constexpr bool fuse_shape(int shape) { return shape == NN_SHAPE_VAD; }
 
 // compiled shapes: the pipelined recurrence (one tile per workgroup)
-// mt: the several-tiles instantiation (FastRun.tseq > 1)
-const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes, bool mt = false) {
+// mode 0: one tile per workgroup; 1: several tiles run back to back
+// (FastRun.tseq > 1); 2: one tile, the prefix layers fused in (FastRun.fuse)
+template <class SH>
+const void* pipe_of(bool acc32, int mode, int* waves, size_t* tile_bytes) {
+    if (mode == 2) {
+        if constexpr (fuse_shape(std::is_same<SH, ShapeVad>::value ? NN_SHAPE_VAD : NN_SHAPE_GENERIC)) {
+            *waves = PipeCfg<SH, true>::WPG;
+            *tile_bytes = sizeof(PipeTile<SH, 1, true>);
+            return pipe_fn_fp<SH>(acc32);
+        }
+        return nullptr;
+    }
+    *waves = PipeCfg<SH>::WPG;
+    *tile_bytes = mode == 1 ? sizeof(PipeTile<SH, PIPE_KT>) : sizeof(PipeTile<SH, 1>);
+    return mode == 1 ? pipe_fn_mt<SH>(acc32) : pipe_fn<SH>(acc32);
+}
+const void* pick_pipe(int shape, bool acc32, int* waves, size_t* tile_bytes, int mode = 0) {
     switch (shape) {
-        case NN_SHAPE_VAD:
-            *waves = PipeCfg<ShapeVad>::WPG;
-            *tile_bytes = sizeof(PipeTile<ShapeVad>);
-            return mt ? pipe_fn_mt<ShapeVad>(acc32) : pipe_fn<ShapeVad>(acc32);
-        case NN_SHAPE_KWS:
-            *waves = PipeCfg<ShapeKws>::WPG;
-            *tile_bytes = sizeof(PipeTile<ShapeKws>);
-            return mt ? pipe_fn_mt<ShapeKws>(acc32) : pipe_fn<ShapeKws>(acc32);
-        case NN_SHAPE_S2I:
-            *waves = PipeCfg<ShapeS2i>::WPG;
-            *tile_bytes = sizeof(PipeTile<ShapeS2i>);
-            return mt ? pipe_fn_mt<ShapeS2i>(acc32) : pipe_fn<ShapeS2i>(acc32);
+        case NN_SHAPE_VAD: return pipe_of<ShapeVad>(acc32, mode, waves, tile_bytes);
+        case NN_SHAPE_KWS: return pipe_of<ShapeKws>(acc32, mode, waves, tile_bytes);
+        case NN_SHAPE_S2I: return pipe_of<ShapeS2i>(acc32, mode, waves, tile_bytes);
         default: return nullptr;
     }
 }
@@ -2027,14 +2299,17 @@ size_t proj_wave_bytes(int gpt) {
     return gpt == 4 ? sizeof(ProjWave<SH, 4>) : (gpt == 2 ? sizeof(ProjWave<SH, 2>) : sizeof(ProjWave<SH, 1>));
 }
 // gpt: streams per proj tile of the launch (the ProjWave layout depends on it)
-size_t fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape, int gpt) {
+// pmode (which 1, compiled shapes): the recurrence instantiation (pick_pipe's
+// mode; 1, the largest of the unfused ones, for the planner)
+size_t fast_lds_bytes(int which, int a_bytes, int units, int ep_rows, int shape, int gpt, int pmode = 1) {
     // which 0: proj (units = waves); 1: recur (units = tiles per workgroup)
     const size_t base = (size_t)a_bytes + TT_BYTES + ep_bytes(ep_rows);
     size_t pw = sizeof(ProjWave<ShapeGen>), rt = sizeof(RecTile<ShapeGen>);
+    int wv = 0;
     switch (shape) {   // compiled shapes: recur runs one pipelined tile per workgroup
-        case NN_SHAPE_VAD: pw = proj_wave_bytes<ShapeVad>(gpt); rt = sizeof(PipeTile<ShapeVad>); units = which ? PipeCfg<ShapeVad>::TPW : units; break;
-        case NN_SHAPE_KWS: pw = proj_wave_bytes<ShapeKws>(gpt); rt = sizeof(PipeTile<ShapeKws>); units = which ? PipeCfg<ShapeKws>::TPW : units; break;
-        case NN_SHAPE_S2I: pw = proj_wave_bytes<ShapeS2i>(gpt); rt = sizeof(PipeTile<ShapeS2i>); units = which ? PipeCfg<ShapeS2i>::TPW : units; break;
+        case NN_SHAPE_VAD: pw = proj_wave_bytes<ShapeVad>(gpt); pipe_of<ShapeVad>(false, pmode, &wv, &rt); units = which ? 1 : units; break;
+        case NN_SHAPE_KWS: pw = proj_wave_bytes<ShapeKws>(gpt); pipe_of<ShapeKws>(false, pmode, &wv, &rt); units = which ? 1 : units; break;
+        case NN_SHAPE_S2I: pw = proj_wave_bytes<ShapeS2i>(gpt); pipe_of<ShapeS2i>(false, pmode, &wv, &rt); units = which ? 1 : units; break;
         default: break;
     }
     return base + (size_t)units * (which == 0 ? pw : rt);
@@ -2054,15 +2329,24 @@ int nnspk_launch_proj(const NnImage* img, const FastRun* r, int blocks, int wave
     return launch(pick_proj(r->shape, img->acc32 || r->ep32, r->gpt), dim3(blocks), dim3(64 * waves), lds, stream, img, r);
 }
 
+int nnspk_fast_fuse_ok(int shape, int a_bytes, int ep_rows, int acc32) {
+    return fuse_shape(shape) && acc32 && fast_lds_bytes(1, a_bytes, 1, ep_rows, shape, 1, 2) <= 80 * 1024;
+}
+
 int nnspk_launch_recur(const NnImage* img, const FastRun* r, int tpw, const CascArgs_* ctl, void* stream) {
-    const size_t lds = nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n, r->shape);
     const int nrow = r->n_list_dev ? r->S : (r->list ? r->n_list : r->S);
     if (nrow <= 0) return 0;
     int waves = 0;
     size_t tb = 0;
     FastRun rr = *r;   // tiles per workgroup, run back to back through its pipeline
     rr.tseq = rr.tseq < 1 ? 1 : (rr.tseq > PIPE_KT ? PIPE_KT : rr.tseq);
-    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb, rr.tseq > 1)) {
+    // the fused prefix: one tile per workgroup, features from the cascade's ring
+    if (rr.fuse && (!fuse_shape(r->shape) || rr.tseq != 1 || !r->fs.nring || !(img->acc32 || r->ep32)))
+        return (int)hipErrorInvalidValue;
+    const int pmode = rr.fuse ? 2 : (rr.tseq > 1 ? 1 : 0);
+    const size_t lds = r->shape == NN_SHAPE_GENERIC ? nnspk_fast_lds_bytes(1, r->a_lds_bytes, tpw, r->ep_n, r->shape)
+                                                    : fast_lds_bytes(1, r->a_lds_bytes, 1, r->ep_n, r->shape, 1, pmode);
+    if (const void* fn = pick_pipe(r->shape, img->acc32 || r->ep32, &waves, &tb, pmode)) {
         CascArgs none;
         memset(&none, 0, sizeof none);
         const int tiles = (nrow + 15) / 16;
@@ -2085,11 +2369,12 @@ int nnspk_set_lds_limit(void) {
             int wv = 0;
             size_t tb = 0;
             const void* pipe = pick_pipe(shapes[i], a, &wv, &tb);
-            const void* pipe_mt = pick_pipe(shapes[i], a, &wv, &tb, true);
-            const void* fns[7] = {pick_proj(shapes[i], a, 1), pick_recur(shapes[i], nrts[i], a),
+            const void* pipe_mt = pick_pipe(shapes[i], a, &wv, &tb, 1);
+            const void* pipe_fp = pick_pipe(shapes[i], a, &wv, &tb, 2);
+            const void* fns[8] = {pick_proj(shapes[i], a, 1), pick_recur(shapes[i], nrts[i], a),
                                   pick_recur(NN_SHAPE_GENERIC, nrts[i], a), pipe, pick_proj(shapes[i], a, 2),
-                                  pick_proj(shapes[i], a, 4), pipe_mt};
-            for (int k = 0; k < 7; ++k) {
+                                  pick_proj(shapes[i], a, 4), pipe_mt, pipe_fp};
+            for (int k = 0; k < 8; ++k) {
                 if (!fns[k]) continue;
                 hipError_t e = hipFuncSetAttribute(fns[k], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
                 if (e != hipSuccess) return (int)e;

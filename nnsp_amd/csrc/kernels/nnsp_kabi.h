@@ -205,6 +205,10 @@ typedef struct {
     int16_t *outputs3;        /* [S][T][3] NNSPClass.outputs */
     int32_t net_id;
     int32_t gpt;              /* proj: streams per 16-row tile (1, 2 or 4; compiled shapes) */
+    int32_t fuse;             /* recur (compiled shapes, one tile per workgroup, ring features): it also runs
+                                 the layers before the LSTM itself, one pipeline stage ahead -- no proj launch,
+                                 no x rows through HBM (nnspk_fast_fuse_ok) */
+    int32_t pad_fuse;
     int32_t *n_list_rec;      /* non-NULL: proj records the list length it ran with (stats) */
     FeatSrc fs;               /* cascade feature source (fs.nring NULL: feats) */
     const int32_t *n_list_dev; /* non-NULL: the list length, read on the device (grids sized for S) */
@@ -290,6 +294,10 @@ int nnspk_launch_proj(const NnImage *img, const FastRun *r, int blocks, int wave
  * kernel (compiled shapes only); CascArgs is declared below */
 struct CascArgs_;
 int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, const struct CascArgs_ *ctl, void *stream);
+/* the compiled shape has a fused-prefix recurrence (FastRun.fuse) and its LDS
+ * (all the net's weights, every epilogue row) fits two workgroups per CU;
+ * int32-accumulator nets (acc32: the net or its proven-int32 acc64 form) */
+int nnspk_fast_fuse_ok(int shape, int a_bytes, int ep_rows, int acc32);
 int nnspk_set_lds_limit(void);
 int nnspk_malloc(void **p, size_t n);
 int nnspk_free(void *p);
