@@ -51,6 +51,7 @@ static struct {
      * Median us per frame VAD / KWS / S2I: 32.4 / 34.8 / 38.7 (2), 36.6 /
      * 39.3 / 43.3 (1), 35.9 / 38.6 / 42.4 (0), profiles/r05/dropin_wait/ */
     int wait;
+    int probe;      /* NNSP_DROPIN_PROBE=1 (PROBES builds): the drop-in kernel's phase clocks, nnsp_dropin_probes */
     uint32_t seq;
     void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
 } G = {.port = 2};
@@ -93,6 +94,16 @@ static void fail(int code, const char *what)
     } while (0)
 
 int nnsp_legacy_status(void) { return G.sticky; }
+
+/* development probe (not in the public header): the last drop-in call's
+ * phase clocks (NnRun.probe: 16 s_memrealtime values, 100 MHz) from the mapped
+ * staging; 0 when NNSP_DROPIN_PROBE is off or no call ran */
+int nnsp_dropin_probes(long long *out)
+{
+    if (!G.ready || !G.probe || G.copy || !out) return NNSP_EINVAL;
+    memcpy(out, G.hmap + G.hpin_cap - 16 - 128, 128);
+    return 0;
+}
 void nnsp_legacy_clear(void) { G.sticky = 0; }
 
 static int gctx(void)
@@ -109,6 +120,8 @@ static int gctx(void)
         G.copy = cp && atoi(cp) != 0;
         const char *wt = getenv("NNSP_DROPIN_WAIT");
         G.wait = wt ? atoi(wt) : 2;
+        const char *pb = getenv("NNSP_DROPIN_PROBE");
+        G.probe = pb && atoi(pb) != 0;
     }
     if (!G.copy && (e = nnspk_host_alloc_mapped((void **)&G.hmap, (void **)&G.hmap_dev, G.hpin_cap))) return e;
     G.ready = 1;
@@ -959,8 +972,9 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
      * at o_done = total it moved with the net's h/c size, and after a call to a
      * larger net a smaller net's word held that call's state bytes, which could
      * equal the new sequence number by chance (a stale read, no wait) */
-    const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16;
-    if (total > o_done) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
+    /* (and below it 128 bytes of development probes, NNSP_DROPIN_PROBE) */
+    const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16, o_probe = o_done - 128;
+    if (total > o_probe) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
     uint8_t *hp = G.copy ? G.hpin : G.hmap;
     memcpy(hp + o_pcm, rawPCM, 320);
     memcpy(hp + o_tail, fe->state_stftModule.dataBuffer + 160, 640);
@@ -1028,6 +1042,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
             /* a value the kernel's store cannot be mistaken for, before the launch */
             __atomic_store_n((uint32_t *)(G.hmap + o_done), ~(uint32_t)r.done_seq, __ATOMIC_RELEASE);
         }
+        if (G.probe) r.probe = (long long *)(G.hmap_dev + o_probe);
     }
     if (G.copy) {
         CK(nnspk_launch_nn(&img, &r, G.stream));

@@ -1142,9 +1142,7 @@ struct PipeCfg {
     // frame outputs are stored by the two FC waves (frame t / t + 1) instead of
     // the FC-linear wave
     static constexpr bool STORE_FC12 = SH::NOUT > 2;
-    // FP: two more waves, the fused prefix FC stage (the layer before the
-    // LSTM, two steps ahead of it, one row tile per wave; no proj launch)
-    static constexpr int NWV = LW + 3 + SPLIT + (FP ? 2 : 0); // waves per tile
+    static constexpr int NWV = LW + 3 + SPLIT;               // waves per tile
     // tiles per workgroup (the kernel supports several, sharing the staged
     // weights): one.  Two VAD tiles per workgroup (16 waves, so that every
     // net's recur workgroup fills one CU in a cascade round) measured slower:
@@ -1305,6 +1303,8 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
     // the stage with the most slack (FC linear); S2I, whose FC stages are as
     // long as its LSTM step, splits them over its two FC waves (frame t / t + 1)
     constexpr bool SFC = CF::STORE_FC12;
+    // (FP: the FC-stage waves' vmcnt(0) would also wait for SFC's output stores)
+    static_assert(!(FP && SFC), "recur_pipe_kernel: the fused prefix on nets whose FC stages store outputs");
     const bool store_w = SFC ? (g == RGP || g == RGP + 1) : g == RGP + 2;
     const int store_bits = SFC ? (g == RGP ? 1 : 2) : 3;
     // ---- the tiles' descriptors (post wave, lane = 16 x tile + stream) and
@@ -1491,10 +1491,11 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
                 }
         }
     };
-    // ---- FP: the prefix stage, on waves PFW and PFW + 1 (row tiles p, p + 2,
-    //      ... of the layer before the LSTM: compiled shapes, one FC layer,
-    //      K = 240, tanh) for step st of the tile's 16 streams, two steps
-    //      ahead of the LSTM step that reads its output.  Stream k's rows read
+    // ---- FP: the prefix stage, on the FC-stage waves RGP and RGP + 1 (row
+    //      tiles p, p + 2, ... of the layer before the LSTM: compiled shapes,
+    //      one FC layer, K = 240, tanh; the FC stages leave ~1 600 of the
+    //      iteration's ~2 500 cycles idle) for step st of the tile's 16
+    //      streams, two steps ahead of the LSTM step that reads its output.  Stream k's rows read
     //      the context V[2 st + phase .. + 5] with V = prev5 ++ the segment's
     //      features (as proj_kernel's union, one NN step per MFMA row).  The
     //      frames sit in a per-stream ring of 8 in LDS (R.pfr; V index v at
@@ -1505,10 +1506,11 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
     //      R.xs[st % 3] in the LSTM's B-operand form.  No proj launch, and the
     //      x rows do not go through HBM.  (Measured, not kept: the whole 6-frame
     //      window by LDS-DMA per step -- ~380 cycles per global_load_lds issue,
-    //      the stage 4 100 cycles against the LSTM's 2 300; one prefix wave for
-    //      both row tiles -- its chain of k tiles, 5 500 cycles.)
-    constexpr int PFW = RGP + 3 + CF::SPLIT;   // the first prefix wave (FP)
-    const int pfp = g - PFW;                   // (FP: 0, 1 on the prefix waves)
+    //      the stage 4 100 cycles against the LSTM's 2 300; one or two
+    //      waves of their own -- their chain of k tiles, 5 500 / 3 800 cycles,
+    //      and spills at the 96 registers a 9- or 10-wave workgroup allows
+    //      twice per CU.)
+    const int pfp = g - RGP;   // (FP: 0, 1 on the prefix waves)
     const unsigned prg = (unsigned)r.fs.ring;
     const FeatSrc pfs = r.fs;   // (a copy: a reference into the kernel arguments put them in scratch)
     // the address of V index v of the tile's stream k (the general form:
@@ -1586,36 +1588,42 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
         asm volatile("" : "+v"(qq));
         const int v0 = 2 * st + (R.ti[0][sc].w & 1);
         const int16_t* ring = &R.pfr[sc][0];
-        v4i bh[4], bl[4];
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-            int4 h2[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const int cc = 8 * kt + 2 * qq + e;
-                const int f = (cc * 13) >> 6, part = cc - 5 * f;   // cc / 5, cc % 5 (cc < 32)
-                h2[e] = *reinterpret_cast<const int4*>(ring + ((v0 + f) & 7) * 40 + 8 * part);
-            }
-            split_hilo_r(h2[0], h2[1], bh[kt], bl[kt]);
-        }
         const uint8_t* A0 = W + (L0.a_off - r.a_off);
         const EpRow* e0 = ep + (L0.ep_off - r.ep_lo) + 4 * q;
         const int rsh0 = L0.out_sh < 0 ? -L0.out_sh : 0, lsh0 = L0.out_sh > 0 ? L0.out_sh : 0;
 #pragma unroll
         for (int rt = 0; rt < SH::R0; ++rt) {
             if (rt % 2 != pfp) continue;   // this wave's row tiles
-            v4i w[4];
-#pragma unroll
-            for (int kt = 0; kt < 4; ++kt) w[kt] = *reinterpret_cast<const v4i*>(A0 + (size_t)(rt * 4 + kt) * 1024 + 16 * lane);
             v4i ah = {0, 0, 0, 0};
             // ACC32: the row's constant starts the low-plane accumulator (fc_layer)
             v4i al = ACC32 ? v4i{ep_cst<true>(e0[16 * rt]), ep_cst<true>(e0[16 * rt + 1]), ep_cst<true>(e0[16 * rt + 2]),
                                  ep_cst<true>(e0[16 * rt + 3])}
                            : v4i{0, 0, 0, 0};
+            // k tiles two at a time (B 16 VGPRs, A 8): all four at once, with
+            // the staged chunks beside them, spilled those right after their
+            // loads -- a wait for the load in every step
 #pragma unroll
-            for (int kt = 0; kt < 4; ++kt) {
-                ah = mfma8(w[kt], bh[kt], ah);
-                al = mfma8(w[kt], bl[kt], al);
+            for (int kh = 0; kh < 2; ++kh) {
+                v4i bh[2], bl[2], w[2];
+#pragma unroll
+                for (int k2 = 0; k2 < 2; ++k2) {
+                    const int kt = 2 * kh + k2;
+                    int4 h2[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const int cc = 8 * kt + 2 * qq + e;
+                        const int f = (cc * 13) >> 6, part = cc - 5 * f;   // cc / 5, cc % 5 (cc < 32)
+                        h2[e] = *reinterpret_cast<const int4*>(ring + ((v0 + f) & 7) * 40 + 8 * part);
+                    }
+                    split_hilo_r(h2[0], h2[1], bh[k2], bl[k2]);
+                    w[k2] = *reinterpret_cast<const v4i*>(A0 + (size_t)(rt * 4 + kt) * 1024 + 16 * lane);
+                }
+#pragma unroll
+                for (int k2 = 0; k2 < 2; ++k2) {
+                    ah = mfma8(w[k2], bh[k2], ah);
+                    al = mfma8(w[k2], bl[k2], al);
+                }
+                asm volatile("" ::: "memory");
             }
             if (NNSP_PROBES && pp) pp[0] = (long long)__builtin_amdgcn_s_memtime();
             int32_t o[4];
@@ -1636,7 +1644,7 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
         if (NNSP_PROBES && pp) pp[1] = (long long)__builtin_amdgcn_s_memtime();
     };
     if constexpr (FP) {
-        const bool pfw = g == PFW || g == PFW + 1;
+        const bool pfw = g == RGP || g == RGP + 1;
         if (pfw) {
             if (pfp == 0 && lane < 16) {   // per stream: its ring row and the slot of V index phase + 4
                 const int4 d = R.ti[0][lane];
@@ -1679,6 +1687,7 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
         if (pfw && total > 2) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             pf_store(2);
+            if (total > 3) pf_load(3);   // (stored by the loop's first iteration)
         }
         __syncthreads();
     }
@@ -1760,8 +1769,8 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
 #endif
     constexpr int CLKW = RECUR_CLK_WAVE < RGP ? RECUR_CLK_WAVE : 0;
     long long* clk = (NNSP_PROBES && r.dbg_clk && (!ctl || ca.round == 0) && blockIdx.x == 0 && lane == 0 &&
-                      (g == CLKW || (g >= RGP && g < RGP + 3 + SPL) || (FP && g == RGP + 3 + SPL)))
-                         ? r.dbg_clk + (FP && g == RGP + 3 + SPL ? 14 : 2 * (g == CLKW ? 0 : g - RGP + 1))
+                      (g == CLKW || g >= RGP))
+                         ? r.dbg_clk + 2 * (g == CLKW ? 0 : g - RGP + 1)
                          : nullptr;
     // one pipeline iteration; the buffer parity is a template constant (the
     // loop runs two iterations per trip), so every LDS access of the stages
@@ -1769,10 +1778,27 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
     // parity cost the S2I post wave ~1100 of its ~6000 cycles per step
     // LSTM wave 0's sub-phases (dbg_clk[1536 + 8 j + k]): loads + MFMA, gates, stores, x_half, load_x
     // (in time order 0, 3, 4, 1, 2)
-    // (FP: the prefix wave's sub-phases instead: MFMAs done, x stored, DMAs issued)
-    long long* lclk = (clk && (FP ? g == RGP + 3 + SPL : g == CLKW)) ? r.dbg_clk + 1536 : nullptr;
+    long long* lclk = (clk && g == CLKW) ? r.dbg_clk + 1536 : nullptr;
 #define LCLK(k) \
     if (lclk && j < 64) lclk[8 * j + (k)] = (long long)__builtin_amdgcn_s_memtime()
+    // FP: the prefix stage's share of iteration j (FC-stage waves): step
+    // st = j + 2, whose new frames went to the ring in iteration j - 1.  First
+    // step st + 1's frames (loaded a whole iteration ago) go to the ring --
+    // slots outside step st's window, which the other prefix wave may be
+    // reading -- then step st + 2's loads are issued, then step st is
+    // computed.  (Loaded at the step and stored after it, the loads were
+    // waited for: the HBM latency under load exceeds one step's compute.)
+    auto pf_step = [&](const int j) __attribute__((always_inline)) {
+        if (j + 2 < total) {
+            const int st = j + 2;
+            if (st + 1 < total) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the wave's only vector-memory loads: VAD)
+                pf_store(st + 1);
+            }
+            if (st + 2 < total) pf_load(st + 2);
+            pf_compute(st, st % 3);
+        }
+    };
     auto iteration = [&](const int j, auto CUR, auto RL) {
         constexpr int cur = decltype(CUR)::value;
         constexpr int role = decltype(RL)::value;   // 0 LSTM, 1-3 FC stages 1-3, 4 post
@@ -1906,6 +1932,7 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
                 LCLK(2);
             }
         } else if constexpr (role <= 3) {
+            if constexpr (FP && role <= 2) pf_step(j);
             if constexpr (role == 1) {   // stage 1: step j-1
                 if (j >= 1 && j - 1 < total)
                     fc_layer<ACC32, SH::R1, SH::NKR, ACT_RELU6, SH::NW, SH::NKR, true>(
@@ -1924,21 +1951,6 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
                         L4, W + (L4.a_off - r.a_off), ep + (L4.ep_off - r.ep_lo), &R.a3[cur ^ 1][0][0], RS,
                         &R.a4[cur][0][0], RS, tt, lane);
                 if (!SFC) flush(cur ^ 1);   // the post wave's outputs of the previous iteration
-            }
-        } else if constexpr (role == 5) {   // FP prefix: step j + 2 (its new frames stored in iteration j - 1)
-            if (j + 2 < total) {
-                const int st = j + 2;
-                if (clk && j < 64) clk[j * 16 - 1] = (long long)__builtin_amdgcn_s_memtime();   // (slot 13)
-                if (st + 1 < total) pf_load(st + 1);   // in flight during the compute
-                pf_compute(st, st % 3, lclk && j < 64 ? lclk + 8 * j : nullptr);
-                if (st + 1 < total) {
-                    // (the prefix waves' only vector-memory loads)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    // V[2 st + phase + 6, + 7]: slots outside step st's window
-                    // (the other prefix wave may still read it)
-                    pf_store(st + 1);
-                }
-                LCLK(2);
             }
         } else {   // post: step jp = j-3-SPL
           int wfl = 0;   // frames of this step to store (bits: t, t + 1)
@@ -2042,8 +2054,6 @@ __global__ __launch_bounds__((64 * PipeCfg<SH, FP>::WPG), (PipeCfg<SH, FP>::MINW
         run(std::integral_constant<int, 2>{});
     else if (SPL && g == RGP + 2)
         run(std::integral_constant<int, 3>{});
-    else if (FP && g >= RGP + 3 + SPL)
-        run(std::integral_constant<int, 5>{});
     else
         run(std::integral_constant<int, 4>{});
 #undef LCLK

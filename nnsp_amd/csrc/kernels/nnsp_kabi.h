@@ -173,6 +173,10 @@ typedef struct {
     void *out_dst;
     int32_t out_bytes, done_seq;
     uint32_t *done;
+    /* development probe (PROBES builds, the drop-in call): s_memrealtime (100
+     * MHz) at [0] the kernel's start, [1] the front end's end, [2 + i] the end
+     * of layer i, [14] the post-processing's end, [15] the results copied out */
+    long long *probe;
 } NnRun;
 
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */

@@ -1241,6 +1241,7 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
                 fc_layer_mfma(img, Ly, in, out, sm.tanh_tbl, lane, wv, nwv);
             }
             __syncthreads();
+            if (NNSP_PROBES && r.probe && threadIdx.x == 0 && i < 12) r.probe[2 + i] = (long long)__builtin_amdgcn_s_memrealtime();
         }
         const int16_t* fin = &sm.act[nl & 1][sc][0];
         const int nout = img.L[nl - 1].N;
@@ -1276,11 +1277,13 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
+    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[14] = (long long)__builtin_amdgcn_s_memrealtime();
     if (r.out_bytes) {   // the drop-in call's results, to mapped host memory (one workgroup)
         __threadfence();
         __syncthreads();
         for (int i = threadIdx.x; i < r.out_bytes / 16; i += blockDim.x)
             reinterpret_cast<int4*>(r.out_dst)[i] = reinterpret_cast<const int4*>(r.out_src)[i];
+        if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[15] = (long long)__builtin_amdgcn_s_memrealtime();
         if (r.done) {   // every wave's result stores complete at system scope, then the completion word
             __threadfence_system();
             __syncthreads();
@@ -1296,8 +1299,10 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRu
 // makes the front end's feature row visible to the NN's staging
 template <bool PORT>
 __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r) {
+    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[0] = (long long)__builtin_amdgcn_s_memrealtime();
     fe_body<FE_MODE_BATCH, PORT, NN_WAVES_MAX>(a);
     __syncthreads();
+    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[1] = (long long)__builtin_amdgcn_s_memrealtime();
     nn_body(img, r);
 }
 

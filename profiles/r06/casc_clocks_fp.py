@@ -49,10 +49,3 @@ for n in ("vad",):
     for k, nm in enumerate(("lstm wave 0", "stage 1 fc", "stage 2 fc", "stage 3 fc", "stage 4 post")):
         d = st[3:valid - 4, 2 * k + 1] - st[3:valid - 4, 2 * k]
         print(f"  {nm:16s} work median {np.median(d):7.0f}")
-    if st[3:valid - 4, 14].any():
-        a = st[3:valid - 4]
-        print(f"  prefix           work median {np.median(a[:, 15] - a[:, 14]):7.0f}  (dma wait {np.median(a[:, 13] - a[:, 14]):6.0f},"
-              f" compute+issue {np.median(a[:, 15] - a[:, 13]):6.0f})")
-        lw = raw[1536:2048].reshape(64, 8)[3:valid - 4]
-        print(f"    after wait -> mfma done {np.median(lw[:, 0] - a[:, 13]):6.0f}  -> x stored {np.median(lw[:, 1] - lw[:, 0]):6.0f}"
-              f"  -> dma issued {np.median(lw[:, 2] - lw[:, 1]):6.0f}  -> end {np.median(a[:, 15] - lw[:, 2]):6.0f}")
