@@ -14,10 +14,12 @@
  * sigmoid_fix / relu6_fix / linear_fix double as the layer / activation tags
  * that def_nn*.c store in NeuralNetClass and that nnsp_image.c reads.
  */
+#define _POSIX_C_SOURCE 199309L /* clock_gettime (the development probe) */
 #include <setjmp.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "nnsp_host.h"
 
@@ -51,6 +53,9 @@ static struct {
      * Median us per frame VAD / KWS / S2I: 32.4 / 34.8 / 38.7 (2), 36.6 /
      * 39.3 / 43.3 (1), 35.9 / 38.6 / 42.4 (0), profiles/r05/dropin_wait/ */
     int wait;
+    /* NNSP_DROPIN_LDS (default 1): the drop-in kernel runs the call out of LDS
+     * (inputs copied in there, weights staged beside them; NnRun.st_bytes) */
+    int lds;
     int probe;      /* NNSP_DROPIN_PROBE=1 (PROBES builds): the drop-in kernel's phase clocks, nnsp_dropin_probes */
     uint32_t seq;
     void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
@@ -101,7 +106,7 @@ int nnsp_legacy_status(void) { return G.sticky; }
 int nnsp_dropin_probes(long long *out)
 {
     if (!G.ready || !G.probe || G.copy || !out) return NNSP_EINVAL;
-    memcpy(out, G.hmap + G.hpin_cap - 16 - 128, 128);
+    memcpy(out, G.hmap + G.hpin_cap - 16 - NNSP_PROBE_BYTES, NNSP_PROBE_BYTES);
     return 0;
 }
 void nnsp_legacy_clear(void) { G.sticky = 0; }
@@ -122,6 +127,8 @@ static int gctx(void)
         G.wait = wt ? atoi(wt) : 2;
         const char *pb = getenv("NNSP_DROPIN_PROBE");
         G.probe = pb && atoi(pb) != 0;
+        const char *ld = getenv("NNSP_DROPIN_LDS");
+        G.lds = !ld || atoi(ld) != 0;
     }
     if (!G.copy && (e = nnspk_host_alloc_mapped((void **)&G.hmap, (void **)&G.hmap_dev, G.hpin_cap))) return e;
     G.ready = 1;
@@ -949,12 +956,23 @@ static size_t al16(size_t n) { return (n + 15) & ~(size_t)15; }
  * one download around the launches (round 5 before this; separate small
  * copies from pageable memory made a frame ~160-250 us, bench.py
  * --dropin-latency). */
+/* development probe (NNSP_DROPIN_PROBE): host clock, ns */
+static long long host_ns(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (long long)ts.tv_sec * 1000000000LL + ts.tv_nsec;
+}
+
 static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
 {
     FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
     NeuralNetClass *net = (NeuralNetClass *)pt_inst->pt_net;
+    long long hc[5] = {0, 0, 0, 0, 0};   /* NNSP_DROPIN_PROBE: entry, image found, staged, launched, done */
+    if (G.probe) hc[0] = host_ns();
     begin();
     img_node *n = net_image(net);
+    if (G.probe) hc[1] = host_ns();
     NnImage img = n->im.img;
     img.nn_id = pt_inst->nn_id;
     img.thresh_prob = *pt_inst->pt_thresh_prob;
@@ -972,8 +990,8 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
      * at o_done = total it moved with the net's h/c size, and after a call to a
      * larger net a smaller net's word held that call's state bytes, which could
      * equal the new sequence number by chance (a stale read, no wait) */
-    /* (and below it 128 bytes of development probes, NNSP_DROPIN_PROBE) */
-    const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16, o_probe = o_done - 128;
+    /* (and below it NNSP_PROBE_BYTES of development probes, NNSP_DROPIN_PROBE) */
+    const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16, o_probe = o_done - NNSP_PROBE_BYTES;
     if (total > o_probe) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
     uint8_t *hp = G.copy ? G.hpin : G.hmap;
     memcpy(hp + o_pcm, rawPCM, 320);
@@ -995,6 +1013,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
                 ++l;
             }
     }
+    if (G.probe) hc[2] = host_ns();
     uint8_t *d = (uint8_t *)dscratch(total);
     if (G.copy) CK(nnspk_h2d(d, hp, o_feat, G.stream));
     FeArgs a;
@@ -1043,6 +1062,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
             __atomic_store_n((uint32_t *)(G.hmap + o_done), ~(uint32_t)r.done_seq, __ATOMIC_RELEASE);
         }
         if (G.probe) r.probe = (long long *)(G.hmap_dev + o_probe);
+        if (G.lds) r.st_bytes = (int32_t)total;
     }
     if (G.copy) {
         CK(nnspk_launch_nn(&img, &r, G.stream));
@@ -1050,6 +1070,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     } else {   /* the front end and the NN in one launch */
         CK(nnspk_launch_dropin(&a, &img, &r, G.stream));
     }
+    if (G.probe) hc[3] = host_ns();
     if (!G.copy && G.wait == 2)
         wait_word((volatile uint32_t *)(G.hmap + o_done), (uint32_t)r.done_seq);
     else if (!G.copy && G.wait == 1)
@@ -1073,6 +1094,11 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     memmove(fe->state_stftModule.dataBuffer, fe->state_stftModule.dataBuffer + 160, 320 * 2);
     memcpy(fe->state_stftModule.dataBuffer + 320, rawPCM, 160 * 2);
     post_unpack(pt_inst, &ps);
+    if (G.probe && !G.copy) { /* host phases into the probe area's last longs [88, 93): the kernel wrote its own before */
+        hc[4] = host_ns();
+        long long *hp_probe = (long long *)(G.hmap + o_probe);
+        for (int k = 0; k < 5; ++k) hp_probe[88 + k] = hc[k];
+    }
     return pt_inst->trigger;
 }
 

@@ -176,8 +176,19 @@ typedef struct {
     /* development probe (PROBES builds, the drop-in call): s_memrealtime (100
      * MHz) at [0] the kernel's start, [1] the front end's end, [2 + i] the end
      * of layer i, [14] the post-processing's end, [15] the results copied out */
-    long long *probe;
+    long long *probe;         /* NNSP_PROBE_LONGS */
+    /* the drop-in kernel, st_bytes > 0: the call runs out of LDS -- its staging
+     * image [0, st_bytes) (in_dst's layout: the inputs copied in from mapped
+     * host memory, the results copied out from there), every layer's epilogue
+     * constants (st_rows rows of wsum, wsum_r, bias) and the A fragments of
+     * layers st_first.. ([st_alo, st_alo + st_abytes) of NnImage.A; the rest
+     * from memory).  The caller sets st_bytes; nnspk_launch_dropin the rest. */
+    int32_t st_bytes, st_rows, st_first, st_abytes;
+    int64_t st_alo;
+    const void *st_base;      /* the device staging buffer (FeArgs.in_dst) the image mirrors */
 } NnRun;
+#define NNSP_PROBE_LONGS 96
+#define NNSP_PROBE_BYTES (8 * NNSP_PROBE_LONGS)
 
 /* split NN path (nnsp_fast.hip): nets with exactly one LSTM layer */
 typedef struct {

@@ -24,6 +24,28 @@
 
 using namespace nnsp;
 
+// development probe (PROBES builds, NnRun.probe): the drop-in kernel's phase
+// clocks (s_memrealtime), kept in LDS and written out with the results (a
+// store to mapped host memory per phase made each barrier wait for it).
+// [0] start, [1] front end done, [2 + i] layer i done, [12] the weight
+// staging's end (wave 1), [13] the front end's tables and inputs in, [14]
+// post-processing done, [15] results copied out; [16 + 8 i + k] points k
+// inside layer i (i < 8; wave 0)
+#if NNSP_PROBES
+__shared__ long long di_clk[NNSP_PROBE_LONGS];
+#define DI_CLK_T(k, tid) \
+    do { \
+        if (threadIdx.x == (tid)) di_clk[k] = (long long)__builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#define DI_CLK(k) \
+    do { \
+        if (r.probe) DI_CLK_T(k, 0); \
+    } while (0)
+#else
+#define DI_CLK_T(k, tid) do { } while (0)
+#define DI_CLK(k) do { } while (0)
+#endif
+
 // ============================================================================
 // Front end
 // ============================================================================
@@ -136,17 +158,35 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a);
 // independent, one memory latency -- deriving them took ~21 us per workgroup,
 // chains of dependent table loads, ~5 % of a front-end workgroup's life) or
 // derived in place
+// (four 16-byte loads per lane in flight before their stores: with one load
+// and its store per iteration a 256-lane workgroup waited four memory
+// latencies in a row)
 template <bool PORT>
 __device__ __forceinline__ void fe_tables_load(FeTables& T, const FeArgs& a) {
     if (a.tb_img) {
         const uint4* src = reinterpret_cast<const uint4*>(a.tb_img);
         uint4* dst = reinterpret_cast<uint4*>(&T);
         constexpr int N = (int)(sizeof(FeTables) / 16);
-        for (int i = threadIdx.x; i < N; i += blockDim.x) dst[i] = src[i];
+        const int nt = (int)blockDim.x;
+        for (int i0 = threadIdx.x; i0 < N; i0 += 4 * nt) {
+            const uint4 v0 = src[i0], v1 = src[min(i0 + nt, N - 1)], v2 = src[min(i0 + 2 * nt, N - 1)],
+                        v3 = src[min(i0 + 3 * nt, N - 1)];
+            dst[i0] = v0;
+            if (i0 + nt < N) dst[i0 + nt] = v1;
+            if (i0 + 2 * nt < N) dst[i0 + 2 * nt] = v2;
+            if (i0 + 3 * nt < N) dst[i0 + 3 * nt] = v3;
+        }
     } else {
         fe_tables_init<PORT>(T, a);
     }
 }
+
+// behind the prebuilt tables in FeArgs.tb_img: each lane's Mel segment
+// indexes (fe_lane_init's results), read with one vector load per field
+// instead of the 64-entry scan of nnsp_tbl_melseg (dependent scalar loads)
+struct FeLaneImg {
+    int32_t mj0[64], mfirst[64], mcnt[64];
+};
 
 template <bool PORT>
 __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
@@ -389,9 +429,13 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // PORT: the ARM_OPTIMIZED=0 build's front end (row N4: Frac15 window, fft.c's
 // rfft, spec2pspec >> 15; spectrogram_module.c:33-77, feature_module.c:58-60).
 // fe_body: the kernel's work on WPG waves (fe_kernel: FeGeom's; the drop-in
-// call's fused kernel: eight)
-template <int MODE, bool PORT, int WPG>
-__device__ __forceinline__ void fe_body(FeArgs a) {
+// call's fused kernel: eight, or one when it runs out of LDS).  LI (the
+// drop-in kernel out of LDS): a's inputs and outputs inside in_dst's buffer
+// are used at the same offsets of the LDS image li, where the inputs are
+// copied to (one stream, one frame: no history)
+// IN: the drop-in call's inputs are copied in first (FeArgs.in_bytes)
+template <int MODE, bool PORT, int WPG, bool LI = false, bool IN = LI>
+__device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr) {
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
     // contiguous so that the padded T1 transpose may use both
@@ -441,23 +485,49 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
     // the drop-in call's inputs, from mapped host memory (one workgroup; the
     // waves read them only after the barrier behind the tables, whose loads
     // overlap these)
-    if (a.in_bytes)
-        for (int i = threadIdx.x; i < a.in_bytes / 16; i += blockDim.x)
-            reinterpret_cast<int4*>(a.in_dst)[i] = reinterpret_cast<const int4*>(a.in_src)[i];
-    fe_tables_load<PORT>(TB, a);
+    // (LI: the rebased pointers; otherwise a's own, as they are -- a local
+    // copy of them cost the batch mode's 80-VGPR budget a spill)
+#define FE_RB(T, p) reinterpret_cast<T>(li + (reinterpret_cast<const uint8_t*>(p) - reinterpret_cast<const uint8_t*>(a.in_dst)))
+    const int16_t* const pcm_li = LI ? FE_RB(const int16_t*, a.pcm) : nullptr;
+    const int16_t* const tail_li = LI ? FE_RB(const int16_t*, a.tail) : nullptr;
+    int16_t* const feats_li = LI ? FE_RB(int16_t*, a.feats) : nullptr;
+    int32_t* const dbg_log_li = LI ? FE_RB(int32_t*, a.dbg_log) : nullptr;
+#define FE_P(name) (LI ? name##_li : a.name)
     const int lane = threadIdx.x & 63;
+    // the inputs' first two shares, the lanes' Mel indexes and the tables:
+    // every load in flight before the first store (one memory latency)
+    const int nin = IN ? a.in_bytes / 16 : 0, nt = (int)blockDim.x, tid = (int)threadIdx.x;
+    const int4* const isrc = reinterpret_cast<const int4*>(a.in_src);
+    int4* const idst = reinterpret_cast<int4*>(LI ? li : a.in_dst);
+    int4 iv0 = make_int4(0, 0, 0, 0), iv1 = make_int4(0, 0, 0, 0);
+    if (tid < nin) iv0 = isrc[tid];
+    if (tid + nt < nin) iv1 = isrc[tid + nt];
+    FeLane L;
+    if (a.tb_img) {
+        const FeLaneImg* lg = reinterpret_cast<const FeLaneImg*>(reinterpret_cast<const FeTables*>(a.tb_img) + 1);
+        L.mj0 = lg->mj0[lane];
+        L.mfirst = lg->mfirst[lane];
+        L.mcnt = lg->mcnt[lane];
+        fe_tables_load<PORT>(TB, a);
+    } else {   // (L derived after the tables: not live across their derivation)
+        fe_tables_init<PORT>(TB, a);
+        fe_lane_init(L, lane);
+    }
+    if (tid < nin) idst[tid] = iv0;
+    if (tid + nt < nin) idst[tid + nt] = iv1;
+    for (int i = tid + 2 * nt; i < nin; i += nt) idst[i] = isrc[i];
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     int32_t* X = XPs[wv];
     int32_t* P = XPs[wv] + FE_X_DW;
     // the Mel partial sums go to X, dead once the split has read it (the next
     // frame's cFFT writes X only after the frame's last wave_lds_sync)
     int64_t* Mp = reinterpret_cast<int64_t*>(X);
-    FeLane L;
-    fe_lane_init(L, lane);
     __syncthreads();
+    if constexpr (LI) DI_CLK_T(13, 0);
     // (after the barrier: the drop-in call copies them in above)
-    const int32_t mean = lane < 40 ? a.mean[lane] : 0;
-    const int32_t stdR = lane < 40 ? a.stdR[lane] : 0;
+    const int32_t mean = lane < 40 ? (LI ? FE_RB(const int32_t*, a.mean) : a.mean)[lane] : 0;
+    const int32_t stdR = lane < 40 ? (LI ? FE_RB(const int32_t*, a.stdR) : a.stdR)[lane] : 0;
+#undef FE_RB
     const unsigned wid = blockIdx.x * (unsigned)WPG + (unsigned)wv;
     unsigned fbeg, fend;
     range_of(wid, fbeg, fend);
@@ -495,9 +565,9 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
         if (cold) {
             if (fi < p.z) return nnsp_zero_pcm;
         } else if (fi < p.b) {
-            return a.tail + (size_t)p.s * (a.tail_stride ? (unsigned)a.tail_stride : 320u) + (fi - p.b + 2) * 160;
+            return FE_P(tail) + (size_t)p.s * (a.tail_stride ? (unsigned)a.tail_stride : 320u) + (fi - p.b + 2) * 160;
         }
-        if constexpr (shared) return a.pcm + ((size_t)p.s * a.T + fi) * 160;
+        if constexpr (shared || LI) return FE_P(pcm) + ((size_t)p.s * a.T + fi) * 160;
         const int x = fi - a.lookback;
         return x >= 0 ? a.pcm + ((size_t)p.s * a.T + x) * 160
                       : a.hist + ((size_t)p.s * a.hist_frames + a.hist_frames + x) * 160;
@@ -512,7 +582,7 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
             // buffer loads from a descriptor on the window's first sample (a
             // wave-uniform base, SALU) at the lane's byte offset: no per-lane
             // 64-bit address arithmetic per frame
-            const __amdgpu_buffer_rsrc_t rs = pcm_rsrc(a.pcm + wave_off(((size_t)p.s * a.T + x0) * 160));
+            const __amdgpu_buffer_rsrc_t rs = pcm_rsrc(FE_P(pcm) + wave_off(((size_t)p.s * a.T + x0) * 160));
             const int vo = 2 * o;
             // (the rows' byte offsets as SGPR offsets: one lane-offset VGPR)
             r[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, vo, 0, 0);
@@ -568,7 +638,7 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
                 (r0 + nstride)[lane] = (int16_t)(pv01 >> 16);
                 (r0 + 2 * nstride)[lane] = (int16_t)pv2;
             } else {
-                a.feats[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
+                FE_P(feats)[(size_t)po * 40 + lane] = (int16_t)(pv01 & 0xffff);
             }
         }
     };
@@ -709,7 +779,7 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
                     if (k < L.mcnt) mac += Mp[L.mfirst + k];
             }
             const int32_t lg = log10_q15_lds(sat32_shr15(mac), TB.logp);
-            if (MODE == FE_MODE_BATCH && a.dbg_log) a.dbg_log[(size_t)fo * 40 + lane] = lg;
+            if (MODE == FE_MODE_BATCH && (LI || a.dbg_log)) FE_P(dbg_log)[(size_t)fo * 40 + lane] = lg;
             if constexpr (shared) {
                 // (abs0 + t) % ring with t < T <= ring: one conditional subtract
                 unsigned slot = ring0 + (unsigned)t;
@@ -753,6 +823,7 @@ __device__ __forceinline__ void fe_body(FeArgs a) {
         wclk[3] = (long long)(fend - fbeg) | (nnsp_hw_where() << 32);
     }
 #undef FCLK
+#undef FE_P
 }
 template <int MODE, bool PORT>
 __global__ __launch_bounds__((64 * FeGeom<MODE, PORT>::WPG), (FeGeom<MODE, PORT>::MINW)) void fe_kernel(FeArgs a) {
@@ -1068,32 +1139,80 @@ struct alignas(16) NnLds {
     int32_t active[16];
 };
 
-__device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
-                              int16_t* out, const int16_t* tt, int lane, int rt0, int rstep) {
+// Ab: NnImage.A (or its LDS copy, offsets rebased); ws / bs: the image's
+// wsum / bias (or their LDS copies).  ONE (the drop-in call: stream 0 is the
+// tile's only stream): the accumulators of column 0 (lanes 0, 16, 32, 48, four
+// rows each) are spread over lanes 0..15, one row each, so that the epilogue
+// -- a long dependent chain per row -- runs once per lane instead of four times
+template <bool ONE = false>
+__device__ __forceinline__ void fc_layer_mfma(const uint8_t* Ab, const int32_t* ws, const int16_t* bs,
+                                              const NnLayer& Ly, const int16_t* in, int16_t* out,
+                                              const int16_t* tt, int lane, int rt0, int rstep, int pk = -1) {
+    if (pk >= 0) DI_CLK_T(pk, 0);
+    // the descriptor's fields in registers, and the epilogue in phases (every
+    // row's constants and table entries loaded before its first store): its
+    // LDS stores could alias those loads (the drop-in kernel's constants sit
+    // in LDS), which serialised one row after another, ~1 us per layer
+    const NnLayer L = Ly;
     v4i bh[NN_KT], bl[NN_KT];
-    load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bh, bl);
+    load_b<NN_KT>(in, NN_ASTRIDE, L.nkt, lane, bh, bl);
+    if (pk >= 0) DI_CLK_T(pk + 1, 0);
     const int sc = lane & 15, q = lane >> 4;
-    const uint8_t* A = img.A + Ly.a_off;
-    for (int rt = rt0; rt < Ly.nrt; rt += rstep) {
+    const uint8_t* A = Ab + L.a_off;
+    for (int rt = rt0; rt < L.nrt; rt += rstep) {
         v4i ah = {0, 0, 0, 0}, al = {0, 0, 0, 0};
 #pragma unroll
         for (int kt = 0; kt < NN_KT; ++kt)
-            if (kt < Ly.nkt) {
-                const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
+            if (kt < L.nkt) {
+                const v4i w = load_frag(A + (size_t)(rt * L.nkt + kt) * 1024, lane);
                 ah = mfma8(w, bh[kt], ah);
                 al = mfma8(w, bl[kt], al);
             }
+        if (pk >= 0 && rt == rt0) DI_CLK_T(pk + 2, 0);
+        if constexpr (ONE) {
+            // lane l < 16 takes row 16 rt + l: accumulator l & 3 of lane 16 (l >> 2)
+            int32_t x[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) x[i] = __builtin_amdgcn_ds_bpermute((lane >> 2) << 6, (ah[i] << 8) + al[i]);
+            const int k = lane & 3;
+            const int32_t xs = k == 0 ? x[0] : (k == 1 ? x[1] : (k == 2 ? x[2] : x[3]));
+            const int row = 16 * rt + lane;
+            if (lane < 16) {
+                const int32_t v = affine_out(xs + ws[L.ep_off + row], bs[L.ep_off + row], L, L.acc32);
+                if (row < L.rows) {
+                    if (L.act == ACT_LINEAR)
+                        reinterpret_cast<int32_t*>(out)[row] = v;
+                    else
+                        out[row] = act16(L.act, v, tt);
+                }
+            }
+            if (pk >= 0 && rt == rt0) DI_CLK_T(pk + 3, 0);
+            continue;
+        }
+        // (rows up to 16 * nrt: the constants are padded with zeros)
+        const int r0 = 16 * rt + 4 * q;
+        int32_t v[4];
+        int16_t b[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            const int row = 16 * rt + 4 * q + i;
-            if (row >= Ly.rows) continue;
-            const int32_t sum = (ah[i] << 8) + al[i] + img.wsum[Ly.ep_off + row];
-            const int32_t v = affine_out(sum, img.bias[Ly.ep_off + row], Ly, Ly.acc32);
-            if (Ly.act == ACT_LINEAR)
-                reinterpret_cast<int32_t*>(out + sc * NN_ASTRIDE)[row] = v;
-            else
-                out[sc * NN_ASTRIDE + row] = act16(Ly.act, v, tt);
+            v[i] = ws[L.ep_off + r0 + i];
+            b[i] = bs[L.ep_off + r0 + i];
         }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = affine_out((ah[i] << 8) + al[i] + v[i], b[i], L, L.acc32);
+        if (L.act == ACT_LINEAR) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (r0 + i < L.rows) reinterpret_cast<int32_t*>(out + sc * NN_ASTRIDE)[r0 + i] = v[i];
+        } else {
+            int16_t o[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = act16(L.act, v[i], tt);
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (r0 + i < L.rows) out[sc * NN_ASTRIDE + r0 + i] = o[i];
+        }
+        if (pk >= 0 && rt == rt0) DI_CLK_T(pk + 3, 0);
     }
 }
 
@@ -1102,15 +1221,19 @@ __device__ void fc_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16
 // tile rt holds gates i,j,f,o of unit 4*rt+q in its 4 accumulator registers.
 // h comes staged in hbuf; the cell state row of the lane's stream (cg, NULL
 // for a padding stream) stays in HBM: lane (sc, q) owns units 4*rt + q.
-__device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int16_t* in,
-                                int16_t* out, const int16_t* hbuf, int32_t* cg, const int16_t* tt,
-                                int lane, bool commit, int rt0, int rstep) {
+__device__ __forceinline__ void lstm_layer_mfma(const uint8_t* Ab, const int32_t* ws, const int32_t* wsr,
+                                                const int16_t* bs, const NnLayer& Lg, const int16_t* in,
+                                                int16_t* out, const int16_t* hbuf, int32_t* cg, const int16_t* tt,
+                                                int lane, bool commit, int rt0, int rstep, int pk = -1) {
+    if (pk >= 0) DI_CLK_T(pk, 0);
+    const NnLayer Ly = Lg;   // (fields in registers, as fc_layer_mfma)
     v4i bxh[NN_KT], bxl[NN_KT], bhh[NN_KT], bhl[NN_KT];
     load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
     load_b<NN_KT>(hbuf, NN_ASTRIDE, Ly.nkt_r, lane, bhh, bhl);
+    if (pk >= 0) DI_CLK_T(pk + 1, 0);
     const int sc = lane & 15, q = lane >> 4;
-    const uint8_t* A = img.A + Ly.a_off;
-    const uint8_t* Ar = img.A + Ly.ar_off;
+    const uint8_t* A = Ab + Ly.a_off;
+    const uint8_t* Ar = Ab + Ly.ar_off;
     const int acc32 = Ly.acc32;
     for (int rt = rt0; rt < Ly.nrt; rt += rstep) {
         v4i xh = {0, 0, 0, 0}, xl = {0, 0, 0, 0}, hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
@@ -1128,14 +1251,15 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
                 hh = mfma8(w, bhh[kt], hh);
                 hl = mfma8(w, bhl[kt], hl);
             }
+        if (pk >= 0 && rt == rt0) DI_CLK_T(pk + 2, 0);
         const int u = 4 * rt + q;
         if (u >= Ly.N) continue;
         int16_t g[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int row = 16 * rt + 4 * q + i;
-            const int32_t sx = (xh[i] << 8) + xl[i] + img.wsum[Ly.ep_off + row];
-            const int32_t sh = (hh[i] << 8) + hl[i] + img.wsum_r[Ly.ep_off + row];
+            const int32_t sx = (xh[i] << 8) + xl[i] + ws[Ly.ep_off + row];
+            const int32_t sh = (hh[i] << 8) + hl[i] + wsr[Ly.ep_off + row];
             // rc_Krows_8x16 (affine.c:348-407): x part, shift_64b(qi_rec - qi),
             // then the recurrent part + bias with the is_out epilogue
             int64_t pre;
@@ -1143,7 +1267,7 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
                 pre = (int64_t)wadd(shift32(sx, Ly.xs_sh), sh);
             else
                 pre = shift64((int64_t)sx, Ly.xs_sh) + (int64_t)sh;
-            const int32_t v = affine_out(pre, img.bias[Ly.ep_off + row], Ly, acc32);
+            const int32_t v = affine_out(pre, bs[Ly.ep_off + row], Ly, acc32);
             g[i] = i == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
         }
         const int32_t c_old = cg ? cg[u] : 0;
@@ -1151,6 +1275,85 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
         const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * g[3]) >> 15);
         if (commit && cg) cg[u] = c_new;
         out[sc * NN_ASTRIDE + u] = hv;
+    }
+}
+
+// lstm_layer_mfma for the drop-in call (stream 0 alone): the wave's row tiles
+// in rounds of four, tile g of a round in lane group g (lanes 16 g..16 g + 15).
+// Each tile's MFMA sums of column 0 go through the wave's 2 x 64-word LDS
+// scratch scr (row-major per group), so that lane 16 g + l takes row 16 rt_g +
+// l: gate l & 3 of unit 4 rt_g + (l >> 2); the first lane of each quad then
+// runs the unit's cell.  One epilogue per round instead of four per tile.
+__device__ __forceinline__ void lstm_layer_one(const uint8_t* Ab, const int32_t* ws, const int32_t* wsr,
+                                               const int16_t* bs, const NnLayer& Lg, const int16_t* in,
+                                               int16_t* out, const int16_t* hbuf, int32_t* cg, const int16_t* tt,
+                                               int32_t* scr, int lane, bool commit, int rt0, int rstep,
+                                               int pk = -1) {
+    if (pk >= 0) DI_CLK_T(pk, 0);
+    const NnLayer Ly = Lg;
+    v4i bxh[NN_KT], bxl[NN_KT], bhh[NN_KT], bhl[NN_KT];
+    load_b<NN_KT>(in, NN_ASTRIDE, Ly.nkt, lane, bxh, bxl);
+    load_b<NN_KT>(hbuf, NN_ASTRIDE, Ly.nkt_r, lane, bhh, bhl);
+    if (pk >= 0) DI_CLK_T(pk + 1, 0);
+    const int sc = lane & 15, q = lane >> 4;
+    const uint8_t* A = Ab + Ly.a_off;
+    const uint8_t* Ar = Ab + Ly.ar_off;
+    const int acc32 = Ly.acc32;
+    for (int rb = rt0; rb < Ly.nrt; rb += 4 * rstep) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int rt = rb + g * rstep;
+            if (rt >= Ly.nrt) break;   // (wave-uniform)
+            v4i xh = {0, 0, 0, 0}, xl = {0, 0, 0, 0}, hh = {0, 0, 0, 0}, hl = {0, 0, 0, 0};
+#pragma unroll
+            for (int kt = 0; kt < NN_KT; ++kt)
+                if (kt < Ly.nkt) {
+                    const v4i w = load_frag(A + (size_t)(rt * Ly.nkt + kt) * 1024, lane);
+                    xh = mfma8(w, bxh[kt], xh);
+                    xl = mfma8(w, bxl[kt], xl);
+                }
+#pragma unroll
+            for (int kt = 0; kt < NN_KT; ++kt)
+                if (kt < Ly.nkt_r) {
+                    const v4i w = load_frag(Ar + (size_t)(rt * Ly.nkt_r + kt) * 1024, lane);
+                    hh = mfma8(w, bhh[kt], hh);
+                    hl = mfma8(w, bhl[kt], hl);
+                }
+            if (sc == 0) {   // column 0: rows 4 q .. 4 q + 3 of tile g
+                *reinterpret_cast<int4*>(scr + 16 * g + 4 * q) =
+                    make_int4((xh[0] << 8) + xl[0], (xh[1] << 8) + xl[1], (xh[2] << 8) + xl[2], (xh[3] << 8) + xl[3]);
+                *reinterpret_cast<int4*>(scr + 64 + 16 * g + 4 * q) =
+                    make_int4((hh[0] << 8) + hl[0], (hh[1] << 8) + hl[1], (hh[2] << 8) + hl[2], (hh[3] << 8) + hl[3]);
+            }
+        }
+        if (pk >= 0 && rb == rt0) DI_CLK_T(pk + 2, 0);
+        // (the same wave's LDS stores, then loads: in order)
+        const int rt = rb + q * rstep;
+        const bool ok = rt < Ly.nrt;
+        const int row = 16 * rt + sc, k = lane & 3;
+        const int rr = ok ? row : 0;   // (constants read in range)
+        const int32_t sx = scr[lane] + ws[Ly.ep_off + rr];
+        const int32_t sh = scr[64 + lane] + wsr[Ly.ep_off + rr];
+        // rc_Krows_8x16 (affine.c:348-407), as lstm_layer_mfma
+        int64_t pre;
+        if (acc32)
+            pre = (int64_t)wadd(shift32(sx, Ly.xs_sh), sh);
+        else
+            pre = shift64((int64_t)sx, Ly.xs_sh) + (int64_t)sh;
+        const int32_t v = affine_out(pre, bs[Ly.ep_off + rr], Ly, acc32);
+        const int32_t gk = k == 1 ? tanh_q15(v, tt) : sigmoid_q15(v, tt);
+        const int qb = (lane & ~3) << 2;   // the quad's first lane
+        const int32_t g0 = __builtin_amdgcn_ds_bpermute(qb, gk), g1 = __builtin_amdgcn_ds_bpermute(qb + 4, gk),
+                      g2 = __builtin_amdgcn_ds_bpermute(qb + 8, gk), g3 = __builtin_amdgcn_ds_bpermute(qb + 12, gk);
+        const int u = 4 * rt + (sc >> 2);
+        if (ok && k == 0 && u < Ly.N) {
+            const int32_t c_old = cg[u];
+            const int32_t c_new = sat32(((int64_t)(int16_t)g0 * (int16_t)g1 + (int64_t)(int16_t)g2 * c_old) >> 15);
+            const int16_t hv = sat16(((int32_t)tanh_q15(c_new, tt) * (int16_t)g3) >> 15);
+            if (commit) cg[u] = c_new;
+            out[u] = hv;
+        }
+        if (pk >= 0 && rb == rt0) DI_CLK_T(pk + 3, 0);
     }
 }
 
@@ -1162,8 +1365,18 @@ __device__ void lstm_layer_mfma(const NnImage& img, const NnLayer& Ly, const int
 // wave walked every row tile's weight loads and MFMAs in sequence, ~30-75 us
 // of the call's 54-97 us (rocprofv3, profiles/r05/dropin_nn/).
 #define NN_WAVES_MAX 8
-__device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
+// DI (the drop-in kernel running out of LDS, NnRun.st_bytes > 0): the
+// epilogue constants (ws, wsr, bs) and r's buffers point into LDS, and the
+// layers from r.st_first on read their A fragments there too (Ast: NnImage.A's
+// offsets rebased onto the LDS copy) -- the layer code inlined once per
+// operand address space, so that each copy reads LDS or global memory directly
+template <bool DI>
+__device__ __forceinline__ void nn_body(const NnImage& img, NnRun r, const int32_t* ws, const int32_t* wsr,
+                                        const int16_t* bs, const uint8_t* Ast, const int16_t* ttab = nullptr,
+                                        int32_t* scr = nullptr) {
     __shared__ NnLds sm;
+    // the activation table (DI: ttab, staged in LDS during the front end)
+    const int16_t* const tt = DI ? ttab : sm.tanh_tbl;
     const int lane = threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int nwv = (int)(blockDim.x >> 6);
@@ -1172,7 +1385,8 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
     const int s0 = blockIdx.x * 16;
     const int s = s0 + sc;
     const bool valid = s < r.S;
-    for (int i = threadIdx.x; i < 384; i += blockDim.x) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
+    if (!DI)
+        for (int i = threadIdx.x; i < 384; i += blockDim.x) sm.tanh_tbl[i] = nnsp_tbl_tanh[i];
     // LSTM state rows (neural_nets.c:27-42 layout: h int16[N], c int32[N]) of
     // stream gs, layer l: r.h / r.c + (gs * n_lstm + l) * hs
     const size_t hs = (size_t)r.hs;
@@ -1180,6 +1394,9 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
     if (w0 && lane < 16 && valid && r.post) ps = reinterpret_cast<const PostState*>(r.post)[s];
     if (w0 && lane < 16) sm.slides[lane] = (valid && r.post) ? ps.slides : 1;
     __syncthreads();
+    // (development probes of the prologue, nets of at most five layers: [7] its
+    // first barrier passed, [8] the context staged, [9] the context barrier passed)
+    if (DI && img.nl <= 5) DI_CLK(7);
     const int phase = r.mode == NN_MODE_DIRECT ? 0 : 1 - sm.slides[sc];
     const int T = r.mode == NN_MODE_DIRECT ? 1 : r.T;
     const int nsteps = (T + 1) / 2;
@@ -1199,7 +1416,7 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
                 int4 v = make_int4(0, 0, 0, 0);
                 if (active) {
                     const int16_t* src;
-                    if (r.mode == NN_MODE_DIRECT) {
+                    if (!DI && r.mode == NN_MODE_DIRECT) {   // (DI: stream mode)
                         src = r.direct_in + (size_t)s * NN_MAX_K + 8 * cch;
                     } else {
                         const int idx = t + m;
@@ -1211,7 +1428,9 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
                 *reinterpret_cast<int4*>(&sm.act[0][sc][8 * cch]) = v;
             }
         }
+        if (DI && img.nl <= 5 && j == 0) DI_CLK(8);
         __syncthreads();
+        if (DI && img.nl <= 5 && j == 0) DI_CLK(9);
         int lst = 0;
         for (int i = 0; i < nl; ++i) {
             const NnLayer& Ly = img.L[i];
@@ -1228,8 +1447,17 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
                     sm.h[st][u] = gs < r.S ? r.h[((size_t)gs * img.n_lstm + lst) * hs + u] : (int16_t)0;
                 }
                 __syncthreads();
-                int32_t* cg = valid ? r.c + ((size_t)s * img.n_lstm + lst) * hs : nullptr;
-                lstm_layer_mfma(img, Ly, in, out, &sm.h[0][0], cg, sm.tanh_tbl, lane, active, wv, nwv);
+                // (DI: every lane works for stream 0 -- its cell row and its activity)
+                int32_t* cg = DI ? r.c + (size_t)lst * hs : (valid ? r.c + ((size_t)s * img.n_lstm + lst) * hs : nullptr);
+                const bool commit = DI ? sm.active[0] != 0 : active;
+                if (DI && i >= r.st_first)
+                    lstm_layer_one(Ast, ws, wsr, bs, Ly, in, out, &sm.h[0][0], cg, tt, scr + 128 * wv, lane, commit,
+                                   wv, nwv, NNSP_PROBES && r.probe && i < 8 ? 16 + 8 * i : -1);
+                else if (DI)
+                    lstm_layer_one(img.A, ws, wsr, bs, Ly, in, out, &sm.h[0][0], cg, tt, scr + 128 * wv, lane, commit,
+                                   wv, nwv);
+                else
+                    lstm_layer_mfma(img.A, ws, wsr, bs, Ly, in, out, &sm.h[0][0], cg, tt, lane, commit, wv, nwv);
                 __syncthreads();
                 // h_state := output after all groups (lstm.c:205-206)
                 for (int idx = threadIdx.x; idx < 16 * N; idx += blockDim.x) {
@@ -1238,10 +1466,15 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
                 }
                 ++lst;
             } else {
-                fc_layer_mfma(img, Ly, in, out, sm.tanh_tbl, lane, wv, nwv);
+                if (DI && i >= r.st_first)
+                    fc_layer_mfma<DI>(Ast, ws, bs, Ly, in, out, tt, lane, wv, nwv,
+                                  NNSP_PROBES && r.probe && i < 8 ? 16 + 8 * i : -1);
+                else
+                    fc_layer_mfma<DI>(img.A, ws, bs, Ly, in, out, tt, lane, wv, nwv);
             }
+            if (NNSP_PROBES && r.probe && i < 8) DI_CLK_T(16 + 8 * i + 4, 0);
             __syncthreads();
-            if (NNSP_PROBES && r.probe && threadIdx.x == 0 && i < 12) r.probe[2 + i] = (long long)__builtin_amdgcn_s_memrealtime();
+            if (i < 8) DI_CLK(2 + i);   // (slots 10-13 taken)
         }
         const int16_t* fin = &sm.act[nl & 1][sc][0];
         const int nout = img.L[nl - 1].N;
@@ -1277,13 +1510,18 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
         ps.slides = (int16_t)(ps.slides ^ (T & 1));
         reinterpret_cast<PostState*>(r.post)[s] = ps;
     }
-    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[14] = (long long)__builtin_amdgcn_s_memrealtime();
+    DI_CLK(14);
     if (r.out_bytes) {   // the drop-in call's results, to mapped host memory (one workgroup)
         __threadfence();
         __syncthreads();
         for (int i = threadIdx.x; i < r.out_bytes / 16; i += blockDim.x)
             reinterpret_cast<int4*>(r.out_dst)[i] = reinterpret_cast<const int4*>(r.out_src)[i];
-        if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[15] = (long long)__builtin_amdgcn_s_memrealtime();
+        DI_CLK(15);
+#if NNSP_PROBES
+        if (r.probe && threadIdx.x == 0) di_clk[11] = (long long)__builtin_amdgcn_s_memtime();
+        if (r.probe && threadIdx.x == 0)
+            for (int k = 0; k < NNSP_PROBE_LONGS; ++k) r.probe[k] = di_clk[k];
+#endif
         if (r.done) {   // every wave's result stores complete at system scope, then the completion word
             __threadfence_system();
             __syncthreads();
@@ -1292,18 +1530,121 @@ __device__ __forceinline__ void nn_body(NnImage img, NnRun r) {
         }
     }
 }
-__global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) { nn_body(img, r); }
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void nn_kernel(NnImage img, NnRun r) {
+    nn_body<false>(img, r, img.wsum, img.wsum_r, img.bias, nullptr);
+}
 
 // The drop-in call (NNSPClass_exec, one stream, one frame) in one launch: the
-// front end on eight waves (wave 0 has the frame), then the NN; the barrier
-// makes the front end's feature row visible to the NN's staging
-template <bool PORT>
+// front end (wave 0 has the frame), then the NN on eight waves; the barrier
+// makes the front end's feature row visible to the NN's staging.
+// ST (NnRun.st_bytes > 0): the call runs out of LDS.  The inputs are copied
+// from mapped host memory into an LDS image of the staging buffer (in_dst's
+// layout; every pointer into it rebased), and while wave 0 runs the frame the
+// seven other waves copy the layers' epilogue constants and A fragments into
+// LDS; the results go back to mapped host memory from the image.  Device
+// memory is then read only for the tables and the weights that do not fit:
+// each layer's memory round trips (fragments, constants, h / c, context) were
+// most of its 1.4-4.6 us (dropin_kernel phase clocks, profiles/r06/).
+// d[i] = s[i] for i = i0, i0 + NT, ... < n: U loads in flight per lane
+template <int U, int NT>
+__device__ __forceinline__ void lds_fill(int4* d, const int4* s, int n, int i0) {
+    for (; i0 < n; i0 += NT * U) {
+        int4 w[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) w[u] = s[min(i0 + NT * u, n - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (i0 + NT * u < n) d[i0 + NT * u] = w[u];
+    }
+}
+
+template <bool PORT, bool ST>
 __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r) {
-    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    fe_body<FE_MODE_BATCH, PORT, NN_WAVES_MAX>(a);
-    __syncthreads();
-    if (NNSP_PROBES && r.probe && threadIdx.x == 0) r.probe[1] = (long long)__builtin_amdgcn_s_memrealtime();
-    nn_body(img, r);
+#if NNSP_PROBES
+    if (r.probe && threadIdx.x < NNSP_PROBE_LONGS) di_clk[threadIdx.x] = 0;   // (wave 0's own slots first)
+#endif
+    DI_CLK(0);
+#if NNSP_PROBES
+    if (r.probe && threadIdx.x == 0) di_clk[10] = (long long)__builtin_amdgcn_s_memtime();
+#endif
+    if constexpr (!ST) {
+        fe_body<FE_MODE_BATCH, PORT, NN_WAVES_MAX, false, true>(a);
+        __syncthreads();
+        DI_CLK(1);
+        nn_body<false>(img, r, img.wsum, img.wsum_r, img.bias, nullptr);
+    } else {
+        extern __shared__ __attribute__((aligned(16))) uint8_t di_lds[];
+        // (r.st_base == a.in_dst: reading a's fields here as well made the
+        // compiler keep a copy of FeArgs in scratch)
+        const uint8_t* const dbase = reinterpret_cast<const uint8_t*>(r.st_base);
+        // a pointer into the device staging buffer -> the same byte of the image
+        auto rb = [&](const void* p) -> uint8_t* { return di_lds + (reinterpret_cast<const uint8_t*>(p) - dbase); };
+        // LDS: image [0, st_bytes) | wsum | wsum_r [st_rows] int32 | bias [st_rows] int16 |
+        // the activation table (384 int16) | the LSTM's per-wave scratch (2 x 64 int32) | A fragments
+        const int ob = r.st_bytes, ow = ob + 4 * r.st_rows, oz = ow + 4 * r.st_rows, ot = oz + 2 * r.st_rows,
+                  osc = ot + 768, oa = osc + NN_WAVES_MAX * 512;
+        fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
+        if (threadIdx.x >= 64) {   // the waves without a frame: constants and fragments to LDS
+            {   // every line of the kernel arguments into the scalar cache (invalidated at
+                // each launch), a few lines per wave, ahead of the NN's dependent reads
+                typedef const uint32_t __attribute__((address_space(4))) * kptr;
+                const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+                constexpr int NL = (int)((sizeof(FeArgs) + sizeof(NnImage) + sizeof(NnRun) + 127) / 64);
+                const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 1;
+                uint32_t x = 0;
+                for (int k = w; k < NL; k += NN_WAVES_MAX - 1) x ^= ka[16 * k];
+                asm volatile("" ::"s"(x));
+            }
+            // every segment's first share in flight together (one round trip
+            // for ~56 KB), the rest (nets wider than the reference's) after
+            constexpr int NT = 64 * (NN_WAVES_MAX - 1), U = 16;
+            const int t = (int)threadIdx.x - 64;
+            const int nw = r.st_rows / 4, nz = r.st_rows / 8, na = r.st_abytes / 16;
+            int4* dw = reinterpret_cast<int4*>(di_lds + ob);
+            int4* dr = reinterpret_cast<int4*>(di_lds + ow);
+            int4* dz = reinterpret_cast<int4*>(di_lds + oz);
+            int4* da = reinterpret_cast<int4*>(di_lds + oa);
+            const int4* sw = reinterpret_cast<const int4*>(img.wsum);
+            const int4* sr = reinterpret_cast<const int4*>(img.wsum_r);
+            const int4* sz = reinterpret_cast<const int4*>(img.bias);
+            const int4* sa = reinterpret_cast<const int4*>(img.A + r.st_alo);
+            // (clamped indexes: every load unconditional, into registers;
+            // rows >= 16 and the image's A >= 1 KiB, so index 0 exists)
+            const int4 cw = sw[min(t, nw - 1)], cr = sr[min(t, nw - 1)], cz = sz[min(t, nz - 1)];
+            const int16_t ct = nnsp_tbl_tanh[min(t, 383)];
+            int4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[u] = sa[min(t + NT * u, max(na - 1, 0))];
+            if (t < nw) {
+                dw[t] = cw;
+                dr[t] = cr;
+            }
+            if (t < nz) dz[t] = cz;
+            if (t < 384) reinterpret_cast<int16_t*>(di_lds + ot)[t] = ct;
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (t + NT * u < na) da[t + NT * u] = v[u];
+            lds_fill<U, NT>(dw, sw, nw, NT + t);
+            lds_fill<U, NT>(dr, sr, nw, NT + t);
+            lds_fill<U, NT>(dz, sz, nz, NT + t);
+            lds_fill<U, NT>(da, sa, na, NT * U + t);
+            if (NNSP_PROBES && r.probe) DI_CLK_T(12, 64);
+        }
+        __syncthreads();
+        DI_CLK(1);
+        NnRun q = r;
+        q.feats = reinterpret_cast<const int16_t*>(rb(r.feats));
+        q.prev5 = reinterpret_cast<const int16_t*>(rb(r.prev5));
+        q.h = reinterpret_cast<int16_t*>(rb(r.h));
+        q.c = reinterpret_cast<int32_t*>(rb(r.c));
+        q.post = rb(r.post);
+        q.trig = reinterpret_cast<int16_t*>(rb(r.trig));
+        q.out_src = rb(r.out_src);
+        // (32-bit LDS addresses: NnImage.A offset st_alo lands on the copy's first byte)
+        nn_body<true>(img, q, reinterpret_cast<const int32_t*>(di_lds + ob), reinterpret_cast<const int32_t*>(di_lds + ow),
+                      reinterpret_cast<const int16_t*>(di_lds + oz), di_lds + oa - r.st_alo,
+                      reinterpret_cast<const int16_t*>(di_lds + ot), reinterpret_cast<int32_t*>(di_lds + osc));
+    }
 }
 
 // prev5 := last 5 frames of V = prev5 ++ feats[b..T) after the segment; one
@@ -1845,6 +2186,14 @@ __global__ void k_synth_pcm(int16_t* out, int S, int T, unsigned long long seed,
 template <bool PORT>
 __global__ __launch_bounds__(256) void fe_tables_build_kernel(FeTables* out, FeArgs a) {
     fe_tables_init<PORT>(*out, a);
+    if (threadIdx.x < 64) {
+        FeLane L;
+        fe_lane_init(L, threadIdx.x);
+        FeLaneImg* li = reinterpret_cast<FeLaneImg*>(out + 1);
+        li->mj0[threadIdx.x] = L.mj0;
+        li->mfirst[threadIdx.x] = L.mfirst;
+        li->mcnt[threadIdx.x] = L.mcnt;
+    }
 }
 
 // ============================================================================
@@ -1857,7 +2206,7 @@ extern "C" {
 int nnspk_build_fe_tables(void** out, const FeArgs* a, void* stream) {
     *out = nullptr;
     FeTables* t = nullptr;
-    hipError_t e = hipMalloc((void**)&t, sizeof(FeTables));
+    hipError_t e = hipMalloc((void**)&t, sizeof(FeTables) + sizeof(FeLaneImg));
     if (e != hipSuccess) return (int)e;
     if (a->port)
         hipLaunchKernelGGL(fe_tables_build_kernel<true>, dim3(1), dim3(256), 0, (hipStream_t)stream, t, *a);
@@ -1982,10 +2331,69 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
 int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, void* stream) {
     if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
     if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
+    if (r->st_bytes <= 0) {
+        if (a->port)
+            hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+        else
+            hipLaunchKernelGGL((dropin_kernel<false, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+        return ok(hipGetLastError());
+    }
+    // out of LDS: the image, the constants, and the A fragments of as many
+    // trailing layers as fit beside the kernel's static LDS
+    static size_t lds_static[2] = {0, 0};
+    const void* fn = a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true>)
+                             : reinterpret_cast<const void*>(dropin_kernel<false, true>);
+    if (!lds_static[a->port ? 1 : 0]) {
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, fn);
+        if (e != hipSuccess) return ok(e);
+        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
+        if (e != hipSuccess) return ok(e);
+        lds_static[a->port ? 1 : 0] = fa.sharedSizeBytes;
+    }
+    if (!a->in_dst || !a->in_bytes || !r->out_bytes || (r->st_bytes & 15) || a->in_bytes > r->st_bytes)
+        return ok(hipErrorInvalidValue);
+    NnRun rr = *r;
+    rr.st_base = a->in_dst;
+    int rows = 0;
+    for (int i = 0; i < img->nl; ++i) {
+        const int e = img->L[i].ep_off + 16 * img->L[i].nrt;
+        rows = e > rows ? e : rows;
+    }
+    const size_t cap = 160 * 1024 - lds_static[a->port ? 1 : 0];
+    // rows: multiples of 16; the tanh table; the LSTM scratch
+    const size_t fixed = (size_t)r->st_bytes + 10 * (size_t)rows + 768 + NN_WAVES_MAX * 512;
+    if (fixed > cap) return ok(hipErrorInvalidValue);
+    // the smallest first layer whose fragments through the last layer's fit
+    int first = r->nl_run;
+    int64_t lo = 0, hi = 0;
+    for (int f = r->nl_run - 1; f >= 0; --f) {
+        int64_t l = INT64_MAX, h = 0;
+        for (int i = f; i < r->nl_run; ++i) {
+            const NnLayer& L = img->L[i];
+            const int64_t e = L.a_off + (int64_t)L.nrt * L.nkt * 1024;
+            l = L.a_off < l ? L.a_off : l;
+            h = e > h ? e : h;
+            if (L.type == NN_LSTM) {
+                const int64_t er = L.ar_off + (int64_t)L.nrt * L.nkt_r * 1024;
+                l = L.ar_off < l ? L.ar_off : l;
+                h = er > h ? er : h;
+            }
+        }
+        if (fixed + (size_t)(h - l) > cap) break;
+        first = f;
+        lo = l;
+        hi = h;
+    }
+    rr.st_rows = rows;
+    rr.st_first = first;
+    rr.st_alo = lo;
+    rr.st_abytes = (int32_t)(hi - lo);   // (a_off: multiples of 1 KiB)
+    const size_t dyn = fixed + (size_t)(hi - lo);
     if (a->port)
-        hipLaunchKernelGGL(dropin_kernel<true>, dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+        hipLaunchKernelGGL((dropin_kernel<true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr);
     else
-        hipLaunchKernelGGL(dropin_kernel<false>, dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+        hipLaunchKernelGGL((dropin_kernel<false, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr);
     return ok(hipGetLastError());
 }
 

@@ -16,7 +16,7 @@ import oracle as O
 from oracle import OracleNet, synthetic_pcm
 
 from nnsp_amd import _lib
-from nnsp_amd.nets import synth_net
+from nnsp_amd.nets import GEN_SPECS, LSTM, synth_net
 
 pytestmark = pytest.mark.gpu
 
@@ -239,3 +239,69 @@ def test_nnsp_exec_interleaved_nets():
             assert trig == ref[k][0][0, t], f"{name} frame {t}"
             ctx5 = np.ctypeslib.as_array(feat.normFeatContext)[200:240]
             np.testing.assert_array_equal(ctx5, ref[k][2][0, t], err_msg=f"{name} features frame {t}")
+
+
+def _oracle_hc(row):
+    """Every LSTM's h / c in the oracle's stream state (or_stream,
+    oracle/nnsp_oracle.h: buf[480], ctx[240] int16, then h[10][304] int16 and
+    c[10][304] int32, indexed by LSTM count)"""
+    h = np.frombuffer(row.tobytes(), np.int16, count=10 * 304, offset=1440).reshape(10, 304)
+    c = np.frombuffer(row.tobytes(), np.int32, count=10 * 304, offset=1440 + 6080).reshape(10, 304)
+    return h, c
+
+
+@pytest.mark.parametrize("name", list(GEN_SPECS))
+def test_nnsp_exec_generic_nets(name):
+    """NNSPClass_exec -- the drop-in kernel: the call out of LDS, one stream's
+    epilogues spread over lanes, LSTM row tiles in rounds of four, weights that
+    do not fit LDS read from memory -- on shapes past the reference's nets: rows
+    not a multiple of 4, two and three LSTMs, 256- and 300-wide layers, mixed
+    accumulators, a linear layer inside the stack.  Per frame: the trigger,
+    context slot 5 and every LSTM's h / c against the oracle's."""
+    data = synth_net(name, 8)
+    spec = data.spec
+    orc = OracleNet(data, thresh_prob=3000, th_count=1)
+    h = _lib.NetHandle(data)
+    feat, inst = _lib.FeatureClass(), _lib.NNSPClass()
+    thr, cnt = np.array([3000], np.int16), np.array([1], np.int16)
+    _KEEP.extend([h, feat, inst, thr, cnt])
+    assert L().NNSPClass_init(C.byref(inst), C.c_void_p(h.addr), C.byref(feat), bytes([spec.nn_id]), vp(h.mean),
+                              vp(h.stdR), vp(thr), vp(cnt)) == 0
+    L().NNSPClass_reset(C.byref(inst))
+    T = 9
+    pcm = synthetic_pcm(1, T, seed=123)
+    st = orc.new_states(1)
+    lstm = [i for i, ty in enumerate(spec.types) if ty == LSTM]   # (midlin has none: the trigger only)
+    for t in range(T):
+        o_trig, _, o_feat, st = orc.run(pcm[:, t:t + 1], st)
+        frame = np.ascontiguousarray(pcm[0, t])
+        assert L().NNSPClass_exec(C.byref(inst), vp(frame)) == o_trig[0, 0], f"{name} frame {t}"
+        np.testing.assert_array_equal(np.ctypeslib.as_array(feat.normFeatContext)[200:240], o_feat[0, 0],
+                                      err_msg=f"{name} features frame {t}")
+        oh, oc = _oracle_hc(st[0])
+        for k, i in enumerate(lstm):
+            N = spec.sizes[i + 1]
+            np.testing.assert_array_equal(h.h[i], oh[k, :N], err_msg=f"{name} LSTM {i} h, frame {t}")
+            np.testing.assert_array_equal(h.c[i], oc[k, :N], err_msg=f"{name} LSTM {i} c, frame {t}")
+    assert L().nnsp_legacy_status() == 0
+
+
+def test_nnsp_exec_memory_path():
+    """The drop-in kernel with its operands in device memory (NNSP_DROPIN_LDS=0,
+    read once per process: a child process) on the reference-shaped and the
+    generic nets, against the oracle as above."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    # (as conftest.py: torch first, so that its HIP runtime is the process's;
+    # the oracle directory ahead of the repository root)
+    code = ("import sys; import torch; sys.path[:0] = ['oracle', '.', 'tests']\n"
+            "import test_gpu_legacy as t\n"
+            "t.test_nnsp_exec_interleaved_nets()\n"
+            "for n in ('odd', 'lstm3', 'wide300'): t.test_nnsp_exec_generic_nets(n)\n"
+            "print('ok')\n")
+    env = dict(os.environ, NNSP_DROPIN_LDS="0")
+    out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout[-2000:] + out.stderr[-4000:]
