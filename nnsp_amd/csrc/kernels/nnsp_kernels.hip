@@ -112,6 +112,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pcm_rsrc(const int16_t* base) 
 
 struct FeLane {
     int mj0, mfirst, mcnt;   // Mel segment start bin; first segment and segment count of bank `lane`
+    int bank;                // the bank of segment `lane` (N_MEL = 40: no segment)
 };
 
 // Block-shared constant tables (LDS).
@@ -185,7 +186,7 @@ __device__ __forceinline__ void fe_tables_load(FeTables& T, const FeArgs& a) {
 // indexes (fe_lane_init's results), read with one vector load per field
 // instead of the 64-entry scan of nnsp_tbl_melseg (dependent scalar loads)
 struct FeLaneImg {
-    int32_t mj0[64], mfirst[64], mcnt[64];
+    int32_t mj0[64], mfirst[64], mcnt[64], bank[64];
 };
 
 template <bool PORT>
@@ -236,6 +237,7 @@ __device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int s, int lane) {
 
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
     L.mj0 = nnsp_tbl_melseg[4 * lane + 1];
+    L.bank = nnsp_tbl_melseg[4 * lane];
     L.mfirst = 0;
     L.mcnt = 0;
     for (int k = 0; k < 64; ++k) {
@@ -508,6 +510,7 @@ __device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr) {
         L.mj0 = lg->mj0[lane];
         L.mfirst = lg->mfirst[lane];
         L.mcnt = lg->mcnt[lane];
+        L.bank = lg->bank[lane];
         fe_tables_load<PORT>(TB, a);
     } else {   // (L derived after the tables: not live across their derivation)
         fe_tables_init<PORT>(TB, a);
@@ -751,33 +754,25 @@ __device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr) {
         }
         wave_lds_sync();
         FCLK(3);
-        // ---- Mel (melSpecProc.c:6-27): lane segments of <= FE_MEL_LEN MACs (zero-padded), then per bank
+        // ---- Mel (melSpecProc.c:6-27): lane segments of <= FE_MEL_LEN MACs
+        // (zero-padded), each added into its bank's sum with an LDS atomic
+        // (integer addition in any order equals the reference's sequential
+        // int64 sum): the tail then reads one sum per bank instead of adding
+        // up to FE_MEL_MAXSEG partial sums (address selects and 64-bit adds,
+        // ~8 VALU per frame).  The zeroing precedes the atomics in this wave's
+        // LDS order; slot 40 takes the lanes without a segment (adding 0).
         {
+            if (lane <= 40) Mp[lane] = 0;
             int64_t mac = 0;
 #pragma unroll
             for (int i = 0; i < FE_MEL_LEN; ++i) mac = mad_i64_i32((int32_t)TB.mc[i][lane], P[L.mj0 + i], mac);
-            Mp[lane] = mac;
+            atomicAdd(reinterpret_cast<unsigned long long*>(Mp) + L.bank, (unsigned long long)mac);
         }
         wave_lds_sync();
         FCLK(4);
         // ---- log10 (fixlog10.c:53-61), normalise (feature_module.c:67-73)
         if (lane < 40) {
-            // a bank spans at most FE_MEL_MAXSEG = 3 lane segments, lanes
-            // mfirst.. (tests/test_tables.py checks the table); a missing one
-            // reads lane 63's partial sum, which is zero (no segment there, also
-            // checked): three unconditional reads instead of masked adds
-            // (the shared mode of the shipped build; the other instantiations
-            // keep the masked adds: their registers are at the 80-VGPR limit)
-            static_assert(FE_MEL_MAXSEG == 3, "fe_kernel: bank sums of three segments");
-            int64_t mac;
-            if constexpr (shared && !PORT) {
-                mac = Mp[L.mfirst] + Mp[L.mcnt > 1 ? L.mfirst + 1 : 63] + Mp[L.mcnt > 2 ? L.mfirst + 2 : 63];
-            } else {
-                mac = 0;
-#pragma unroll
-                for (int k = 0; k < FE_MEL_MAXSEG; ++k)
-                    if (k < L.mcnt) mac += Mp[L.mfirst + k];
-            }
+            const int64_t mac = Mp[lane];   // bank `lane`'s sum
             const int32_t lg = log10_q15_lds(sat32_shr15(mac), TB.logp);
             if (MODE == FE_MODE_BATCH && (LI || a.dbg_log)) FE_P(dbg_log)[(size_t)fo * 40 + lane] = lg;
             if constexpr (shared) {
@@ -2193,6 +2188,7 @@ __global__ __launch_bounds__(256) void fe_tables_build_kernel(FeTables* out, FeA
         li->mj0[threadIdx.x] = L.mj0;
         li->mfirst[threadIdx.x] = L.mfirst;
         li->mcnt[threadIdx.x] = L.mcnt;
+        li->bank[threadIdx.x] = L.bank;
     }
 }
 
