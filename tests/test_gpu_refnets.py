@@ -57,6 +57,30 @@ def test_batch_reference_nets(name, acc32):
         assert (trig != 0).any(), "VAD never triggered on the recordings: vacuous"
 
 
+def test_cascade_vad_fused_prefix(monkeypatch):
+    """The fused prefix stage (opt-in NNSP_FUSE_PREFIX=2; measured slower than
+    the default): in the cascade's one-tile VAD recurrences, VAD's
+    FC 240 -> 28 and the LSTM's input projection run inside the recurrence on
+    its FC waves, one step ahead, instead of in proj_kernel.  Bit-exact against
+    the oracle like the default path."""
+    monkeypatch.setenv("NNSP_FUSE_PREFIX", "2")   # read by nnsp_batch_create; 2: refuse rather than fall back
+    S, chunks = 64, [100, 100, 57]
+    gnets = {n: NNSPBatch(ref_net(n), S, 100) for n in ("vad", "kws", "s2i")}
+    gc = NNSPCascade(gnets)
+    oc = OracleCascade({n: OracleNet(ref_net(n)) for n in ("vad", "kws", "s2i")})
+    st = oc.new_states(S)
+    pcm = _pcm(S, sum(chunks), every=1)
+    t0 = 0
+    for Tc in chunks:
+        o_ran, o_det, o_o3, st = oc.run(pcm[:, t0:t0 + Tc], st)
+        g_ran, g_det, g_o3 = gc.exec(pcm[:, t0:t0 + Tc])
+        np.testing.assert_array_equal(g_ran, o_ran, err_msg=f"net_ran chunk@{t0}")
+        np.testing.assert_array_equal(g_det, o_det, err_msg=f"detected chunk@{t0}")
+        np.testing.assert_array_equal(g_o3, o_o3, err_msg=f"outputs3 chunk@{t0}")
+        t0 += Tc
+    gc.close()
+
+
 @pytest.mark.parametrize("name", list(GEN_SPECS))
 def test_batch_n3_shapes(name):
     """Rows not a multiple of 4, odd K, 3 / 7 layers, two LSTMs, a 256-wide FC
