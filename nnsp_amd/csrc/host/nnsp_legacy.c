@@ -56,6 +56,9 @@ static struct {
     /* NNSP_DROPIN_LDS (default 1): the drop-in kernel runs the call out of LDS
      * (inputs copied in there, weights staged beside them; NnRun.st_bytes) */
     int lds;
+    /* NNSP_DROPIN_KARG (default 1, with NNSP_DROPIN_LDS): the inputs travel in the
+     * kernel arguments (device memory) instead of being read from mapped host memory */
+    int karg;
     int probe;      /* NNSP_DROPIN_PROBE=1 (PROBES builds): the drop-in kernel's phase clocks, nnsp_dropin_probes */
     uint32_t seq;
     void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
@@ -129,6 +132,8 @@ static int gctx(void)
         G.probe = pb && atoi(pb) != 0;
         const char *ld = getenv("NNSP_DROPIN_LDS");
         G.lds = !ld || atoi(ld) != 0;
+        const char *ka = getenv("NNSP_DROPIN_KARG");
+        G.karg = !ka || atoi(ka) != 0;
     }
     if (!G.copy && (e = nnspk_host_alloc_mapped((void **)&G.hmap, (void **)&G.hmap_dev, G.hpin_cap))) return e;
     G.ready = 1;
@@ -1068,7 +1073,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         CK(nnspk_launch_nn(&img, &r, G.stream));
         CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
     } else {   /* the front end and the NN in one launch */
-        CK(nnspk_launch_dropin(&a, &img, &r, G.stream));
+        CK(nnspk_launch_dropin(&a, &img, &r, G.lds && G.karg ? hp : NULL, G.stream));
     }
     if (G.probe) hc[3] = host_ns();
     if (!G.copy && G.wait == 2)

@@ -272,7 +272,10 @@ int nnspk_launch_nring_fill(int16_t *const nring[3], const int32_t *const nmean[
 int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
 /* the drop-in call's front end (FE_MODE_BATCH, one stream, one frame) and NN
  * (NN_MODE_STREAM, T = 1) in one launch */
-int nnspk_launch_dropin(const FeArgs *a, const NnImage *img, const NnRun *r, void *stream);
+/* kin (NULL: none): a host copy of the call's in_bytes of inputs, passed in the
+ * kernel arguments when they fit NNSP_DROPIN_KARG_BYTES (the LDS path only) */
+#define NNSP_DROPIN_KARG_BYTES 2176
+int nnspk_launch_dropin(const FeArgs *a, const NnImage *img, const NnRun *r, const void *kin, void *stream);
 int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
                           int n_list, const int32_t *seg_begin, int seg_len, void *stream);
 int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, const int32_t *list,

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include "nnsp_dev.h"
 // development probes (s_memtime per phase): compiled in only with -DNNSP_PROBES=1
@@ -437,7 +438,7 @@ __device__ __forceinline__ void wave_split_dc(const int32_t* X, int32_t& dc, int
 // copied to (one stream, one frame: no history)
 // IN: the drop-in call's inputs are copied in first (FeArgs.in_bytes)
 template <int MODE, bool PORT, int WPG, bool LI = false, bool IN = LI>
-__device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr) {
+__device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr, const int4* ksrc = nullptr) {
     // per wave: the cFFT buffer X (256 complex) and, right behind it, the
     // power spectrum P (257 used; +pad for branch-free Mel reads) -- X and P
     // contiguous so that the padded T1 transpose may use both
@@ -499,7 +500,9 @@ __device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr) {
     // the inputs' first two shares, the lanes' Mel indexes and the tables:
     // every load in flight before the first store (one memory latency)
     const int nin = IN ? a.in_bytes / 16 : 0, nt = (int)blockDim.x, tid = (int)threadIdx.x;
-    const int4* const isrc = reinterpret_cast<const int4*>(a.in_src);
+    // (ksrc: the inputs passed in the kernel arguments, which the launch
+    // writes to device memory -- read from there instead of across PCIe)
+    const int4* const isrc = ksrc ? ksrc : reinterpret_cast<const int4*>(a.in_src);
     int4* const idst = reinterpret_cast<int4*>(LI ? li : a.in_dst);
     int4 iv0 = make_int4(0, 0, 0, 0), iv1 = make_int4(0, 0, 0, 0);
     if (tid < nin) iv0 = isrc[tid];
@@ -1553,8 +1556,19 @@ __device__ __forceinline__ void lds_fill(int4* d, const int4* s, int n, int i0) 
     }
 }
 
-template <bool PORT, bool ST>
-__global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r) {
+// the drop-in call's inputs in the kernel arguments (KI): the launch writes
+// them to device memory with the rest of the arguments, so that the kernel
+// reads them from there instead of from mapped host memory across PCIe
+template <bool KI>
+struct DropinKin {
+    int32_t unused;
+};
+template <>
+struct DropinKin<true> {
+    int4 b[NNSP_DROPIN_KARG_BYTES / 16];
+};
+template <bool PORT, bool ST, bool KI = false>
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r, DropinKin<KI> kin) {
 #if NNSP_PROBES
     if (r.probe && threadIdx.x < NNSP_PROBE_LONGS) di_clk[threadIdx.x] = 0;   // (wave 0's own slots first)
 #endif
@@ -1578,7 +1592,10 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnI
         // the activation table (384 int16) | the LSTM's per-wave scratch (2 x 64 int32) | A fragments
         const int ob = r.st_bytes, ow = ob + 4 * r.st_rows, oz = ow + 4 * r.st_rows, ot = oz + 2 * r.st_rows,
                   osc = ot + 768, oa = osc + NN_WAVES_MAX * 512;
-        fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
+        if constexpr (KI)
+            fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds, kin.b);
+        else
+            fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
         if (threadIdx.x >= 64) {   // the waves without a frame: constants and fragments to LDS
             {   // every line of the kernel arguments into the scalar cache (invalidated at
                 // each launch), a few lines per wave, ahead of the NN's dependent reads
@@ -2324,28 +2341,34 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, void* stream) {
+int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, const void* kin, void* stream) {
     if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
     if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
+    const DropinKin<false> k0 = {0};
     if (r->st_bytes <= 0) {
         if (a->port)
-            hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+            hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
         else
-            hipLaunchKernelGGL((dropin_kernel<false, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r);
+            hipLaunchKernelGGL((dropin_kernel<false, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
         return ok(hipGetLastError());
     }
     // out of LDS: the image, the constants, and the A fragments of as many
     // trailing layers as fit beside the kernel's static LDS
-    static size_t lds_static[2] = {0, 0};
-    const void* fn = a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true>)
-                             : reinterpret_cast<const void*>(dropin_kernel<false, true>);
-    if (!lds_static[a->port ? 1 : 0]) {
+    // (KI: the inputs in the kernel arguments when they fit)
+    const int ki = kin && a->in_bytes <= NNSP_DROPIN_KARG_BYTES;
+    static size_t lds_static[4] = {0, 0, 0, 0};
+    const int fx = (a->port ? 1 : 0) + (ki ? 2 : 0);
+    if (!lds_static[fx]) {
+        const void* fn = ki ? (a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true, true>)
+                                       : reinterpret_cast<const void*>(dropin_kernel<false, true, true>))
+                            : (a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true>)
+                                       : reinterpret_cast<const void*>(dropin_kernel<false, true>));
         hipFuncAttributes fa;
         hipError_t e = hipFuncGetAttributes(&fa, fn);
         if (e != hipSuccess) return ok(e);
         e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
         if (e != hipSuccess) return ok(e);
-        lds_static[a->port ? 1 : 0] = fa.sharedSizeBytes;
+        lds_static[fx] = fa.sharedSizeBytes;
     }
     if (!a->in_dst || !a->in_bytes || !r->out_bytes || (r->st_bytes & 15) || a->in_bytes > r->st_bytes)
         return ok(hipErrorInvalidValue);
@@ -2356,7 +2379,7 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, voi
         const int e = img->L[i].ep_off + 16 * img->L[i].nrt;
         rows = e > rows ? e : rows;
     }
-    const size_t cap = 160 * 1024 - lds_static[a->port ? 1 : 0];
+    const size_t cap = 160 * 1024 - lds_static[fx];
     // rows: multiples of 16; the tanh table; the LSTM scratch
     const size_t fixed = (size_t)r->st_bytes + 10 * (size_t)rows + 768 + NN_WAVES_MAX * 512;
     if (fixed > cap) return ok(hipErrorInvalidValue);
@@ -2386,10 +2409,18 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, voi
     rr.st_alo = lo;
     rr.st_abytes = (int32_t)(hi - lo);   // (a_off: multiples of 1 KiB)
     const size_t dyn = fixed + (size_t)(hi - lo);
-    if (a->port)
-        hipLaunchKernelGGL((dropin_kernel<true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr);
-    else
-        hipLaunchKernelGGL((dropin_kernel<false, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr);
+    if (ki) {
+        DropinKin<true> k;
+        memcpy(k.b, kin, (size_t)a->in_bytes);
+        if (a->port)
+            hipLaunchKernelGGL((dropin_kernel<true, true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k);
+        else
+            hipLaunchKernelGGL((dropin_kernel<false, true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k);
+    } else if (a->port) {
+        hipLaunchKernelGGL((dropin_kernel<true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k0);
+    } else {
+        hipLaunchKernelGGL((dropin_kernel<false, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k0);
+    }
     return ok(hipGetLastError());
 }
 
