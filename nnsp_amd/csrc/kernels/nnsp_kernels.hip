@@ -113,7 +113,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t pcm_rsrc(const int16_t* base) 
 
 struct FeLane {
     int mj0, mfirst, mcnt;   // Mel segment start bin; first segment and segment count of bank `lane`
-    int bank;                // the bank of segment `lane` (N_MEL = 40: no segment)
 };
 
 // Block-shared constant tables (LDS).
@@ -129,6 +128,8 @@ struct FeTables {
     int16_t mc[FE_MEL_LEN][64];   // per lane: its Mel segment's coefficients, zero-padded, read with
                           // sign-extending ds_read_i16 (no VALU unpacking; LDS, not VGPRs:
                           // keeps fe_kernel at 80 VGPRs, six waves per SIMD)
+    int8_t bank[64];      // per lane: the bank of its Mel segment (N_MEL = 40: none), read per frame (a
+                          // VGPR held across the frame loop cost the batch mode a spill)
 };   // 27 KB with fe_kernel's buffers: six workgroups fit the CU's 160 KB
 static_assert(sizeof(FeTables) % 16 == 0, "FeTables: copied as 16-byte chunks");
 // fe_kernel's LDS (the tables + FE_WPG frame buffers), granted in 512-byte
@@ -187,7 +188,7 @@ __device__ __forceinline__ void fe_tables_load(FeTables& T, const FeArgs& a) {
 // indexes (fe_lane_init's results), read with one vector load per field
 // instead of the 64-entry scan of nnsp_tbl_melseg (dependent scalar loads)
 struct FeLaneImg {
-    int32_t mj0[64], mfirst[64], mcnt[64], bank[64];
+    int32_t mj0[64], mfirst[64], mcnt[64];
 };
 
 template <bool PORT>
@@ -226,6 +227,7 @@ __device__ __forceinline__ void fe_tables_init(FeTables& T, const FeArgs& a) {
         const int mn = sg[2];
         for (int i = 0; i < FE_MEL_LEN; ++i) T.mc[i][lane] = (int16_t)(i < mn ? nnsp_tbl_mel[sg[3] + i] : 0);
         T.win[lane] = make_uint4(w[0], w[1], w[2], w[3]);
+        T.bank[lane] = (int8_t)sg[0];
     }
 }
 
@@ -238,7 +240,6 @@ __device__ __forceinline__ Tw3 lds_tw3(const FeTables& T, int s, int lane) {
 
 __device__ __forceinline__ void fe_lane_init(FeLane& L, int lane) {
     L.mj0 = nnsp_tbl_melseg[4 * lane + 1];
-    L.bank = nnsp_tbl_melseg[4 * lane];
     L.mfirst = 0;
     L.mcnt = 0;
     for (int k = 0; k < 64; ++k) {
@@ -513,7 +514,6 @@ __device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr, const i
         L.mj0 = lg->mj0[lane];
         L.mfirst = lg->mfirst[lane];
         L.mcnt = lg->mcnt[lane];
-        L.bank = lg->bank[lane];
         fe_tables_load<PORT>(TB, a);
     } else {   // (L derived after the tables: not live across their derivation)
         fe_tables_init<PORT>(TB, a);
@@ -769,7 +769,7 @@ __device__ __forceinline__ void fe_body(FeArgs a, uint8_t* li = nullptr, const i
             int64_t mac = 0;
 #pragma unroll
             for (int i = 0; i < FE_MEL_LEN; ++i) mac = mad_i64_i32((int32_t)TB.mc[i][lane], P[L.mj0 + i], mac);
-            atomicAdd(reinterpret_cast<unsigned long long*>(Mp) + L.bank, (unsigned long long)mac);
+            atomicAdd(reinterpret_cast<unsigned long long*>(Mp) + TB.bank[lane], (unsigned long long)mac);
         }
         wave_lds_sync();
         FCLK(4);
@@ -2205,7 +2205,6 @@ __global__ __launch_bounds__(256) void fe_tables_build_kernel(FeTables* out, FeA
         li->mj0[threadIdx.x] = L.mj0;
         li->mfirst[threadIdx.x] = L.mfirst;
         li->mcnt[threadIdx.x] = L.mcnt;
-        li->bank[threadIdx.x] = L.bank;
     }
 }
 

@@ -1,0 +1,16 @@
+#!/bin/bash
+# round 6: drop-in staging loads issued before the front end -- parity (required), clocks, latency x3
+set -o pipefail
+O=gpurun_out/r06/${TAG:-g21}; mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_legacy.py tests/test_gpu_legacy_portable.py tests/test_gpu_nnsp_e2e.py tests/test_gpu_refnets.py > $O/pytest_req.log 2>&1 || { echo "pytest (required) failed"; tail -40 $O/pytest_req.log; exit 1; }
+tail -1 $O/pytest_req.log
+NNSP_LIB=abtest/p6/nnsp_amd/libnnsp_mi355x.so timeout -k 10 120 python profiles/r06/dropin_probe.py > $O/probe.txt 2>&1 || { echo "probe failed"; tail -20 $O/probe.txt; exit 1; }
+grep -v "^   L" $O/probe.txt
+for rep in 1 2 3; do
+  timeout -k 10 200 python bench.py --dropin-latency > $O/lat_$rep.json 2> $O/lat_$rep.err || { echo "latency failed"; tail -20 $O/lat_$rep.err; exit 1; }
+  python -c "
+import json; d=json.loads(open('$O/lat_$rep.json').read().strip().split('\n')[-1])
+print('rep $rep', {k:(round(v['gpu_us_per_frame_median'],1), round(v['gpu_us_per_frame_p99'],1)) for k,v in d['nets'].items()})"
+done
+echo all-ok
