@@ -2344,7 +2344,16 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
     if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
     if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
     const DropinKin<false> k0 = {0};
-    if (r->st_bytes <= 0) {
+    // out of LDS when the image and every layer's constants fit beside the
+    // kernel's static LDS (a net of very many rows runs from device memory)
+    int rows = 0;
+    for (int i = 0; i < img->nl; ++i) {
+        const int e = img->L[i].ep_off + 16 * img->L[i].nrt;
+        rows = e > rows ? e : rows;
+    }
+    // rows: multiples of 16; the tanh table; the LSTM scratch
+    const size_t fixed = (size_t)(r->st_bytes > 0 ? r->st_bytes : 0) + 10 * (size_t)rows + 768 + NN_WAVES_MAX * 512;
+    if (r->st_bytes <= 0 || fixed > 160 * 1024 - 56 * 1024) {   // (the LDS kernels' static LDS is < 56 KB)
         if (a->port)
             hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
         else
@@ -2373,15 +2382,8 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
         return ok(hipErrorInvalidValue);
     NnRun rr = *r;
     rr.st_base = a->in_dst;
-    int rows = 0;
-    for (int i = 0; i < img->nl; ++i) {
-        const int e = img->L[i].ep_off + 16 * img->L[i].nrt;
-        rows = e > rows ? e : rows;
-    }
     const size_t cap = 160 * 1024 - lds_static[fx];
-    // rows: multiples of 16; the tanh table; the LSTM scratch
-    const size_t fixed = (size_t)r->st_bytes + 10 * (size_t)rows + 768 + NN_WAVES_MAX * 512;
-    if (fixed > cap) return ok(hipErrorInvalidValue);
+    if (fixed > cap) return ok(hipErrorInvalidValue);   // (checked against a bound above)
     // the smallest first layer whose fragments through the last layer's fit
     int first = r->nl_run;
     int64_t lo = 0, hi = 0;
