@@ -1368,7 +1368,9 @@ __device__ __forceinline__ void lstm_layer_one(const uint8_t* Ab, const int32_t*
 // layers from r.st_first on read their A fragments there too (Ast: NnImage.A's
 // offsets rebased onto the LDS copy) -- the layer code inlined once per
 // operand address space, so that each copy reads LDS or global memory directly
-template <bool DI>
+// (ALLST: every layer's fragments in LDS, the global copy not compiled -- its
+// uniform values no longer crowd the scalar registers of the prologue)
+template <bool DI, bool ALLST = false>
 __device__ __forceinline__ void nn_body(const NnImage& img, NnRun r, const int32_t* ws, const int32_t* wsr,
                                         const int16_t* bs, const uint8_t* Ast, const int16_t* ttab = nullptr,
                                         int32_t* scr = nullptr) {
@@ -1396,7 +1398,9 @@ __device__ __forceinline__ void nn_body(const NnImage& img, NnRun r, const int32
     // first barrier passed, [8] the context staged, [9] the context barrier passed)
     if (DI && img.nl <= 5) DI_CLK(7);
     const int phase = r.mode == NN_MODE_DIRECT ? 0 : 1 - sm.slides[sc];
-    const int T = r.mode == NN_MODE_DIRECT ? 1 : r.T;
+    // (DI: one frame, T == 1 checked at the launch -- the step loop known to
+    // run once, so that nothing is hoisted out of it)
+    const int T = DI || r.mode == NN_MODE_DIRECT ? 1 : r.T;
     const int nsteps = (T + 1) / 2;
     const int nl = r.nl_run;
     if (w0 && lane < 16 && valid && phase == 1 && r.trig) r.trig[(size_t)s * T] = ps.trigger;
@@ -1448,7 +1452,7 @@ __device__ __forceinline__ void nn_body(const NnImage& img, NnRun r, const int32
                 // (DI: every lane works for stream 0 -- its cell row and its activity)
                 int32_t* cg = DI ? r.c + (size_t)lst * hs : (valid ? r.c + ((size_t)s * img.n_lstm + lst) * hs : nullptr);
                 const bool commit = DI ? sm.active[0] != 0 : active;
-                if (DI && i >= r.st_first)
+                if (DI && (ALLST || i >= r.st_first))
                     lstm_layer_one(Ast, ws, wsr, bs, Ly, in, out, &sm.h[0][0], cg, tt, scr + 128 * wv, lane, commit,
                                    wv, nwv, NNSP_PROBES && r.probe && i < 8 ? 16 + 8 * i : -1);
                 else if (DI)
@@ -1464,7 +1468,7 @@ __device__ __forceinline__ void nn_body(const NnImage& img, NnRun r, const int32
                 }
                 ++lst;
             } else {
-                if (DI && i >= r.st_first)
+                if (DI && (ALLST || i >= r.st_first))
                     fc_layer_mfma<DI>(Ast, ws, bs, Ly, in, out, tt, lane, wv, nwv,
                                   NNSP_PROBES && r.probe && i < 8 ? 16 + 8 * i : -1);
                 else
@@ -1567,7 +1571,7 @@ template <>
 struct DropinKin<true> {
     int4 b[NNSP_DROPIN_KARG_BYTES / 16];
 };
-template <bool PORT, bool ST, bool KI = false>
+template <bool PORT, bool ST, bool KI = false, bool ALLST = false>
 __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r, DropinKin<KI> kin) {
 #if NNSP_PROBES
     if (r.probe && threadIdx.x < NNSP_PROBE_LONGS) di_clk[threadIdx.x] = 0;   // (wave 0's own slots first)
@@ -1653,7 +1657,7 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnI
         q.trig = reinterpret_cast<int16_t*>(rb(r.trig));
         q.out_src = rb(r.out_src);
         // (32-bit LDS addresses: NnImage.A offset st_alo lands on the copy's first byte)
-        nn_body<true>(img, q, reinterpret_cast<const int32_t*>(di_lds + ob), reinterpret_cast<const int32_t*>(di_lds + ow),
+        nn_body<true, ALLST>(img, q, reinterpret_cast<const int32_t*>(di_lds + ob), reinterpret_cast<const int32_t*>(di_lds + ow),
                       reinterpret_cast<const int16_t*>(di_lds + oz), di_lds + oa - r.st_alo,
                       reinterpret_cast<const int16_t*>(di_lds + ot), reinterpret_cast<int32_t*>(di_lds + osc));
     }
@@ -2363,26 +2367,29 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
     // out of LDS: the image, the constants, and the A fragments of as many
     // trailing layers as fit beside the kernel's static LDS
     // (KI: the inputs in the kernel arguments when they fit)
-    const int ki = kin && a->in_bytes <= NNSP_DROPIN_KARG_BYTES;
-    static size_t lds_static[4] = {0, 0, 0, 0};
-    const int fx = (a->port ? 1 : 0) + (ki ? 2 : 0);
-    if (!lds_static[fx]) {
-        const void* fn = ki ? (a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true, true>)
-                                       : reinterpret_cast<const void*>(dropin_kernel<false, true, true>))
-                            : (a->port ? reinterpret_cast<const void*>(dropin_kernel<true, true>)
-                                       : reinterpret_cast<const void*>(dropin_kernel<false, true>));
-        hipFuncAttributes fa;
-        hipError_t e = hipFuncGetAttributes(&fa, fn);
-        if (e != hipSuccess) return ok(e);
-        e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
-        if (e != hipSuccess) return ok(e);
-        lds_static[fx] = fa.sharedSizeBytes;
-    }
     if (!a->in_dst || !a->in_bytes || !r->out_bytes || (r->st_bytes & 15) || a->in_bytes > r->st_bytes)
         return ok(hipErrorInvalidValue);
-    NnRun rr = *r;
-    rr.st_base = a->in_dst;
-    const size_t cap = 160 * 1024 - lds_static[fx];
+    // the variants: port + 2 KI (the inputs in the kernel arguments when they
+    // fit) + 4 ALLST (every layer's fragments in LDS); one static LDS size
+    static const void* const fns[8] = {
+        reinterpret_cast<const void*>(dropin_kernel<false, true, false, false>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, false, false>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, true, false>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, true, false>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, false, true>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, false, true>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, true, true>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, true, true>)};
+    static size_t lds_static[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (!lds_static[0]) {
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, fns[0]);
+        if (e != hipSuccess) return ok(e);
+        lds_static[0] = fa.sharedSizeBytes;
+        e = hipFuncSetAttribute(fns[0], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
+        if (e != hipSuccess) return ok(e);
+    }
+    const size_t cap = 160 * 1024 - lds_static[0];
     if (fixed > cap) return ok(hipErrorInvalidValue);   // (checked against a bound above)
     // the smallest first layer whose fragments through the last layer's fit
     int first = r->nl_run;
@@ -2405,23 +2412,45 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
         lo = l;
         hi = h;
     }
+    const int ki = kin && a->in_bytes <= NNSP_DROPIN_KARG_BYTES;
+    const int fx = (a->port ? 1 : 0) + (ki ? 2 : 0) + (first == 0 ? 4 : 0);
+    if (!lds_static[fx]) {
+        hipFuncAttributes fa;
+        hipError_t e = hipFuncGetAttributes(&fa, fns[fx]);
+        if (e != hipSuccess) return ok(e);
+        if (fa.sharedSizeBytes != lds_static[0]) return ok(hipErrorInvalidValue);
+        e = hipFuncSetAttribute(fns[fx], hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
+        if (e != hipSuccess) return ok(e);
+        lds_static[fx] = fa.sharedSizeBytes;
+    }
+    NnRun rr = *r;
+    rr.st_base = a->in_dst;
     rr.st_rows = rows;
     rr.st_first = first;
     rr.st_alo = lo;
     rr.st_abytes = (int32_t)(hi - lo);   // (a_off: multiples of 1 KiB)
     const size_t dyn = fixed + (size_t)(hi - lo);
+#define NNSP_DI_LAUNCH(P, K, AL, KARG)                                                                              \
+    hipLaunchKernelGGL((dropin_kernel<P, true, K, AL>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, \
+                       *a, *img, rr, KARG)
     if (ki) {
         DropinKin<true> k;
         memcpy(k.b, kin, (size_t)a->in_bytes);
-        if (a->port)
-            hipLaunchKernelGGL((dropin_kernel<true, true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k);
-        else
-            hipLaunchKernelGGL((dropin_kernel<false, true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k);
-    } else if (a->port) {
-        hipLaunchKernelGGL((dropin_kernel<true, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k0);
+        switch (fx) {
+        case 2: NNSP_DI_LAUNCH(false, true, false, k); break;
+        case 3: NNSP_DI_LAUNCH(true, true, false, k); break;
+        case 6: NNSP_DI_LAUNCH(false, true, true, k); break;
+        default: NNSP_DI_LAUNCH(true, true, true, k); break;
+        }
     } else {
-        hipLaunchKernelGGL((dropin_kernel<false, true>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, *a, *img, rr, k0);
+        switch (fx) {
+        case 0: NNSP_DI_LAUNCH(false, false, false, k0); break;
+        case 1: NNSP_DI_LAUNCH(true, false, false, k0); break;
+        case 4: NNSP_DI_LAUNCH(false, false, true, k0); break;
+        default: NNSP_DI_LAUNCH(true, false, true, k0); break;
+        }
     }
+#undef NNSP_DI_LAUNCH
     return ok(hipGetLastError());
 }
 
