@@ -29,6 +29,7 @@
  * the old one is freed at the start of the next call, once nothing in flight
  * uses it), and the sticky error of the last failed call
  * ------------------------------------------------------------------------- */
+#define NNSP_WORKERS 4
 static struct {
     void *stream;
     uint8_t *arena;
@@ -60,9 +61,24 @@ static struct {
      * kernel arguments (device memory) instead of being read from mapped host memory */
     int karg;
     int probe;      /* NNSP_DROPIN_PROBE=1 (PROBES builds): the drop-in kernel's phase clocks, nnsp_dropin_probes */
+    /* NNSP_DROPIN_WORKER (default 1, with NNSP_DROPIN_LDS and the completion
+     * word): calls go to a resident worker workgroup that keeps the net in LDS
+     * (dropin_worker_kernel) instead of one launch each; it leaves after
+     * NNSP_DROPIN_IDLE_MS (default 50) without a request */
+    int worker;
+    long long idle_ns;
+    struct dropin_worker {
+        void *stream;
+        FeArgs a;   /* the arguments it serves (r.done_seq 0) */
+        NnImage img;
+        NnRun r;
+        int live;
+        long long last; /* host clock of its last request, ns */
+    } W[NNSP_WORKERS];
     uint32_t seq;
     void *fetab[2]; /* the front end's prebuilt tables, per build (shipped, portable); built on first use */
 } G = {.port = 2};
+static void workers_stop(void);
 
 /* The build the drop-in API reproduces: the reference selects it at compile
  * time (ARM_OPTIMIZED, ambiq_nnsp_debug.h:4); here nnsp_set_arm_optimized()
@@ -134,6 +150,11 @@ static int gctx(void)
         G.lds = !ld || atoi(ld) != 0;
         const char *ka = getenv("NNSP_DROPIN_KARG");
         G.karg = !ka || atoi(ka) != 0;
+        const char *wk = getenv("NNSP_DROPIN_WORKER");
+        G.worker = !wk || atoi(wk) != 0;
+        const char *im = getenv("NNSP_DROPIN_IDLE_MS");
+        const int ms = im ? atoi(im) : 50;
+        G.idle_ns = (long long)(ms > 2 ? ms : 2) * 1000000LL;
     }
     if (!G.copy && (e = nnspk_host_alloc_mapped((void **)&G.hmap, (void **)&G.hmap_dev, G.hpin_cap))) return e;
     G.ready = 1;
@@ -171,6 +192,7 @@ static void begin(void)
     /* the previous call synchronised (fin) or failed after a sync-free
      * launch error: wait for the stream, then nothing uses the old arenas */
     if (G.n_retired) {
+        workers_stop();
         nnspk_sync(G.stream);
         for (int i = 0; i < G.n_retired; ++i) nnspk_free(G.retired[i]);
         G.n_retired = 0;
@@ -190,17 +212,22 @@ static void fin(void) { CK(nnspk_sync(G.stream)); }
 /* NNSP_DROPIN_WAIT=2: spin until the kernel's completion word holds seq; the
  * stream is queried now and then, so that a failed launch is reported (and a
  * completed stream without the word is an error) instead of spinning for ever */
-static void wait_word(volatile uint32_t *w, uint32_t seq)
+static int wait_word_on(volatile uint32_t *w, uint32_t seq, void *stream)
 {
     for (unsigned i = 1;; ++i) {
         if (*w == seq) break;
         if ((i & 255) == 0) {
-            const int d = nnspk_stream_done(G.stream);
+            const int d = nnspk_stream_done(stream);
             if (d < 0) CK(-d);
-            if (d > 0 && *w != seq) fail(NNSP_EINVAL, "NNSPClass_exec: the completion word");
+            if (d > 0 && *w != seq) return 1;
         }
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    return 0;
+}
+static void wait_word(volatile uint32_t *w, uint32_t seq)
+{
+    if (wait_word_on(w, seq, G.stream)) fail(NNSP_EINVAL, "NNSPClass_exec: the completion word");
 }
 
 /* ---------------------------------------------------------------------------
@@ -273,6 +300,7 @@ static img_node *img_add(const void *k0, const void *k1, const void *k2, const v
         last = n;
     }
     if (count >= IMG_MAX && last) { /* evict the least recently used (nothing in flight uses it) */
+        workers_stop();
         const int se = nnspk_sync(G.stream);
         if (se) {
             free(blob);
@@ -380,6 +408,7 @@ static img_node *net_image(const NeuralNetClass *net)
     img_node *n = img_find(net, NULL, NULL, NULL, ik, 0);
     if (n && tables_equal(n->blob, n->blob_n, L, nl)) return n;
     if (n) { /* tables changed in place: this image is stale */
+        workers_stop();
         CK(nnspk_sync(G.stream));
         g_imgs = n->next; /* img_find moved it to the front */
         nnsp_image_free(&n->im);
@@ -969,6 +998,72 @@ static long long host_ns(void)
     return (long long)ts.tv_sec * 1000000000LL + ts.tv_nsec;
 }
 
+/* The resident workers' mailboxes: 64 bytes each below the probe area of the
+ * mapped staging; word 0 the request's sequence number, word 1 stop. */
+static size_t mbox_off(int k) { return G.hpin_cap - 16 - NNSP_PROBE_BYTES - 64 * (size_t)(k + 1); }
+
+static void worker_stop(int k)
+{
+    struct dropin_worker *w = &G.W[k];
+    if (!w->live) return;
+    __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)) + 1, 1u, __ATOMIC_RELEASE);
+    w->live = 0;
+    CK(nnspk_sync(w->stream));
+}
+static void workers_stop(void)
+{
+    for (int k = 0; k < NNSP_WORKERS; ++k) worker_stop(k);
+}
+/* at exit: every live worker told to leave (its idle limit would end it too) */
+static void workers_atexit(void)
+{
+    for (int k = 0; k < NNSP_WORKERS; ++k)
+        if (G.W[k].live) __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)) + 1, 1u, __ATOMIC_RELEASE);
+}
+
+/* the call (inputs staged, completion word cleared) to the live worker with
+ * these arguments, or to a worker launched for them; returns its slot */
+static int worker_post(const FeArgs *a, const NnImage *img, const NnRun *r)
+{
+    static int registered;
+    NnRun rc = *r;
+    rc.done_seq = 0;
+    const long long now = host_ns();
+    int k = -1, pick = 0;
+    for (int i = 0; i < NNSP_WORKERS; ++i) {
+        const struct dropin_worker *w = &G.W[i];
+        if (w->live && !memcmp(&w->a, a, sizeof *a) && !memcmp(&w->img, img, sizeof *img) &&
+            !memcmp(&w->r, &rc, sizeof rc)) {
+            k = i;
+            break;
+        }
+        const struct dropin_worker *p = &G.W[pick];
+        if (p->live && (!w->live || w->last < p->last)) pick = i;   /* a free slot, else the least recent */
+    }
+    /* (a worker idle for half its limit may be leaving: replaced, not posted to) */
+    if (k >= 0 && now - G.W[k].last < G.idle_ns / 2) {
+        G.W[k].last = now;
+        __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)), (uint32_t)r->done_seq, __ATOMIC_RELEASE);
+        return k;
+    }
+    if (k < 0) k = pick;
+    worker_stop(k);
+    struct dropin_worker *w = &G.W[k];
+    if (!w->stream) CK(nnspk_stream_create(&w->stream));
+    uint32_t *mb = (uint32_t *)(G.hmap + mbox_off(k));
+    mb[1] = 0;
+    __atomic_store_n(mb, (uint32_t)r->done_seq, __ATOMIC_RELEASE);
+    CK(nnspk_launch_dropin_worker(a, img, r, (const uint32_t *)(G.hmap_dev + mbox_off(k)), (uint32_t)r->done_seq,
+                                  G.idle_ns / 10, w->stream));
+    w->a = *a;
+    w->img = *img;
+    w->r = rc;
+    w->live = 1;
+    w->last = now;
+    if (!registered) registered = atexit(workers_atexit) == 0;
+    return k;
+}
+
 static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-127 */
 {
     FeatureClass *fe = (FeatureClass *)pt_inst->pt_feat;
@@ -997,7 +1092,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
      * equal the new sequence number by chance (a stale read, no wait) */
     /* (and below it NNSP_PROBE_BYTES of development probes, NNSP_DROPIN_PROBE) */
     const size_t total = al16(o_trig + 2), o_done = G.hpin_cap - 16, o_probe = o_done - NNSP_PROBE_BYTES;
-    if (total > o_probe) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
+    if (total > mbox_off(NNSP_WORKERS - 1)) fail(NNSP_EUNSUPPORTED, "NNSPClass_exec: staging");
     uint8_t *hp = G.copy ? G.hpin : G.hmap;
     memcpy(hp + o_pcm, rawPCM, 320);
     memcpy(hp + o_tail, fe->state_stftModule.dataBuffer + 160, 640);
@@ -1069,14 +1164,25 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         if (G.probe) r.probe = (long long *)(G.hmap_dev + o_probe);
         if (G.lds) r.st_bytes = (int32_t)total;
     }
+    int wk = -1;   /* the resident worker serving the call */
     if (G.copy) {
         CK(nnspk_launch_nn(&img, &r, G.stream));
         CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
+    } else if (G.worker && G.lds && G.wait == 2 && !G.probe && nnspk_dropin_worker_ok(&img, &r)) {
+        wk = worker_post(&a, &img, &r);
     } else {   /* the front end and the NN in one launch */
         CK(nnspk_launch_dropin(&a, &img, &r, G.lds && G.karg ? hp : NULL, G.stream));
     }
     if (G.probe) hc[3] = host_ns();
-    if (!G.copy && G.wait == 2)
+    if (wk >= 0) {
+        /* a worker that left before it saw the request (its idle limit): the
+         * call in one launch instead, from the same staging */
+        if (wait_word_on((volatile uint32_t *)(G.hmap + o_done), (uint32_t)r.done_seq, G.W[wk].stream)) {
+            G.W[wk].live = 0;
+            CK(nnspk_launch_dropin(&a, &img, &r, G.karg ? hp : NULL, G.stream));
+            wait_word((volatile uint32_t *)(G.hmap + o_done), (uint32_t)r.done_seq);
+        }
+    } else if (!G.copy && G.wait == 2)
         wait_word((volatile uint32_t *)(G.hmap + o_done), (uint32_t)r.done_seq);
     else if (!G.copy && G.wait == 1)
         CK(nnspk_stream_spin(G.stream));

@@ -276,6 +276,16 @@ int nnspk_launch_nn(const NnImage *img, const NnRun *r, void *stream);
  * kernel arguments when they fit NNSP_DROPIN_KARG_BYTES (the LDS path only) */
 #define NNSP_DROPIN_KARG_BYTES 2176
 int nnspk_launch_dropin(const FeArgs *a, const NnImage *img, const NnRun *r, const void *kin, void *stream);
+/* the resident drop-in worker: one workgroup that serves every later call with
+ * these same arguments (r->done_seq aside) from its LDS, one request per
+ * sequence number the host writes to mbox[0] (device address of mapped host
+ * memory) after staging the call's inputs; seq0: the first request's, posted
+ * before the launch.  It leaves when mbox[1] != 0 or after idle_ticks (100 MHz)
+ * without a request.  Its stream is its own until then.
+ * nnspk_dropin_worker_ok: 1 when the call runs out of LDS (the worker's form). */
+int nnspk_dropin_worker_ok(const NnImage *img, const NnRun *r);
+int nnspk_launch_dropin_worker(const FeArgs *a, const NnImage *img, const NnRun *r, const uint32_t *mbox,
+                               uint32_t seq0, long long idle_ticks, void *stream);
 int nnspk_launch_ctx_roll(int16_t *prev5, const int16_t *feats, int S, int T, const int32_t *list,
                           int n_list, const int32_t *seg_begin, int seg_len, void *stream);
 int nnspk_launch_tail_roll(int16_t *tail, const int16_t *pcm, int S, int T, const int32_t *list,

@@ -1571,6 +1571,90 @@ template <>
 struct DropinKin<true> {
     int4 b[NNSP_DROPIN_KARG_BYTES / 16];
 };
+// one drop-in call out of LDS (ST): dropin_kernel's body, and the resident
+// worker's per request.  stage: the waves without a frame also copy the
+// constants and A fragments into LDS (a worker's later requests find them
+// there); seq: the completion word's value
+template <bool PORT, bool KI, bool ALLST>
+__device__ __forceinline__ void di_call(const FeArgs& a, const NnImage& img, const NnRun& r, const DropinKin<KI>& kin,
+                                        bool stage, int32_t seq) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t di_lds[];
+    // (r.st_base == a.in_dst: reading a's fields here as well made the
+    // compiler keep a copy of FeArgs in scratch)
+    const uint8_t* const dbase = reinterpret_cast<const uint8_t*>(r.st_base);
+    // a pointer into the device staging buffer -> the same byte of the image
+    auto rb = [&](const void* p) -> uint8_t* { return di_lds + (reinterpret_cast<const uint8_t*>(p) - dbase); };
+    // LDS: image [0, st_bytes) | wsum | wsum_r [st_rows] int32 | bias [st_rows] int16 |
+    // the activation table (384 int16) | the LSTM's per-wave scratch (2 x 64 int32) | A fragments
+    const int ob = r.st_bytes, ow = ob + 4 * r.st_rows, oz = ow + 4 * r.st_rows, ot = oz + 2 * r.st_rows,
+              osc = ot + 768, oa = osc + NN_WAVES_MAX * 512;
+    if constexpr (KI)
+        fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds, kin.b);
+    else
+        fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
+    if (stage && threadIdx.x >= 64) {   // the waves without a frame: constants and fragments to LDS
+        {   // every line of the kernel arguments into the scalar cache (invalidated at
+            // each launch), a few lines per wave, ahead of the NN's dependent reads
+            typedef const uint32_t __attribute__((address_space(4))) * kptr;
+            const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+            constexpr int NL = (int)((sizeof(FeArgs) + sizeof(NnImage) + sizeof(NnRun) + 127) / 64);
+            const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 1;
+            uint32_t x = 0;
+            for (int k = w; k < NL; k += NN_WAVES_MAX - 1) x ^= ka[16 * k];
+            asm volatile("" ::"s"(x));
+        }
+        // every segment's first share in flight together (one round trip
+        // for ~56 KB), the rest (nets wider than the reference's) after
+        constexpr int NT = 64 * (NN_WAVES_MAX - 1), U = 16;
+        const int t = (int)threadIdx.x - 64;
+        const int nw = r.st_rows / 4, nz = r.st_rows / 8, na = r.st_abytes / 16;
+        int4* dw = reinterpret_cast<int4*>(di_lds + ob);
+        int4* dr = reinterpret_cast<int4*>(di_lds + ow);
+        int4* dz = reinterpret_cast<int4*>(di_lds + oz);
+        int4* da = reinterpret_cast<int4*>(di_lds + oa);
+        const int4* sw = reinterpret_cast<const int4*>(img.wsum);
+        const int4* sr = reinterpret_cast<const int4*>(img.wsum_r);
+        const int4* sz = reinterpret_cast<const int4*>(img.bias);
+        const int4* sa = reinterpret_cast<const int4*>(img.A + r.st_alo);
+        // (clamped indexes: every load unconditional, into registers;
+        // rows >= 16 and the image's A >= 1 KiB, so index 0 exists)
+        const int4 cw = sw[min(t, nw - 1)], cr = sr[min(t, nw - 1)], cz = sz[min(t, nz - 1)];
+        const int16_t ct = nnsp_tbl_tanh[min(t, 383)];
+        int4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = sa[min(t + NT * u, max(na - 1, 0))];
+        if (t < nw) {
+            dw[t] = cw;
+            dr[t] = cr;
+        }
+        if (t < nz) dz[t] = cz;
+        if (t < 384) reinterpret_cast<int16_t*>(di_lds + ot)[t] = ct;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t + NT * u < na) da[t + NT * u] = v[u];
+        lds_fill<U, NT>(dw, sw, nw, NT + t);
+        lds_fill<U, NT>(dr, sr, nw, NT + t);
+        lds_fill<U, NT>(dz, sz, nz, NT + t);
+        lds_fill<U, NT>(da, sa, na, NT * U + t);
+        if (NNSP_PROBES && r.probe) DI_CLK_T(12, 64);
+    }
+    __syncthreads();
+    DI_CLK(1);
+    NnRun q = r;
+    q.done_seq = seq;
+    q.feats = reinterpret_cast<const int16_t*>(rb(r.feats));
+    q.prev5 = reinterpret_cast<const int16_t*>(rb(r.prev5));
+    q.h = reinterpret_cast<int16_t*>(rb(r.h));
+    q.c = reinterpret_cast<int32_t*>(rb(r.c));
+    q.post = rb(r.post);
+    q.trig = reinterpret_cast<int16_t*>(rb(r.trig));
+    q.out_src = rb(r.out_src);
+    // (32-bit LDS addresses: NnImage.A offset st_alo lands on the copy's first byte)
+    nn_body<true, ALLST>(img, q, reinterpret_cast<const int32_t*>(di_lds + ob), reinterpret_cast<const int32_t*>(di_lds + ow),
+                  reinterpret_cast<const int16_t*>(di_lds + oz), di_lds + oa - r.st_alo,
+                  reinterpret_cast<const int16_t*>(di_lds + ot), reinterpret_cast<int32_t*>(di_lds + osc));
+}
+
 template <bool PORT, bool ST, bool KI = false, bool ALLST = false>
 __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnImage img, NnRun r, DropinKin<KI> kin) {
 #if NNSP_PROBES
@@ -1586,80 +1670,49 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnI
         DI_CLK(1);
         nn_body<false>(img, r, img.wsum, img.wsum_r, img.bias, nullptr);
     } else {
-        extern __shared__ __attribute__((aligned(16))) uint8_t di_lds[];
-        // (r.st_base == a.in_dst: reading a's fields here as well made the
-        // compiler keep a copy of FeArgs in scratch)
-        const uint8_t* const dbase = reinterpret_cast<const uint8_t*>(r.st_base);
-        // a pointer into the device staging buffer -> the same byte of the image
-        auto rb = [&](const void* p) -> uint8_t* { return di_lds + (reinterpret_cast<const uint8_t*>(p) - dbase); };
-        // LDS: image [0, st_bytes) | wsum | wsum_r [st_rows] int32 | bias [st_rows] int16 |
-        // the activation table (384 int16) | the LSTM's per-wave scratch (2 x 64 int32) | A fragments
-        const int ob = r.st_bytes, ow = ob + 4 * r.st_rows, oz = ow + 4 * r.st_rows, ot = oz + 2 * r.st_rows,
-                  osc = ot + 768, oa = osc + NN_WAVES_MAX * 512;
-        if constexpr (KI)
-            fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds, kin.b);
-        else
-            fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
-        if (threadIdx.x >= 64) {   // the waves without a frame: constants and fragments to LDS
-            {   // every line of the kernel arguments into the scalar cache (invalidated at
-                // each launch), a few lines per wave, ahead of the NN's dependent reads
-                typedef const uint32_t __attribute__((address_space(4))) * kptr;
-                const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
-                constexpr int NL = (int)((sizeof(FeArgs) + sizeof(NnImage) + sizeof(NnRun) + 127) / 64);
-                const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 1;
-                uint32_t x = 0;
-                for (int k = w; k < NL; k += NN_WAVES_MAX - 1) x ^= ka[16 * k];
-                asm volatile("" ::"s"(x));
+        di_call<PORT, KI, ALLST>(a, img, r, kin, true, r.done_seq);
+    }
+}
+
+// The resident drop-in worker (NNSP_DROPIN_WORKER): one workgroup that keeps a
+// net's constants and A fragments in LDS and runs one call per request posted
+// in mapped host memory, instead of one launch per call (the launch and the
+// dispatch were ~10 us of every call).  mbox[0]: the request's sequence number,
+// written by the host after the call's inputs are staged (seq0: the first
+// request's); mbox[1]: stop.  Every wave leaves when stop is set or no request
+// came for `idle` ticks of the 100 MHz clock, so the grid drains by itself.
+// The arguments are those of every request it serves (the host compares them).
+template <bool PORT, bool ALLST>
+__global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_worker_kernel(FeArgs a, NnImage img, NnRun r,
+                                                                          const uint32_t* mbox, uint32_t seq0,
+                                                                          long long idle) {
+    __shared__ uint32_t wk_seq;
+    const DropinKin<false> k0 = {0};
+    uint32_t last = seq0 - 1u;
+    for (int it = 0;; ++it) {
+        if (threadIdx.x == 0) {
+            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+            uint32_t sq = last;
+            for (;;) {   // (both words in one load: one trip across PCIe per poll)
+                const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(mbox),
+                                                               __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+                if ((uint32_t)v != last) {
+                    sq = (uint32_t)v;
+                    break;
+                }
+                if ((uint32_t)(v >> 32) != 0u) break;
+                if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > idle) break;
+                __builtin_amdgcn_s_sleep(1);
             }
-            // every segment's first share in flight together (one round trip
-            // for ~56 KB), the rest (nets wider than the reference's) after
-            constexpr int NT = 64 * (NN_WAVES_MAX - 1), U = 16;
-            const int t = (int)threadIdx.x - 64;
-            const int nw = r.st_rows / 4, nz = r.st_rows / 8, na = r.st_abytes / 16;
-            int4* dw = reinterpret_cast<int4*>(di_lds + ob);
-            int4* dr = reinterpret_cast<int4*>(di_lds + ow);
-            int4* dz = reinterpret_cast<int4*>(di_lds + oz);
-            int4* da = reinterpret_cast<int4*>(di_lds + oa);
-            const int4* sw = reinterpret_cast<const int4*>(img.wsum);
-            const int4* sr = reinterpret_cast<const int4*>(img.wsum_r);
-            const int4* sz = reinterpret_cast<const int4*>(img.bias);
-            const int4* sa = reinterpret_cast<const int4*>(img.A + r.st_alo);
-            // (clamped indexes: every load unconditional, into registers;
-            // rows >= 16 and the image's A >= 1 KiB, so index 0 exists)
-            const int4 cw = sw[min(t, nw - 1)], cr = sr[min(t, nw - 1)], cz = sz[min(t, nz - 1)];
-            const int16_t ct = nnsp_tbl_tanh[min(t, 383)];
-            int4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) v[u] = sa[min(t + NT * u, max(na - 1, 0))];
-            if (t < nw) {
-                dw[t] = cw;
-                dr[t] = cr;
-            }
-            if (t < nz) dz[t] = cz;
-            if (t < 384) reinterpret_cast<int16_t*>(di_lds + ot)[t] = ct;
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (t + NT * u < na) da[t + NT * u] = v[u];
-            lds_fill<U, NT>(dw, sw, nw, NT + t);
-            lds_fill<U, NT>(dr, sr, nw, NT + t);
-            lds_fill<U, NT>(dz, sz, nz, NT + t);
-            lds_fill<U, NT>(da, sa, na, NT * U + t);
-            if (NNSP_PROBES && r.probe) DI_CLK_T(12, 64);
+            wk_seq = sq;
         }
         __syncthreads();
-        DI_CLK(1);
-        NnRun q = r;
-        q.feats = reinterpret_cast<const int16_t*>(rb(r.feats));
-        q.prev5 = reinterpret_cast<const int16_t*>(rb(r.prev5));
-        q.h = reinterpret_cast<int16_t*>(rb(r.h));
-        q.c = reinterpret_cast<int32_t*>(rb(r.c));
-        q.post = rb(r.post);
-        q.trig = reinterpret_cast<int16_t*>(rb(r.trig));
-        q.out_src = rb(r.out_src);
-        // (32-bit LDS addresses: NnImage.A offset st_alo lands on the copy's first byte)
-        nn_body<true, ALLST>(img, q, reinterpret_cast<const int32_t*>(di_lds + ob), reinterpret_cast<const int32_t*>(di_lds + ow),
-                      reinterpret_cast<const int16_t*>(di_lds + oz), di_lds + oa - r.st_alo,
-                      reinterpret_cast<const int16_t*>(di_lds + ot), reinterpret_cast<int32_t*>(di_lds + osc));
+        const uint32_t sq = wk_seq;
+        if (sq == last) break;   // stop, or idle: every wave leaves
+        last = sq;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // (system scope: the staged inputs)
+        di_call<PORT, false, ALLST>(a, img, r, k0, it == 0, (int32_t)sq);
+        __syncthreads();
     }
 }
 
@@ -2344,54 +2397,29 @@ int nnspk_launch_nring_fill(int16_t* const nring[3], const int32_t* const nmean[
     return ok(hipGetLastError());
 }
 
-int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, const void* kin, void* stream) {
-    if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
-    if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
-    const DropinKin<false> k0 = {0};
-    // out of LDS when the image and every layer's constants fit beside the
-    // kernel's static LDS (a net of very many rows runs from device memory)
+// the drop-in call's LDS layout (ST): rows of epilogue constants, the bytes
+// before the A fragments, and the smallest first layer whose fragments through
+// the last layer's fit beside lds_static; 1: the image and the constants do
+// not fit (the device-memory kernel runs the call)
+static int di_rows(const NnImage* img) {
     int rows = 0;
     for (int i = 0; i < img->nl; ++i) {
         const int e = img->L[i].ep_off + 16 * img->L[i].nrt;
         rows = e > rows ? e : rows;
     }
-    // rows: multiples of 16; the tanh table; the LSTM scratch
-    const size_t fixed = (size_t)(r->st_bytes > 0 ? r->st_bytes : 0) + 10 * (size_t)rows + 768 + NN_WAVES_MAX * 512;
-    if (r->st_bytes <= 0 || fixed > 160 * 1024 - 56 * 1024) {   // (the LDS kernels' static LDS is < 56 KB)
-        if (a->port)
-            hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
-        else
-            hipLaunchKernelGGL((dropin_kernel<false, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
-        return ok(hipGetLastError());
-    }
-    // out of LDS: the image, the constants, and the A fragments of as many
-    // trailing layers as fit beside the kernel's static LDS
-    // (KI: the inputs in the kernel arguments when they fit)
+    return rows;   // (multiples of 16)
+}
+static size_t di_fixed(const NnImage* img, const NnRun* r) {   // + the tanh table, the LSTM scratch
+    return (size_t)(r->st_bytes > 0 ? r->st_bytes : 0) + 10 * (size_t)di_rows(img) + 768 + NN_WAVES_MAX * 512;
+}
+static bool di_fits(const NnImage* img, const NnRun* r) {   // (the LDS kernels' static LDS is < 56 KB)
+    return r->st_bytes > 0 && di_fixed(img, r) <= 160 * 1024 - 56 * 1024;
+}
+static int di_layout(const FeArgs* a, const NnImage* img, const NnRun* r, size_t lds_static, NnRun* rr, size_t* dyn) {
     if (!a->in_dst || !a->in_bytes || !r->out_bytes || (r->st_bytes & 15) || a->in_bytes > r->st_bytes)
         return ok(hipErrorInvalidValue);
-    // the variants: port + 2 KI (the inputs in the kernel arguments when they
-    // fit) + 4 ALLST (every layer's fragments in LDS); one static LDS size
-    static const void* const fns[8] = {
-        reinterpret_cast<const void*>(dropin_kernel<false, true, false, false>),
-        reinterpret_cast<const void*>(dropin_kernel<true, true, false, false>),
-        reinterpret_cast<const void*>(dropin_kernel<false, true, true, false>),
-        reinterpret_cast<const void*>(dropin_kernel<true, true, true, false>),
-        reinterpret_cast<const void*>(dropin_kernel<false, true, false, true>),
-        reinterpret_cast<const void*>(dropin_kernel<true, true, false, true>),
-        reinterpret_cast<const void*>(dropin_kernel<false, true, true, true>),
-        reinterpret_cast<const void*>(dropin_kernel<true, true, true, true>)};
-    static size_t lds_static[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (!lds_static[0]) {
-        hipFuncAttributes fa;
-        hipError_t e = hipFuncGetAttributes(&fa, fns[0]);
-        if (e != hipSuccess) return ok(e);
-        lds_static[0] = fa.sharedSizeBytes;
-        e = hipFuncSetAttribute(fns[0], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
-        if (e != hipSuccess) return ok(e);
-    }
-    const size_t cap = 160 * 1024 - lds_static[0];
-    if (fixed > cap) return ok(hipErrorInvalidValue);   // (checked against a bound above)
-    // the smallest first layer whose fragments through the last layer's fit
+    const size_t fixed = di_fixed(img, r), cap = 160 * 1024 - lds_static;
+    if (fixed > cap) return ok(hipErrorInvalidValue);   // (checked against a bound before)
     int first = r->nl_run;
     int64_t lo = 0, hi = 0;
     for (int f = r->nl_run - 1; f >= 0; --f) {
@@ -2412,24 +2440,65 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
         lo = l;
         hi = h;
     }
-    const int ki = kin && a->in_bytes <= NNSP_DROPIN_KARG_BYTES;
-    const int fx = (a->port ? 1 : 0) + (ki ? 2 : 0) + (first == 0 ? 4 : 0);
-    if (!lds_static[fx]) {
-        hipFuncAttributes fa;
-        hipError_t e = hipFuncGetAttributes(&fa, fns[fx]);
-        if (e != hipSuccess) return ok(e);
-        if (fa.sharedSizeBytes != lds_static[0]) return ok(hipErrorInvalidValue);
-        e = hipFuncSetAttribute(fns[fx], hipFuncAttributeMaxDynamicSharedMemorySize, (int)cap);
-        if (e != hipSuccess) return ok(e);
-        lds_static[fx] = fa.sharedSizeBytes;
+    *rr = *r;
+    rr->st_base = a->in_dst;
+    rr->st_rows = di_rows(img);
+    rr->st_first = first;
+    rr->st_alo = lo;
+    rr->st_abytes = (int32_t)(hi - lo);   // (a_off: multiples of 1 KiB)
+    *dyn = fixed + (size_t)(hi - lo);
+    return 0;
+}
+// a kernel's static LDS, and its dynamic LDS limit raised to the rest (once per kernel)
+static int di_prepare(const void* fn, size_t* lds_static) {
+    if (*lds_static) return 0;
+    hipFuncAttributes fa;
+    hipError_t e = hipFuncGetAttributes(&fa, fn);
+    if (e != hipSuccess) return ok(e);
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - (int)fa.sharedSizeBytes);
+    if (e != hipSuccess) return ok(e);
+    *lds_static = fa.sharedSizeBytes;
+    return 0;
+}
+
+int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, const void* kin, void* stream) {
+    if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1) return ok(hipErrorInvalidValue);
+    if (img->n_lstm && r->hs < 8) return ok(hipErrorInvalidValue);
+    const DropinKin<false> k0 = {0};
+    // out of LDS when the image and every layer's constants fit beside the
+    // kernel's static LDS (a net of very many rows runs from device memory)
+    if (!di_fits(img, r)) {
+        if (a->port)
+            hipLaunchKernelGGL((dropin_kernel<true, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
+        else
+            hipLaunchKernelGGL((dropin_kernel<false, false>), dim3(1), dim3(64 * NN_WAVES_MAX), 0, (hipStream_t)stream, *a, *img, *r, k0);
+        return ok(hipGetLastError());
     }
-    NnRun rr = *r;
-    rr.st_base = a->in_dst;
-    rr.st_rows = rows;
-    rr.st_first = first;
-    rr.st_alo = lo;
-    rr.st_abytes = (int32_t)(hi - lo);   // (a_off: multiples of 1 KiB)
-    const size_t dyn = fixed + (size_t)(hi - lo);
+    // out of LDS: the image, the constants, and the A fragments of as many
+    // trailing layers as fit beside the kernel's static LDS.  The variants:
+    // port + 2 KI (the inputs in the kernel arguments when they fit) + 4 ALLST
+    // (every layer's fragments in LDS); one static LDS size
+    static const void* const fns[8] = {
+        reinterpret_cast<const void*>(dropin_kernel<false, true, false, false>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, false, false>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, true, false>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, true, false>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, false, true>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, false, true>),
+        reinterpret_cast<const void*>(dropin_kernel<false, true, true, true>),
+        reinterpret_cast<const void*>(dropin_kernel<true, true, true, true>)};
+    static size_t lds_static[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int e = di_prepare(fns[0], &lds_static[0]);
+    if (e) return e;
+    NnRun rr;
+    size_t dyn = 0;
+    e = di_layout(a, img, r, lds_static[0], &rr, &dyn);
+    if (e) return e;
+    const int ki = kin && a->in_bytes <= NNSP_DROPIN_KARG_BYTES;
+    const int fx = (a->port ? 1 : 0) + (ki ? 2 : 0) + (rr.st_first == 0 ? 4 : 0);
+    e = di_prepare(fns[fx], &lds_static[fx]);
+    if (e) return e;
+    if (lds_static[fx] != lds_static[0]) return ok(hipErrorInvalidValue);
 #define NNSP_DI_LAUNCH(P, K, AL, KARG)                                                                              \
     hipLaunchKernelGGL((dropin_kernel<P, true, K, AL>), dim3(1), dim3(64 * NN_WAVES_MAX), dyn, (hipStream_t)stream, \
                        *a, *img, rr, KARG)
@@ -2451,6 +2520,39 @@ int nnspk_launch_dropin(const FeArgs* a, const NnImage* img, const NnRun* r, con
         }
     }
 #undef NNSP_DI_LAUNCH
+    return ok(hipGetLastError());
+}
+
+int nnspk_dropin_worker_ok(const NnImage* img, const NnRun* r) { return di_fits(img, r) ? 1 : 0; }
+
+int nnspk_launch_dropin_worker(const FeArgs* a, const NnImage* img, const NnRun* r, const uint32_t* mbox,
+                               uint32_t seq0, long long idle_ticks, void* stream) {
+    if (a->S != 1 || a->T != 1 || a->mode != FE_MODE_BATCH || r->S != 1 || r->T != 1 || !mbox || idle_ticks <= 0)
+        return ok(hipErrorInvalidValue);
+    if ((img->n_lstm && r->hs < 8) || !di_fits(img, r) || !r->done) return ok(hipErrorInvalidValue);
+    static const void* const fns[4] = {reinterpret_cast<const void*>(dropin_worker_kernel<false, false>),
+                                       reinterpret_cast<const void*>(dropin_worker_kernel<true, false>),
+                                       reinterpret_cast<const void*>(dropin_worker_kernel<false, true>),
+                                       reinterpret_cast<const void*>(dropin_worker_kernel<true, true>)};
+    static size_t lds_static[4] = {0, 0, 0, 0};
+    int e = di_prepare(fns[0], &lds_static[0]);
+    if (e) return e;
+    NnRun rr;
+    size_t dyn = 0;
+    e = di_layout(a, img, r, lds_static[0], &rr, &dyn);
+    if (e) return e;
+    const int fx = (a->port ? 1 : 0) + (rr.st_first == 0 ? 2 : 0);
+    e = di_prepare(fns[fx], &lds_static[fx]);
+    if (e) return e;
+    if (lds_static[fx] != lds_static[0]) return ok(hipErrorInvalidValue);
+    const dim3 g(1), b(64 * NN_WAVES_MAX);
+    const hipStream_t s = (hipStream_t)stream;
+    switch (fx) {
+    case 0: hipLaunchKernelGGL((dropin_worker_kernel<false, false>), g, b, dyn, s, *a, *img, rr, mbox, seq0, idle_ticks); break;
+    case 1: hipLaunchKernelGGL((dropin_worker_kernel<true, false>), g, b, dyn, s, *a, *img, rr, mbox, seq0, idle_ticks); break;
+    case 2: hipLaunchKernelGGL((dropin_worker_kernel<false, true>), g, b, dyn, s, *a, *img, rr, mbox, seq0, idle_ticks); break;
+    default: hipLaunchKernelGGL((dropin_worker_kernel<true, true>), g, b, dyn, s, *a, *img, rr, mbox, seq0, idle_ticks); break;
+    }
     return ok(hipGetLastError());
 }
 

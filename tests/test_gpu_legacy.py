@@ -213,7 +213,14 @@ def test_nnsp_exec_interleaved_nets():
     """NNSPClass_exec on VAD, KWS and S2I instances in turn, frame by frame
     (ADVICE r5): the three nets' staging layouts differ in size, and the
     drop-in completion word must not be satisfied by another net's bytes left
-    from the call before.  Every call is compared with that net's oracle."""
+    from the call before.  Every call is compared with that net's oracle.
+    (With the resident workers, the default: three of them live at once.)"""
+    _interleaved(0.0)
+
+
+def _interleaved(pause):
+    """test_nnsp_exec_interleaved_nets, pause seconds before every call"""
+    import time
     nets = []
     for k, name in enumerate(("s2i", "vad", "kws")):
         data = synth_net(name, 30 + k)
@@ -235,6 +242,8 @@ def test_nnsp_exec_interleaved_nets():
         for k in (2, 0, 1) if t % 2 else (1, 2, 0):   # large and small staging layouts alternate
             name, _, inst, feat = nets[k]
             frame = np.ascontiguousarray(pcm[k, t])
+            if pause:
+                time.sleep(pause)
             trig = L().NNSPClass_exec(C.byref(inst), vp(frame))
             assert trig == ref[k][0][0, t], f"{name} frame {t}"
             ctx5 = np.ctypeslib.as_array(feat.normFeatContext)[200:240]
@@ -305,3 +314,29 @@ def test_nnsp_exec_memory_path():
     out = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True, text=True,
                          timeout=240)
     assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout[-2000:] + out.stderr[-4000:]
+
+
+def _child(code, **env_add):
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = "import sys; import torch; sys.path[:0] = ['oracle', '.', 'tests']\nimport test_gpu_legacy as t\n" + code
+    out = subprocess.run([sys.executable, "-c", code + "\nprint('ok')\n"], cwd=root, env=dict(os.environ, **env_add),
+                         capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0 and out.stdout.strip().endswith("ok"), out.stdout[-2000:] + out.stderr[-4000:]
+
+
+def test_nnsp_exec_one_launch_per_call():
+    """The drop-in call as one launch each (NNSP_DROPIN_WORKER=0, the
+    resident workers off; a child process) against the oracle."""
+    _child("t.test_nnsp_exec_interleaved_nets()\nfor n in ('odd', 'lstm3'): t.test_nnsp_exec_generic_nets(n)",
+           NNSP_DROPIN_WORKER="0")
+
+
+def test_nnsp_exec_worker_idle_expiry():
+    """Resident workers that leave after 2 ms without a request
+    (NNSP_DROPIN_IDLE_MS=2) and calls 3 ms apart: every call finds its worker
+    expired or leaving, and is relaunched or run in one launch -- results as
+    the oracle's."""
+    _child("t._interleaved(0.003)", NNSP_DROPIN_IDLE_MS="2")
