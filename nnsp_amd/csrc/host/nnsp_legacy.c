@@ -1168,7 +1168,7 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     if (G.copy) {
         CK(nnspk_launch_nn(&img, &r, G.stream));
         CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
-    } else if (G.worker && G.lds && G.wait == 2 && !G.probe && nnspk_dropin_worker_ok(&img, &r)) {
+    } else if (G.worker && G.lds && G.wait == 2 && nnspk_dropin_worker_ok(&img, &r)) {
         wk = worker_post(&a, &img, &r);
     } else {   /* the front end and the NN in one launch */
         CK(nnspk_launch_dropin(&a, &img, &r, G.lds && G.karg ? hp : NULL, G.stream));

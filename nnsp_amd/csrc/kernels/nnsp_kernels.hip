@@ -1571,13 +1571,66 @@ template <>
 struct DropinKin<true> {
     int4 b[NNSP_DROPIN_KARG_BYTES / 16];
 };
+// the waves without a frame (threadIdx.x >= 64): the epilogue constants, the
+// activation table and the A fragments of layers st_first.. into the drop-in
+// call's LDS (layout in di_call)
+__device__ __forceinline__ void di_stage(const NnImage& img, const NnRun& r) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t di_lds[];
+    const int ob = r.st_bytes, ow = ob + 4 * r.st_rows, oz = ow + 4 * r.st_rows, ot = oz + 2 * r.st_rows,
+              osc = ot + 768, oa = osc + NN_WAVES_MAX * 512;
+    {   // every line of the kernel arguments into the scalar cache (invalidated at
+        // each launch), a few lines per wave, ahead of the NN's dependent reads
+        typedef const uint32_t __attribute__((address_space(4))) * kptr;
+        const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+        constexpr int NL = (int)((sizeof(FeArgs) + sizeof(NnImage) + sizeof(NnRun) + 127) / 64);
+        const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 1;
+        uint32_t x = 0;
+        for (int k = w; k < NL; k += NN_WAVES_MAX - 1) x ^= ka[16 * k];
+        asm volatile("" ::"s"(x));
+    }
+    // every segment's first share in flight together (one round trip
+    // for ~56 KB), the rest (nets wider than the reference's) after
+    constexpr int NT = 64 * (NN_WAVES_MAX - 1), U = 16;
+    const int t = (int)threadIdx.x - 64;
+    const int nw = r.st_rows / 4, nz = r.st_rows / 8, na = r.st_abytes / 16;
+    int4* dw = reinterpret_cast<int4*>(di_lds + ob);
+    int4* dr = reinterpret_cast<int4*>(di_lds + ow);
+    int4* dz = reinterpret_cast<int4*>(di_lds + oz);
+    int4* da = reinterpret_cast<int4*>(di_lds + oa);
+    const int4* sw = reinterpret_cast<const int4*>(img.wsum);
+    const int4* sr = reinterpret_cast<const int4*>(img.wsum_r);
+    const int4* sz = reinterpret_cast<const int4*>(img.bias);
+    const int4* sa = reinterpret_cast<const int4*>(img.A + r.st_alo);
+    // (clamped indexes: every load unconditional, into registers;
+    // rows >= 16 and the image's A >= 1 KiB, so index 0 exists)
+    const int4 cw = sw[min(t, nw - 1)], cr = sr[min(t, nw - 1)], cz = sz[min(t, nz - 1)];
+    const int16_t ct = nnsp_tbl_tanh[min(t, 383)];
+    int4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = sa[min(t + NT * u, max(na - 1, 0))];
+    if (t < nw) {
+        dw[t] = cw;
+        dr[t] = cr;
+    }
+    if (t < nz) dz[t] = cz;
+    if (t < 384) reinterpret_cast<int16_t*>(di_lds + ot)[t] = ct;
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+        if (t + NT * u < na) da[t + NT * u] = v[u];
+    lds_fill<U, NT>(dw, sw, nw, NT + t);
+    lds_fill<U, NT>(dr, sr, nw, NT + t);
+    lds_fill<U, NT>(dz, sz, nz, NT + t);
+    lds_fill<U, NT>(da, sa, na, NT * U + t);
+    if (NNSP_PROBES && r.probe) DI_CLK_T(12, 64);
+}
+
 // one drop-in call out of LDS (ST): dropin_kernel's body, and the resident
-// worker's per request.  stage: the waves without a frame also copy the
-// constants and A fragments into LDS (a worker's later requests find them
-// there); seq: the completion word's value
-template <bool PORT, bool KI, bool ALLST>
+// worker's per request.  STAGE: the waves without a frame also stage the
+// constants and A fragments (the worker stages them once, before its first
+// request); seq: the completion word's value
+template <bool PORT, bool KI, bool ALLST, bool STAGE>
 __device__ __forceinline__ void di_call(const FeArgs& a, const NnImage& img, const NnRun& r, const DropinKin<KI>& kin,
-                                        bool stage, int32_t seq) {
+                                        int32_t seq) {
     extern __shared__ __attribute__((aligned(16))) uint8_t di_lds[];
     // (r.st_base == a.in_dst: reading a's fields here as well made the
     // compiler keep a copy of FeArgs in scratch)
@@ -1592,52 +1645,7 @@ __device__ __forceinline__ void di_call(const FeArgs& a, const NnImage& img, con
         fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds, kin.b);
     else
         fe_body<FE_MODE_BATCH, PORT, 1, true>(a, di_lds);
-    if (stage && threadIdx.x >= 64) {   // the waves without a frame: constants and fragments to LDS
-        {   // every line of the kernel arguments into the scalar cache (invalidated at
-            // each launch), a few lines per wave, ahead of the NN's dependent reads
-            typedef const uint32_t __attribute__((address_space(4))) * kptr;
-            const kptr ka = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
-            constexpr int NL = (int)((sizeof(FeArgs) + sizeof(NnImage) + sizeof(NnRun) + 127) / 64);
-            const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) - 1;
-            uint32_t x = 0;
-            for (int k = w; k < NL; k += NN_WAVES_MAX - 1) x ^= ka[16 * k];
-            asm volatile("" ::"s"(x));
-        }
-        // every segment's first share in flight together (one round trip
-        // for ~56 KB), the rest (nets wider than the reference's) after
-        constexpr int NT = 64 * (NN_WAVES_MAX - 1), U = 16;
-        const int t = (int)threadIdx.x - 64;
-        const int nw = r.st_rows / 4, nz = r.st_rows / 8, na = r.st_abytes / 16;
-        int4* dw = reinterpret_cast<int4*>(di_lds + ob);
-        int4* dr = reinterpret_cast<int4*>(di_lds + ow);
-        int4* dz = reinterpret_cast<int4*>(di_lds + oz);
-        int4* da = reinterpret_cast<int4*>(di_lds + oa);
-        const int4* sw = reinterpret_cast<const int4*>(img.wsum);
-        const int4* sr = reinterpret_cast<const int4*>(img.wsum_r);
-        const int4* sz = reinterpret_cast<const int4*>(img.bias);
-        const int4* sa = reinterpret_cast<const int4*>(img.A + r.st_alo);
-        // (clamped indexes: every load unconditional, into registers;
-        // rows >= 16 and the image's A >= 1 KiB, so index 0 exists)
-        const int4 cw = sw[min(t, nw - 1)], cr = sr[min(t, nw - 1)], cz = sz[min(t, nz - 1)];
-        const int16_t ct = nnsp_tbl_tanh[min(t, 383)];
-        int4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) v[u] = sa[min(t + NT * u, max(na - 1, 0))];
-        if (t < nw) {
-            dw[t] = cw;
-            dr[t] = cr;
-        }
-        if (t < nz) dz[t] = cz;
-        if (t < 384) reinterpret_cast<int16_t*>(di_lds + ot)[t] = ct;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (t + NT * u < na) da[t + NT * u] = v[u];
-        lds_fill<U, NT>(dw, sw, nw, NT + t);
-        lds_fill<U, NT>(dr, sr, nw, NT + t);
-        lds_fill<U, NT>(dz, sz, nz, NT + t);
-        lds_fill<U, NT>(da, sa, na, NT * U + t);
-        if (NNSP_PROBES && r.probe) DI_CLK_T(12, 64);
-    }
+    if (STAGE && threadIdx.x >= 64) di_stage(img, r);   // the waves without a frame: constants and fragments to LDS
     __syncthreads();
     DI_CLK(1);
     NnRun q = r;
@@ -1670,7 +1678,7 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_kernel(FeArgs a, NnI
         DI_CLK(1);
         nn_body<false>(img, r, img.wsum, img.wsum_r, img.bias, nullptr);
     } else {
-        di_call<PORT, KI, ALLST>(a, img, r, kin, true, r.done_seq);
+        di_call<PORT, KI, ALLST, true>(a, img, r, kin, r.done_seq);
     }
 }
 
@@ -1689,7 +1697,8 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_worker_kernel(FeArgs
     __shared__ uint32_t wk_seq;
     const DropinKin<false> k0 = {0};
     uint32_t last = seq0 - 1u;
-    for (int it = 0;; ++it) {
+    if (threadIdx.x >= 64) di_stage(img, r);   // (wave 0 meanwhile waits for the first request)
+    for (;;) {
         if (threadIdx.x == 0) {
             const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
             uint32_t sq = last;
@@ -1711,7 +1720,11 @@ __global__ __launch_bounds__(64 * NN_WAVES_MAX) void dropin_worker_kernel(FeArgs
         if (sq == last) break;   // stop, or idle: every wave leaves
         last = sq;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");   // (system scope: the staged inputs)
-        di_call<PORT, false, ALLST>(a, img, r, k0, it == 0, (int32_t)sq);
+#if NNSP_PROBES
+        if (r.probe && threadIdx.x < NNSP_PROBE_LONGS) di_clk[threadIdx.x] = 0;
+#endif
+        DI_CLK(0);
+        di_call<PORT, false, ALLST, false>(a, img, r, k0, (int32_t)sq);
         __syncthreads();
     }
 }
