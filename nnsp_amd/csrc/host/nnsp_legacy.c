@@ -383,8 +383,12 @@ static void tables_copy(uint8_t *blob, const nnsp_layer_desc *L, int nl)
  * bytes are compared with the copy the image was built from (memcmp: the
  * reference reads its tables on every call, so tables rewritten in place get
  * a new image -- a byte-wise hash of them was ~30 % of a drop-in S2I frame) */
-static img_node *net_image(const NeuralNetClass *net)
+/* check 0: a cached image without the comparison of the tables' bytes (*fresh
+ * 0; NNSPClass_exec compares them while the call runs, net_tables_match), 1 when
+ * built here */
+static img_node *net_image_ex(const NeuralNetClass *net, int check, int *fresh)
 {
+    if (fresh) *fresh = 0;
     uint64_t h = 1469598103934665603ULL;
 #define MIX(v)                                   \
     do {                                         \
@@ -406,7 +410,7 @@ static img_node *net_image(const NeuralNetClass *net)
     for (int i = 0; i < nl; ++i) L[i].portable = port_on();
     const int ik[8] = {(int)(h & 0xffffffffu), (int)(h >> 32), net->numlayers, 0, 0, 0, 0, 0};
     img_node *n = img_find(net, NULL, NULL, NULL, ik, 0);
-    if (n && tables_equal(n->blob, n->blob_n, L, nl)) return n;
+    if (n && (!check || tables_equal(n->blob, n->blob_n, L, nl))) return n;
     if (n) { /* tables changed in place: this image is stale */
         workers_stop();
         CK(nnspk_sync(G.stream));
@@ -419,7 +423,17 @@ static img_node *net_image(const NeuralNetClass *net)
     uint8_t *blob = (uint8_t *)malloc(nb ? nb : 1);
     if (!blob) fail(NNSP_ENOMEM, "image cache tables copy");
     tables_copy(blob, L, nl);
+    if (fresh) *fresh = 1;
     return img_add(net, NULL, NULL, NULL, ik, 0, L, nl, lin, blob, nb);
+}
+static img_node *net_image(const NeuralNetClass *net) { return net_image_ex(net, 1, NULL); }
+/* the net's tables still hold the bytes image n was built from */
+static int net_tables_match(const NeuralNetClass *net, const img_node *n)
+{
+    nnsp_layer_desc L[NN_MAX_LAYERS];
+    int nl = 0, lin = 0;
+    CK(nnsp_describe_net(net, L, &nl, &lin));
+    return tables_equal(n->blob, n->blob_n, L, nl);
 }
 
 /* LSTM h/c of a NeuralNetClass <-> device rows [l][hs] (hs: the widest
@@ -1071,7 +1085,11 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
     long long hc[5] = {0, 0, 0, 0, 0};   /* NNSP_DROPIN_PROBE: entry, image found, staged, launched, done */
     if (G.probe) hc[0] = host_ns();
     begin();
-    img_node *n = net_image(net);
+    /* the tables' bytes are compared with the image's while the call runs: a
+     * call that ran on tables since rewritten in place is run again */
+    int checked = 0;
+    img_node *n = net_image_ex(net, 0, &checked);
+restart:
     if (G.probe) hc[1] = host_ns();
     NnImage img = n->im.img;
     img.nn_id = pt_inst->nn_id;
@@ -1174,6 +1192,8 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         CK(nnspk_launch_dropin(&a, &img, &r, G.lds && G.karg ? hp : NULL, G.stream));
     }
     if (G.probe) hc[3] = host_ns();
+    const int stale = !checked && !net_tables_match(net, n);
+    checked = 1;
     if (wk >= 0) {
         /* a worker that left before it saw the request (its idle limit): the
          * call in one launch instead, from the same staging */
@@ -1188,6 +1208,10 @@ static int16_t NNSPClass_exec_impl(NNSPClass *pt_inst, int16_t *rawPCM) /* :74-1
         CK(nnspk_stream_spin(G.stream));
     else
         fin();
+    if (stale) { /* (the caller's state is untouched until here) */
+        n = net_image(net);
+        goto restart;
+    }
     memcpy(&ps, hp + o_post, sizeof ps);
     {
         int l = 0;

@@ -250,6 +250,52 @@ def _interleaved(pause):
             np.testing.assert_array_equal(ctx5, ref[k][2][0, t], err_msg=f"{name} features frame {t}")
 
 
+def test_nnsp_exec_tables_rewritten_in_place():
+    """NNSPClass_exec on tables rewritten in place mid-stream (the reference
+    reads them on every call): the library compares their bytes with the
+    device image's while the call runs, and runs again a call that ran on the
+    old ones.  Frames 0-7 on net a, then a's buffers rewritten with net b's
+    weights and frames 8-15 continue the stream: every frame, h and c equal the
+    oracle's a then b from the same carried state.  (Not after a reset: the
+    reference's FeatureClass_setDefault keeps the last context slot, so a
+    reset stream is not a fresh oracle stream.)"""
+    from nnsp_amd.nets import NetData
+    a, b0 = synth_net("kws", 51), synth_net("kws", 52)
+    b = NetData(b0.spec, b0.W, b0.Wr, b0.B, a.mean, a.stdR)   # (the feature normalisation unchanged)
+    h = _lib.NetHandle(a)
+    feat = _lib.FeatureClass()
+    inst = _lib.NNSPClass()
+    thr = np.array([3000], np.int16)
+    cnt = np.array([1], np.int16)
+    _KEEP.extend([h, feat, inst, thr, cnt])
+    assert L().NNSPClass_init(C.byref(inst), C.c_void_p(h.addr), C.byref(feat), bytes([1]), vp(h.mean), vp(h.stdR),
+                              vp(thr), vp(cnt)) == 0
+    L().NNSPClass_reset(C.byref(inst))
+    T = 16
+    pcm = synthetic_pcm(1, T, seed=57)
+    orcs = [OracleNet(d, thresh_prob=3000, th_count=1) for d in (a, b)]
+    st = orcs[0].new_states(1)
+    N = a.spec.sizes[2]   # (layer 1: the LSTM)
+    for t in range(T):
+        if t == T // 2:   # overwrite the net's buffers in place
+            Wp, Wrp, Bp = b.packed()
+            for i in range(b.spec.nl):
+                np.copyto(np.ctypeslib.as_array((C.c_int8 * len(Wp[i])).from_address(h.net.pt_kernel[i])),
+                          Wp[i].view(np.int8))
+                np.copyto(np.ctypeslib.as_array((C.c_int16 * len(Bp[i])).from_address(h.net.pt_bias[i])), Bp[i])
+                if Wrp[i] is not None:
+                    np.copyto(np.ctypeslib.as_array((C.c_int8 * len(Wrp[i])).from_address(h.net.pt_kernel_rec[i])),
+                              Wrp[i].view(np.int8))
+        o_trig, _, o_feat, st = orcs[t >= T // 2].run(pcm[:, t:t + 1], st)
+        frame = np.ascontiguousarray(pcm[0, t])
+        assert L().NNSPClass_exec(C.byref(inst), vp(frame)) == o_trig[0, 0], f"frame {t}"
+        np.testing.assert_array_equal(np.ctypeslib.as_array(feat.normFeatContext)[200:240], o_feat[0, 0])
+        oh, oc = _oracle_hc(st[0])
+        np.testing.assert_array_equal(h.h[1], oh[0, :N], err_msg=f"LSTM h, frame {t}")
+        np.testing.assert_array_equal(h.c[1], oc[0, :N], err_msg=f"LSTM c, frame {t}")
+    assert L().nnsp_legacy_status() == 0
+
+
 def _oracle_hc(row):
     """Every LSTM's h / c in the oracle's stream state (or_stream,
     oracle/nnsp_oracle.h: buf[480], ctx[240] int16, then h[10][304] int16 and
