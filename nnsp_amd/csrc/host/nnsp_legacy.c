@@ -30,6 +30,8 @@
  * uses it), and the sticky error of the last failed call
  * ------------------------------------------------------------------------- */
 #define NNSP_WORKERS 4
+#define DMB_IN 4096                                  /* G.dmb: mailboxes [0, 256), the inputs from 4 KiB */
+#define DMB_BYTES (DMB_IN + (64u << 10))
 static struct {
     void *stream;
     uint8_t *arena;
@@ -67,6 +69,11 @@ static struct {
      * NNSP_DROPIN_IDLE_MS (default 50) without a request */
     int worker;
     long long idle_ns;
+    /* the workers' mailboxes and the calls' inputs in fine-grained device
+     * memory the host writes (NNSP_DROPIN_DEVMBOX, default 1; NULL: in the
+     * mapped staging): the worker polls and reads them without a trip across
+     * PCIe (profiles/r06/devmbox/: 6.45 -> 5.35 us a round trip) */
+    uint8_t *dmb;
     struct dropin_worker {
         void *stream;
         FeArgs a;   /* the arguments it serves (r.done_seq 0) */
@@ -152,6 +159,11 @@ static int gctx(void)
         G.karg = !ka || atoi(ka) != 0;
         const char *wk = getenv("NNSP_DROPIN_WORKER");
         G.worker = !wk || atoi(wk) != 0;
+        const char *dm = getenv("NNSP_DROPIN_DEVMBOX");
+        if (!dm || atoi(dm) != 0) {
+            void *p = NULL;
+            if (!nnspk_malloc_finegrained(&p, DMB_BYTES)) G.dmb = (uint8_t *)p;
+        }
         const char *im = getenv("NNSP_DROPIN_IDLE_MS");
         const int ms = im ? atoi(im) : 50;
         G.idle_ns = (long long)(ms > 2 ? ms : 2) * 1000000LL;
@@ -1015,12 +1027,24 @@ static long long host_ns(void)
 /* The resident workers' mailboxes: 64 bytes each below the probe area of the
  * mapped staging; word 0 the request's sequence number, word 1 stop. */
 static size_t mbox_off(int k) { return G.hpin_cap - 16 - NNSP_PROBE_BYTES - 64 * (size_t)(k + 1); }
+/* worker k's mailbox: host view, device address */
+static uint32_t *mbox_host(int k) { return G.dmb ? (uint32_t *)(G.dmb + 64 * (size_t)k) : (uint32_t *)(G.hmap + mbox_off(k)); }
+static const uint32_t *mbox_dev(int k)
+{
+    return G.dmb ? (const uint32_t *)(G.dmb + 64 * (size_t)k) : (const uint32_t *)(G.hmap_dev + mbox_off(k));
+}
+/* the host's stores to G.dmb (write-combined device memory) drained, in order */
+static void dmb_fence(void)
+{
+    if (G.dmb) __builtin_ia32_sfence();
+}
 
 static void worker_stop(int k)
 {
     struct dropin_worker *w = &G.W[k];
     if (!w->live) return;
-    __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)) + 1, 1u, __ATOMIC_RELEASE);
+    __atomic_store_n(mbox_host(k) + 1, 1u, __ATOMIC_RELEASE);
+    dmb_fence();
     w->live = 0;
     CK(nnspk_sync(w->stream));
 }
@@ -1032,7 +1056,10 @@ static void workers_stop(void)
 static void workers_atexit(void)
 {
     for (int k = 0; k < NNSP_WORKERS; ++k)
-        if (G.W[k].live) __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)) + 1, 1u, __ATOMIC_RELEASE);
+        if (G.W[k].live) {
+            __atomic_store_n(mbox_host(k) + 1, 1u, __ATOMIC_RELEASE);
+            dmb_fence();
+        }
 }
 
 /* the call (inputs staged, completion word cleared) to the live worker with
@@ -1057,18 +1084,21 @@ static int worker_post(const FeArgs *a, const NnImage *img, const NnRun *r)
     /* (a worker idle for half its limit may be leaving: replaced, not posted to) */
     if (k >= 0 && now - G.W[k].last < G.idle_ns / 2) {
         G.W[k].last = now;
-        __atomic_store_n((uint32_t *)(G.hmap + mbox_off(k)), (uint32_t)r->done_seq, __ATOMIC_RELEASE);
+        dmb_fence();   /* (the inputs first) */
+        __atomic_store_n(mbox_host(k), (uint32_t)r->done_seq, __ATOMIC_RELEASE);
+        dmb_fence();
         return k;
     }
     if (k < 0) k = pick;
     worker_stop(k);
     struct dropin_worker *w = &G.W[k];
     if (!w->stream) CK(nnspk_stream_create(&w->stream));
-    uint32_t *mb = (uint32_t *)(G.hmap + mbox_off(k));
+    uint32_t *mb = mbox_host(k);
     mb[1] = 0;
+    dmb_fence();
     __atomic_store_n(mb, (uint32_t)r->done_seq, __ATOMIC_RELEASE);
-    CK(nnspk_launch_dropin_worker(a, img, r, (const uint32_t *)(G.hmap_dev + mbox_off(k)), (uint32_t)r->done_seq,
-                                  G.idle_ns / 10, w->stream));
+    dmb_fence();
+    CK(nnspk_launch_dropin_worker(a, img, r, mbox_dev(k), (uint32_t)r->done_seq, G.idle_ns / 10, w->stream));
     w->a = *a;
     w->img = *img;
     w->r = rc;
@@ -1187,7 +1217,12 @@ restart:
         CK(nnspk_launch_nn(&img, &r, G.stream));
         CK(nnspk_d2h(hp + o_post, d + o_post, total - o_post, G.stream));
     } else if (G.worker && G.lds && G.wait == 2 && nnspk_dropin_worker_ok(&img, &r)) {
-        wk = worker_post(&a, &img, &r);
+        FeArgs aw = a;
+        if (G.dmb && o_feat <= DMB_BYTES - DMB_IN) { /* the inputs where the worker reads them */
+            memcpy(G.dmb + DMB_IN, hp, o_feat);
+            aw.in_src = G.dmb + DMB_IN;
+        }
+        wk = worker_post(&aw, &img, &r);
     } else {   /* the front end and the NN in one launch */
         CK(nnspk_launch_dropin(&a, &img, &r, G.lds && G.karg ? hp : NULL, G.stream));
     }

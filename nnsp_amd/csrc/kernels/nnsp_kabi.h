@@ -328,6 +328,7 @@ int nnspk_launch_recur(const NnImage *img, const FastRun *r, int waves, const st
 int nnspk_fast_fuse_ok(int shape, int a_bytes, int ep_rows, int acc32);
 int nnspk_set_lds_limit(void);
 int nnspk_malloc(void **p, size_t n);
+int nnspk_malloc_finegrained(void **p, size_t n); /* device memory the host writes directly, zeroed */
 int nnspk_free(void *p);
 int nnspk_memset(void *p, int v, size_t n, void *stream);
 int nnspk_h2d(void *d, const void *h, size_t n, void *stream);

@@ -2688,6 +2688,14 @@ int nnspk_launch_nn_default(int16_t* h, int32_t* c, void* post, int row, const u
 // ---- thin runtime wrappers so the C host library needs no HIP headers -------
 int nnspk_malloc(void** p, size_t n) { return ok(hipMalloc(p, n ? n : 16)); }
 int nnspk_free(void* p) { return p ? ok(hipFree(p)) : 0; }
+// fine-grained device memory the host writes directly (the drop-in workers'
+// mailboxes and inputs), zeroed
+int nnspk_malloc_finegrained(void** p, size_t n) {
+    hipError_t e = hipExtMallocWithFlags(p, n, hipDeviceMallocFinegrained);
+    if (e == hipSuccess) e = hipMemset(*p, 0, n);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    return ok(e);
+}
 int nnspk_memset(void* p, int v, size_t n, void* stream) { return ok(hipMemsetAsync(p, v, n, (hipStream_t)stream)); }
 int nnspk_h2d(void* d, const void* h, size_t n, void* stream) {
     return ok(hipMemcpyAsync(d, h, n, hipMemcpyHostToDevice, (hipStream_t)stream));
